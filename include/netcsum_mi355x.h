@@ -1,0 +1,201 @@
+/*
+ * netcsum_mi355x.h — C ABI of the MI355X (gfx950) Internet-checksum path.
+ *
+ * Drop-in for µC/TCP-IP V3.06.01 Source/net_util.c's 16-bit one's-complement checksum
+ * (RFC 1071). Everything here is plain C: pointers, sizes, NET_ERR codes. No torch or HIP
+ * types cross this boundary; HIP streams are passed as `void *` (a hipStream_t, NULL = the
+ * legacy default stream of the current device).
+ *
+ * Library: uc-tcp-ip_amd/libnetcsum_mi355x.so (built by `make -C uc-tcp-ip_amd`).
+ *
+ * Three groups of entry points:
+ *
+ *  (1) The reference's four public checksum functions, SAME signatures and semantics
+ *      (Source/net_util.h:422-438). Callers in net_ipv4.c, net_icmpv4.c, net_igmp.c,
+ *      net_tcp.c, net_udp.c, net_icmpv6.c link against these unchanged (SURVEY §8(b) lists all
+ *      23 call sites). The host side walks the NET_BUF chain and the bytes are summed on the GPU.
+ *
+ *  (2) The additive batch ABI (the throughput path): N independent segments resident in HBM,
+ *      one output element per segment, results bit-identical to calling (1) once per segment
+ *      with a one-buffer NET_BUF chain.
+ *
+ *  (3) Support: the exact stream sum used by (1), the NET_BUF chain walk (host logic, exported
+ *      so it can be tested without a GPU), synthetic-input generation and a read-stream
+ *      roofline probe for the bench.
+ */
+#ifndef NETCSUM_MI355X_H
+#define NETCSUM_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "netcsum_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ============================================================================================
+ * (1) Reference signatures (Source/net_util.h:422-438, implemented in net_util.c:159-449).
+ *
+ *  NetUtil_16BitOnesCplChkSumHdrCalc      replaces Source/net_util.c:159  (decl net_util.h:422)
+ *  NetUtil_16BitOnesCplChkSumHdrVerify    replaces Source/net_util.c:245  (decl net_util.h:426)
+ *  NetUtil_16BitOnesCplChkSumDataCalc     replaces Source/net_util.c:344  (decl net_util.h:430)
+ *  NetUtil_16BitOnesCplChkSumDataVerify   replaces Source/net_util.c:428  (decl net_util.h:435)
+ *
+ * Return-value convention is the reference's: Calc returns the checksum in HOST order such that
+ * a memcpy into the header yields network byte order (net_util.c:187-188, :358); Verify returns
+ * DEF_OK/DEF_FAIL. *p_err = NET_UTIL_ERR_NONE on success; NET_UTIL_ERR_INVALID_PROTOCOL for an
+ * unknown ProtocolHdrType (net_util.c:1637-1639). With NETCSUM_ARG_CHK_DBG_EN=1 at build time the
+ * NET_ERR_CFG_ARG_CHK_DBG_EN checks of net_util.c:168-179,255-266,1566-1577,1642-1672 apply.
+ * A device failure returns 0 / DEF_FAIL with *p_err = NET_UTIL_ERR_MI355X_DEV (never a CPU path).
+ * ============================================================================================ */
+NET_CHK_SUM  NetUtil_16BitOnesCplChkSumHdrCalc   (void        *phdr,
+                                                  CPU_INT16U   hdr_size,
+                                                  NET_ERR     *p_err);
+
+CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumHdrVerify (void        *phdr,
+                                                  CPU_INT16U   hdr_size,
+                                                  NET_ERR     *p_err);
+
+NET_CHK_SUM  NetUtil_16BitOnesCplChkSumDataCalc  (void        *pdata_buf,
+                                                  void        *ppseudo_hdr,
+                                                  CPU_INT16U   pseudo_hdr_size,
+                                                  NET_ERR     *p_err);
+
+CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumDataVerify(void        *pdata_buf,
+                                                  void        *ppseudo_hdr,
+                                                  CPU_INT16U   pseudo_hdr_size,
+                                                  NET_ERR     *p_err);
+
+/* ============================================================================================
+ * (2) Batch ABI — device-resident segments.
+ *
+ * Segment i is the byte span [seg_i, seg_i + len_i) in device memory, any alignment (odd starts
+ * are fine); its optional pseudo-header is [d_pseudo + i*pseudo_stride, +pseudo_len).
+ * out[i] equals what the reference returns for ONE NET_BUF whose data area holds the segment
+ * (ProtocolHdrType TCP/UDP, TransportHdrIx -> segment start) and ppseudo_hdr -> the pseudo-header:
+ *
+ *   NETCSUM_OP_DATA_CALC    uint16_t out[i] = NetUtil_16BitOnesCplChkSumDataCalc(...)
+ *   NETCSUM_OP_DATA_VERIFY  uint8_t  out[i] = NetUtil_16BitOnesCplChkSumDataVerify(...)
+ *   NETCSUM_OP_HDR_CALC     uint16_t out[i] = NetUtil_16BitOnesCplChkSumHdrCalc(seg_i, len_i)
+ *   NETCSUM_OP_HDR_VERIFY   uint8_t  out[i] = NetUtil_16BitOnesCplChkSumHdrVerify(seg_i, len_i)
+ *
+ * (HDR ops take no pseudo-header: pass d_pseudo = NULL.) Lengths are CPU_INT16U as in the
+ * reference (net_util.c:1617,1628: per-buffer data_len is 16-bit). The call is asynchronous
+ * on `hip_stream`; returns NET_UTIL_ERR_NONE when the launch was queued.
+ * ============================================================================================ */
+typedef enum netcsum_op {
+    NETCSUM_OP_DATA_CALC   = 0,
+    NETCSUM_OP_DATA_VERIFY = 1,
+    NETCSUM_OP_HDR_CALC    = 2,
+    NETCSUM_OP_HDR_VERIFY  = 3
+} NETCSUM_OP;
+
+/* Uniform segments: seg_i = d_seg + i*seg_stride, len_i = seg_len (config C2/C3/C5). */
+NET_ERR  NetUtil_MI355X_ChkSumBatchStrided (const void  *d_seg,
+                                            uint64_t     seg_stride,
+                                            CPU_INT16U   seg_len,
+                                            const void  *d_pseudo,
+                                            uint32_t     pseudo_stride,
+                                            CPU_INT16U   pseudo_len,
+                                            uint32_t     n_seg,
+                                            void        *d_out,
+                                            NETCSUM_OP   op,
+                                            void        *hip_stream);
+
+/* Variable-length segments: seg_i = d_base + d_seg_off[i], len_i = d_seg_len[i] (config C4). */
+NET_ERR  NetUtil_MI355X_ChkSumBatchVarLen  (const void      *d_base,
+                                            const uint64_t  *d_seg_off,
+                                            const uint16_t  *d_seg_len,
+                                            const void      *d_pseudo,
+                                            uint32_t         pseudo_stride,
+                                            CPU_INT16U       pseudo_len,
+                                            uint32_t         n_seg,
+                                            void            *d_out,
+                                            NETCSUM_OP       op,
+                                            void            *hip_stream);
+
+/* Host-memory variant of the strided batch (the path starts and ends in host memory: NIC Rx
+ * buffers / socket Tx buffers). h_seg/h_pseudo/h_out should be pinned (hipHostMalloc) for
+ * overlap; the call pipelines H2D -> kernel -> D2H over `n_chunks` chunks on internal streams of
+ * the current device and returns when h_out is complete. */
+NET_ERR  NetUtil_MI355X_ChkSumBatchStridedHost(const void  *h_seg,
+                                               uint64_t     seg_stride,
+                                               CPU_INT16U   seg_len,
+                                               const void  *h_pseudo,
+                                               uint32_t     pseudo_stride,
+                                               CPU_INT16U   pseudo_len,
+                                               uint32_t     n_seg,
+                                               void        *h_out,
+                                               NETCSUM_OP   op,
+                                               uint32_t     n_chunks);
+
+/* ============================================================================================
+ * (3) Support entry points.
+ * ============================================================================================ */
+
+/* One contiguous piece of the checksummed byte stream (host memory). */
+typedef struct netcsum_span {
+    const void  *p;
+    uint32_t     len;
+    uint32_t     rsvd;
+} NETCSUM_SPAN;
+
+/* Reference-exact 32-bit accumulator of the concatenated spans, computed on the GPU:
+ *   *p_sum32 = ( Σ big-endian 16-bit words of span_0 ‖ span_1 ‖ … , odd tail padded with 0x00 )
+ *              mod 2^32
+ * which is exactly the u32 `sum` of net_util.c:1554/:1163 before its end-around-carry fold
+ * (per-buffer partials never exceed 2^31, net_util.c:1321-1475, so only the cross-buffer u32
+ * accumulation wraps, at :1685). Spans are staged through pinned memory of the calling
+ * thread's context. */
+NET_ERR  NetUtil_MI355X_StreamSum32        (const NETCSUM_SPAN *spans,
+                                            uint32_t            n_spans,
+                                            uint32_t           *p_sum32);
+
+/* NET_BUF chain walk of NetUtil_16BitOnesCplSumDataCalc (net_util.c:1589-1687) as pure host
+ * logic: emits the spans whose concatenation is the checksummed stream (pseudo-header first).
+ * Returns NET_UTIL_ERR_NONE, NET_UTIL_ERR_INVALID_PROTOCOL, NET_UTIL_ERR_BUF_TOO_SMALL (more
+ * than max_spans pieces) or — with dbg_chk != 0 — the NET_ERR_CFG_ARG_CHK_DBG_EN errors. */
+NET_ERR  NetUtil_MI355X_ChainToSpans       (const void   *pdata_buf,
+                                            const void   *ppseudo_hdr,
+                                            CPU_INT16U    pseudo_hdr_size,
+                                            NETCSUM_SPAN *spans,
+                                            uint32_t      max_spans,
+                                            uint32_t     *p_n_spans,
+                                            int           dbg_chk);
+
+/* Deterministic synthetic bytes, generated on the device: byte k of the buffer is byte (k & 7)
+ * of splitmix64(seed + (k >> 3)) for pattern 0; 1 = all 0x00; 2 = all 0xFF; 3 = 0xFF,0xFF,0x00,
+ * 0x01 repeating (maximal carries). Asynchronous on hip_stream. */
+NET_ERR  NetUtil_MI355X_Fill               (void      *d_buf,
+                                            uint64_t   n_bytes,
+                                            uint64_t   seed,
+                                            int        pattern,
+                                            void      *hip_stream);
+
+/* Roofline probe: a pure HBM read stream over [d_buf, d_buf + n_bytes) (16-B aligned, n_bytes a
+ * multiple of 16) summing dwords into *d_sink (device uint64). Same launch geometry policy as the
+ * checksum kernels; used by bench.py as the measured achievable read bandwidth. */
+NET_ERR  NetUtil_MI355X_ReadStream         (const void *d_buf,
+                                            uint64_t    n_bytes,
+                                            uint64_t   *d_sink,
+                                            void       *hip_stream);
+
+/* Launch tuning knobs (process-wide; 0 = automatic). */
+typedef enum netcsum_tune_key {
+    NETCSUM_TUNE_GRID_BLOCKS   = 1,   /* workgroups per launch (0: derived from the CU count)    */
+    NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */
+    NETCSUM_TUNE_NT_LOADS      = 3,   /* 1: non-temporal loads on the segment stream             */
+    NETCSUM_TUNE_BLOCK_THREADS = 4    /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
+} NETCSUM_TUNE_KEY;
+
+NET_ERR  NetUtil_MI355X_Tune               (int key, int value);
+
+/* Version / build identification string ("netcsum-mi355x <ver> gfx950"). */
+const char *NetUtil_MI355X_Version         (void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NETCSUM_MI355X_H */

@@ -1,0 +1,136 @@
+"""ORACLE — test infrastructure only (ctypes loader for oracle/build/liboracle_netutil.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker / CPU baseline. The product library never links or calls it.
+
+The C restatement it loads is documented in oracle/net_util_oracle.h (parity status: pinned by
+external RFC 1071 / IPv4 KATs and by the independent numpy restatement oracle/oracle_np.py;
+"parity unpinned" by the reference's own artefacts, which do not exist).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle_netutil.so")
+_lib = None
+
+OP_DATA_CALC, OP_DATA_VERIFY, OP_HDR_CALC, OP_HDR_VERIFY = 0, 1, 2, 3
+
+
+def build() -> str:
+    """Compile the C restatement with gcc (oracle/Makefile)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        pu32 = ctypes.POINTER(ctypes.c_uint32)
+        L.Oracle_HdrCalc.argtypes = [vp, u16, pu32, i32]
+        L.Oracle_HdrCalc.restype = u16
+        L.Oracle_HdrVerify.argtypes = [vp, u16, pu32, i32]
+        L.Oracle_HdrVerify.restype = ctypes.c_uint8
+        L.Oracle_DataCalc.argtypes = [vp, vp, u16, pu32, i32]
+        L.Oracle_DataCalc.restype = u16
+        L.Oracle_DataVerify.argtypes = [vp, vp, u16, pu32, i32]
+        L.Oracle_DataVerify.restype = ctypes.c_uint8
+        L.Oracle_DataSum32.argtypes = [vp, vp, u16, pu32]
+        L.Oracle_DataSum32.restype = u32
+        L.Oracle_BatchStrided.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, i32]
+        L.Oracle_BatchStrided.restype = None
+        L.Oracle_BatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
+        L.Oracle_BatchVarLen.restype = None
+        L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
+        L.Oracle_Fill.restype = None
+        L.Oracle_MaxThreads.argtypes = []
+        L.Oracle_MaxThreads.restype = i32
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return ctypes.cast(a, ctypes.c_void_p).value
+
+
+# ----------------------------------------------------------------------------- per-packet API
+def hdr_calc(ptr, size, dbg=False):
+    err = ctypes.c_uint32(0)
+    v = lib().Oracle_HdrCalc(_ptr(ptr), size, ctypes.byref(err), int(dbg))
+    return int(v), int(err.value)
+
+
+def hdr_verify(ptr, size, dbg=False):
+    err = ctypes.c_uint32(0)
+    v = lib().Oracle_HdrVerify(_ptr(ptr), size, ctypes.byref(err), int(dbg))
+    return int(v), int(err.value)
+
+
+def data_calc(pbuf, pseudo, pseudo_size, dbg=False):
+    err = ctypes.c_uint32(0)
+    v = lib().Oracle_DataCalc(_ptr(pbuf), _ptr(pseudo), pseudo_size, ctypes.byref(err), int(dbg))
+    return int(v), int(err.value)
+
+
+def data_verify(pbuf, pseudo, pseudo_size, dbg=False):
+    err = ctypes.c_uint32(0)
+    v = lib().Oracle_DataVerify(_ptr(pbuf), _ptr(pseudo), pseudo_size, ctypes.byref(err), int(dbg))
+    return int(v), int(err.value)
+
+
+def data_sum32(pbuf, pseudo, pseudo_size):
+    s = ctypes.c_uint32(0)
+    err = lib().Oracle_DataSum32(_ptr(pbuf), _ptr(pseudo), pseudo_size, ctypes.byref(s))
+    return int(s.value), int(err)
+
+
+# ----------------------------------------------------------------------------- batch drivers
+def _out_array(n, op):
+    return np.zeros(n, dtype=np.uint16 if op in (OP_DATA_CALC, OP_HDR_CALC) else np.uint8)
+
+
+def batch_strided(seg: np.ndarray, seg_stride: int, seg_len: int, pseudo, pseudo_stride: int,
+                  pseudo_len: int, n_seg: int, op: int = OP_DATA_CALC, n_threads: int = 1,
+                  seg_offset: int = 0) -> np.ndarray:
+    """Reference semantics of NetUtil_MI355X_ChkSumBatchStrided over host numpy buffers."""
+    out = _out_array(n_seg, op)
+    base = seg.ctypes.data + seg_offset
+    lib().Oracle_BatchStrided(base, seg_stride, seg_len, _ptr(pseudo), pseudo_stride, pseudo_len,
+                              n_seg, out.ctypes.data, op, n_threads)
+    return out
+
+
+def batch_varlen(base: np.ndarray, seg_off: np.ndarray, seg_len: np.ndarray, pseudo, pseudo_stride: int,
+                 pseudo_len: int, op: int = OP_DATA_CALC, n_threads: int = 1) -> np.ndarray:
+    seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    seg_len = np.ascontiguousarray(seg_len, dtype=np.uint16)
+    n = int(seg_off.shape[0])
+    out = _out_array(n, op)
+    lib().Oracle_BatchVarLen(base.ctypes.data, seg_off.ctypes.data, seg_len.ctypes.data, _ptr(pseudo),
+                             pseudo_stride, pseudo_len, n, out.ctypes.data, op, n_threads)
+    return out
+
+
+def fill(first_byte: int, n_bytes: int, seed: int, pattern: int = 0) -> np.ndarray:
+    buf = np.empty(n_bytes, dtype=np.uint8)
+    lib().Oracle_Fill(buf.ctypes.data, first_byte, n_bytes, seed, pattern)
+    return buf
+
+
+def max_threads() -> int:
+    return int(lib().Oracle_MaxThreads())

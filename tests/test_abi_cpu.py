@@ -1,0 +1,109 @@
+"""CPU-side checks of the product C ABI (no kernel launches):
+
+* libnetcsum_mi355x.so loads and exports every function include/netcsum_mi355x.h declares;
+* the gfx950 code object is embedded (the library is a HIP fat binary for gfx950 only);
+* the NET_BUF chain walk (host logic of net_util.c:1589-1687) yields exactly the byte stream of the
+  numpy oracle's stream view, for random chains, every protocol type, odd pseudo-headers, the
+  NULL-chain quirk and the DBG-mode errors;
+* argument validation errors are returned before any device work;
+* without a GPU the per-packet functions FAIL LOUDLY (NET_UTIL_ERR_MI355X_DEV) — there is no CPU
+  fallback to silently produce numbers.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+import netcsum
+import oracle_np as onp
+from conftest import gpu_available
+from helpers import rand_bytes, rand_chain, to_np_buf
+
+
+def test_library_exports_every_header_symbol():
+    L = netcsum.lib()
+    names = netcsum.exported_symbols_from_headers()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/netcsum_mi355x.h but not exported"
+    assert netcsum.version().endswith("gfx950")
+
+
+def test_library_carries_gfx950_code_object():
+    """The .hip_fatbin section embeds an amdgcn code object whose target id is gfx950."""
+    blob = open(netcsum.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def _stream_bytes(spans):
+    return b"".join(ctypes.string_at(p, ln) for p, ln in spans)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_chain_to_spans_matches_stream_view(seed):
+    rng = random.Random(seed)
+    for _ in range(120):
+        nbuf = rng.randint(1, 5)
+        chain = rand_chain(rng, rng.randint(0, 2000), nbuf)
+        plen = rng.choice([0, 1, 11, 12, 40])
+        pseudo = rand_bytes(rng, plen) if rng.random() < 0.8 else None
+        ch = netcsum.Chain(chain)
+        ph = netcsum.HostBytes(pseudo, rng.randint(0, 7)) if pseudo is not None else None
+        spans, err = netcsum.chain_to_spans(ch.ptr, ph.ptr if ph else None, plen if ph else 0)
+        want, werr = onp.chain_stream([to_np_buf(b) for b in chain], pseudo)
+        assert err == werr == 200
+        assert _stream_bytes(spans) == want
+
+
+def test_chain_to_spans_quirks_and_errors():
+    ph = netcsum.HostBytes(b"\x01\x02\x03")
+    spans, err = netcsum.chain_to_spans(None, ph.ptr, 3)          # NULL chain: odd octet dropped
+    assert err == 200 and _stream_bytes(spans) == b"\x01\x02"
+    bad = netcsum.Chain([{"data": b"ab", "proto": 71}, {"data": b"cd", "proto": 62}])
+    assert netcsum.chain_to_spans(bad.ptr, None, 0)[1] == 211
+    assert netcsum.chain_to_spans(None, None, 0, dbg=True)[1] == 23
+    empty = netcsum.Chain([{"data": b"", "proto": 70}])
+    assert netcsum.chain_to_spans(empty.ptr, None, 0, dbg=True)[1] == 210
+    assert netcsum.chain_to_spans(empty.ptr, None, 0, dbg=False) == ([], 200)
+    ix = netcsum.Chain([{"data": b"abcd", "proto": 71, "transport_ix": 0xFFFF, "data_len": 0}])
+    assert netcsum.chain_to_spans(ix.ptr, None, 0, dbg=True)[1] == 622
+    many = netcsum.Chain([{"data": b"ab", "proto": 71}] * 10)
+    assert netcsum.chain_to_spans(many.ptr, None, 0, max_spans=4)[1] == netcsum.NET_UTIL_ERR_BUF_TOO_SMALL
+
+
+def test_batch_argument_validation_before_device_work():
+    L = netcsum.lib()
+    # HDR ops take no pseudo-header
+    assert L.NetUtil_MI355X_ChkSumBatchStrided(1, 20, 20, 8, 12, 12, 4, 16, netcsum.OP_HDR_CALC, None) == 219
+    assert L.NetUtil_MI355X_ChkSumBatchStrided(1, 20, 20, None, 0, 0, 4, 16, 7, None) == 219
+    assert L.NetUtil_MI355X_ChkSumBatchStrided(None, 20, 20, None, 0, 0, 4, 16, 0, None) == 23
+    assert L.NetUtil_MI355X_ChkSumBatchStrided(None, 20, 20, None, 0, 0, 0, None, 0, None) == 200   # n=0
+    assert L.NetUtil_MI355X_ChkSumBatchVarLen(8, None, 8, None, 0, 0, 4, 16, 0, None) == 23
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
+    assert L.NetUtil_MI355X_Tune(99, 1) == 219
+    assert L.NetUtil_MI355X_Fill(3, 10, 0, 0, None) == 219                    # not 8-B aligned
+    assert L.NetUtil_MI355X_ReadStream(16, 17, 8, None) == 219                # not a multiple of 16
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU behaviour")
+def test_no_gpu_fails_loudly_without_fallback():
+    hb = netcsum.HostBytes(bytes.fromhex("450000730000400040110000c0a80001c0a800c7"))
+    v, err = netcsum.HdrCalc(hb.ptr, 20)
+    assert (v, err) == (0, netcsum.NET_UTIL_ERR_MI355X_DEV)
+    ch = netcsum.Chain([{"data": b"abcdef", "proto": 71}])
+    assert netcsum.DataVerify(ch.ptr, None, 0) == (0, netcsum.NET_UTIL_ERR_MI355X_DEV)
+    assert netcsum.stream_sum32([(hb.ptr, 20)])[1] == netcsum.NET_UTIL_ERR_MI355X_DEV
+
+
+def test_header_is_plain_c():
+    """include/*.h compile as C89-ish C11 with no HIP/torch types (the drop-in boundary)."""
+    inc = os.path.join(netcsum.REPO, "include")
+    src = '#include "netcsum_mi355x.h"\n#include "netcsum_netbuf.h"\nint main(void){return 0;}\n'
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-pedantic", "-I", inc, "-x", "c", "-",
+                        "-fsyntax-only"], input=src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

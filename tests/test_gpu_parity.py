@@ -1,0 +1,284 @@
+"""GPU parity: every product entry point, through the C ABI, against the oracle on the same bytes.
+
+Bar: bit-exact (integer checksums). Small/medium sizes compare every output with the C oracle
+(which the KAT and cross tests pin); the full BASELINE size (config C2: 1 M x 1500 B + 12 B
+pseudo-header) is checked with size-independent properties (Calc -> write back -> Verify round
+trip over every segment, single-byte corruption detection) plus an oracle-compared random sample.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle
+from helpers import rand_bytes, rand_chain
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _reset_tuning():
+    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES, netcsum.TUNE_NT_LOADS, netcsum.TUNE_BLOCK_THREADS):
+        netcsum.tune(k, 0)
+
+
+@pytest.fixture(autouse=True)
+def _tuning_defaults():
+    _reset_tuning()
+    yield
+    _reset_tuning()
+
+
+def _host_bytes(rng, n, pattern):
+    if pattern == "zero":
+        return np.zeros(n, np.uint8)
+    if pattern == "ff":
+        return np.full(n, 0xFF, np.uint8)
+    if pattern == "carry":
+        return np.resize(np.array([0xFF, 0xFF, 0x00, 0x01], np.uint8), n)
+    return rng.integers(0, 256, size=n, dtype=np.uint8)
+
+
+def _out(n, op):
+    return torch.zeros(n, dtype=torch.int16 if op in (0, 2) else torch.uint8, device=DEV)
+
+
+def _np_out(t):
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if a.dtype == np.int16 else a
+
+
+def _gpu_strided(data_d, base_off, stride, L, ph_d, pstride, plen, n, op):
+    out = _out(n, op)
+    netcsum.batch_strided(data_d.data_ptr() + base_off, stride, L, ph_d if plen else None, pstride, plen, n, out, op)
+    torch.cuda.synchronize()
+    return _np_out(out)
+
+
+LENGTHS = [0, 1, 2, 3, 4, 5, 7, 15, 16, 17, 19, 20, 21, 31, 33, 40, 63, 64, 65, 127, 255, 256, 257,
+           1023, 1499, 1500, 1501, 4520, 8999, 9000, 16385, 65535]
+
+
+@pytest.mark.parametrize("L", LENGTHS)
+def test_strided_matrix_vs_oracle(L):
+    rng = np.random.default_rng(L + 11)
+    n = 37 if L < 20000 else 5
+    for pattern in ("random", "zero", "ff", "carry"):
+        for stride in (L, L + 1, L + 3, L + 13):
+            stride = max(stride, 1)
+            data = _host_bytes(rng, n * stride + L + 64, pattern)
+            data_d = torch.from_numpy(data).to(DEV)
+            for base_off in (0, 1, 2, 3) if pattern == "random" else (0, 1):
+                for plen, pstride in ((0, 0), (12, 12), (11, 13), (40, 41), (1, 1)):
+                    ph = _host_bytes(rng, n * max(pstride, 1) + 64, pattern)
+                    ph_d = torch.from_numpy(ph).to(DEV)
+                    pofs = int(rng.integers(0, 3)) if plen else 0
+                    for op in (0, 1, 2, 3):
+                        if op >= 2 and plen:
+                            continue
+                        got = _gpu_strided(data_d, base_off, stride, L, ph_d.data_ptr() + pofs if plen else None,
+                                           pstride, plen, n, op)
+                        want = oracle.batch_strided(data, stride, L, ph[pofs:] if plen else None, pstride, plen, n, op,
+                                                    seg_offset=base_off)
+                        assert np.array_equal(got, want), (L, pattern, stride, base_off, plen, op)
+
+
+@pytest.mark.parametrize("group", [1, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("nt", [0, 1])
+def test_every_group_width_and_load_policy(group, nt):
+    """Force each lane-group width / nt policy and a tiny grid (deep grid-stride loops)."""
+    rng = np.random.default_rng(group * 2 + nt)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+    netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 3)
+    for L, stride in ((1500, 1500), (20, 20), (4519, 4523), (77, 80)):
+        n = 700
+        data = rng.integers(0, 256, size=n * stride + 64, dtype=np.uint8)
+        ph = rng.integers(0, 256, size=n * 12 + 16, dtype=np.uint8)
+        data_d, ph_d = torch.from_numpy(data).to(DEV), torch.from_numpy(ph).to(DEV)
+        for op in (0, 1):
+            got = _gpu_strided(data_d, 1, stride, L, ph_d.data_ptr(), 12, 12, n, op)
+            want = oracle.batch_strided(data, stride, L, ph, 12, 12, n, op, seg_offset=1)
+            assert np.array_equal(got, want), (group, nt, L, op)
+
+
+def _packed_udp(rng, n, lo=40, hi=9000, pattern="random"):
+    lens = rng.integers(lo, hi + 1, size=n).astype(np.uint16)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    base = _host_bytes(rng, int(off[-1]) + int(lens[-1]) + 64, pattern)
+    ph = np.zeros((n, 12), np.uint8)
+    ph[:, 0:4] = rng.integers(0, 256, size=(n, 4))
+    ph[:, 4:8] = rng.integers(0, 256, size=(n, 4))
+    ph[:, 9] = 17
+    ph[:, 10] = (lens >> 8).astype(np.uint8)
+    ph[:, 11] = (lens & 0xFF).astype(np.uint8)
+    return base, off, lens, ph.reshape(-1).copy()
+
+
+@pytest.mark.parametrize("pattern", ["random", "zero", "ff", "carry"])
+def test_varlen_packed_odd_starts_vs_oracle(pattern):
+    rng = np.random.default_rng(7)
+    n = 3000
+    base, off, lens, ph = _packed_udp(rng, n, pattern=pattern)
+    assert (off & 1).sum() > n // 4                            # plenty of odd starts
+    base_d, off_d = torch.from_numpy(base).to(DEV), torch.from_numpy(off.view(np.int64)).to(DEV)
+    len_d, ph_d = torch.from_numpy(lens.view(np.int16)).to(DEV), torch.from_numpy(ph).to(DEV)
+    for op in (0, 1):
+        out = _out(n, op)
+        netcsum.batch_varlen(base_d, off_d, len_d, ph_d, 12, 12, n, out, op)
+        torch.cuda.synchronize()
+        want = oracle.batch_varlen(base, off, lens, ph, 12, 12, op)
+        assert np.array_equal(_np_out(out), want), op
+    # HDR ops on variable-length spans without pseudo-header; also zero-length segments
+    lens2 = lens.copy()
+    lens2[::17] = 0
+    len2_d = torch.from_numpy(lens2.view(np.int16)).to(DEV)
+    for op in (2, 3):
+        out = _out(n, op)
+        netcsum.batch_varlen(base_d, off_d, len2_d, None, 0, 0, n, out, op)
+        torch.cuda.synchronize()
+        want = oracle.batch_varlen(base, off, lens2, None, 0, 0, op)
+        assert np.array_equal(_np_out(out), want), op
+
+
+def test_many_tiny_ipv4_headers_vs_oracle():
+    """Config C3 shape (20-B IPv4 headers, HdrCalc semantics) at 1 M headers."""
+    rng = np.random.default_rng(3)
+    n = 1 << 20
+    hdr = rng.integers(0, 256, size=n * 20, dtype=np.uint8)
+    hdr_d = torch.from_numpy(hdr).to(DEV)
+    for op in (2, 3):
+        got = _gpu_strided(hdr_d, 0, 20, 20, None, 0, 0, n, op)
+        want = oracle.batch_strided(hdr, 20, 20, None, 0, 0, n, op, n_threads=8)
+        assert np.array_equal(got, want), op
+    # write each header's checksum into bytes 10-11 -> every header verifies
+    csum = _gpu_strided(hdr_d, 0, 20, 20, None, 0, 0, n, 2)
+    h2 = hdr.reshape(n, 20).copy()
+    h2[:, 10:12] = 0
+    h2d = torch.from_numpy(h2.reshape(-1)).to(DEV)
+    c0 = _gpu_strided(h2d, 0, 20, 20, None, 0, 0, n, 2)
+    h2[:, 10:12] = c0.view(np.uint8).reshape(n, 2)
+    ok = _gpu_strided(torch.from_numpy(h2.reshape(-1)).to(DEV), 0, 20, 20, None, 0, 0, n, 3)
+    assert ok.all()
+    del csum
+
+
+def test_reference_signatures_on_gpu_vs_oracle():
+    """The four drop-in functions (NET_BUF chains in host memory) against the C oracle."""
+    rng = random.Random(99)
+    for it in range(400):
+        nbuf = rng.randint(1, 4)
+        pat = rng.choice(["random", "random", "zero", "ff", "carry"])
+        chain = rand_chain(rng, rng.choice([0, 1, 7, rng.randint(0, 3000)]), nbuf, pattern=pat)
+        ch = netcsum.Chain(chain)
+        plen = rng.choice([0, 11, 12, 40])
+        ph = netcsum.HostBytes(rand_bytes(rng, plen, pat), rng.randint(0, 3)) if rng.random() < 0.85 else None
+        args = (ch.ptr, ph.ptr if ph else None, plen if ph else 0)
+        assert netcsum.DataCalc(*args) == oracle.data_calc(*args), it
+        assert netcsum.DataVerify(*args) == oracle.data_verify(*args), it
+        hsz = rng.randint(0, 60)
+        hb = netcsum.HostBytes(rand_bytes(rng, hsz, pat), rng.randint(0, 7))
+        assert netcsum.HdrCalc(hb.ptr, hsz) == oracle.hdr_calc(hb.ptr, hsz), it
+        assert netcsum.HdrVerify(hb.ptr, hsz) == oracle.hdr_verify(hb.ptr, hsz), it
+    # KATs straight through the drop-in
+    ip = netcsum.HostBytes(bytes.fromhex("450000730000400040110000c0a80001c0a800c7"), 1)
+    assert netcsum.HdrCalc(ip.ptr, 20) == (0x61B8, 200)
+    bad = netcsum.Chain([{"data": b"abcd", "proto": netcsum.NET_PROTOCOL_TYPE_IGMP}])
+    assert netcsum.DataCalc(bad.ptr, None, 0) == (0, 211)
+    ph12 = netcsum.HostBytes(b"\x0a\x00\x00\x01\x0a\x00\x00\x02\x00\x06\x00\x14")
+    assert netcsum.DataCalc(None, ph12.ptr, 12) == oracle.data_calc(None, ph12.ptr, 12)
+
+
+def test_stream_sum32_reproduces_u32_wrap():
+    chain = [{"data": b"\xff" * 65535, "proto": netcsum.NET_PROTOCOL_TYPE_TCP_V4} for _ in range(3)]
+    ch = netcsum.Chain(chain)
+    spans, err = netcsum.chain_to_spans(ch.ptr, None, 0)
+    s, err2 = netcsum.stream_sum32(spans)
+    want, werr = oracle.data_sum32(ch.ptr, None, 0)
+    assert (s, err2) == (want, 200)
+    assert netcsum.DataCalc(ch.ptr, None, 0) == oracle.data_calc(ch.ptr, None, 0)
+
+
+def test_fill_matches_host_regeneration():
+    n = (1 << 20) + 13
+    buf = torch.empty(n + 3, dtype=torch.uint8, device=DEV)
+    for pattern in range(4):
+        netcsum.fill(buf, n, 0x5EED0001, pattern)
+        torch.cuda.synchronize()
+        got = buf[:n].cpu().numpy()
+        assert np.array_equal(got[:4096], oracle.fill(0, 4096, 0x5EED0001, pattern))
+        assert np.array_equal(got[n - 777:], oracle.fill(n - 777, 777, 0x5EED0001, pattern))
+
+
+def test_read_stream_probe_runs():
+    buf = torch.ones(1 << 24, dtype=torch.uint8, device=DEV)
+    sink = torch.zeros(1, dtype=torch.int64, device=DEV)
+    netcsum.read_stream(buf, buf.numel(), sink)
+    torch.cuda.synchronize()
+    assert int(sink.item()) == 0
+
+
+def test_host_memory_pipeline_vs_oracle():
+    rng = np.random.default_rng(5)
+    n, L = 50_000, 1500
+    data = torch.from_numpy(rng.integers(0, 256, size=n * L, dtype=np.uint8)).pin_memory()
+    ph = torch.from_numpy(rng.integers(0, 256, size=n * 12, dtype=np.uint8)).pin_memory()
+    for op, chunks in ((0, 1), (0, 7), (1, 5)):
+        out = torch.zeros(n, dtype=torch.int16 if op == 0 else torch.uint8).pin_memory()
+        netcsum.batch_strided_host(data, L, L, ph, 12, 12, n, out, op, n_chunks=chunks)
+        want = oracle.batch_strided(data.numpy(), L, L, ph.numpy(), 12, 12, n, op, n_threads=8)
+        got = out.numpy().view(np.uint16) if op == 0 else out.numpy()
+        assert np.array_equal(got, want), (op, chunks)
+
+
+def _c2_batch(n):
+    """Config C2 synthetic batch on device: n x 1500-B TCP segments + n x 12-B pseudo-headers."""
+    L = 1500
+    seg = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    netcsum.fill(seg, seg.numel(), 0x5EED0001, 0)
+    idx = torch.arange(n, device=DEV, dtype=torch.int64)
+    ph = torch.zeros(n, 12, dtype=torch.uint8, device=DEV)
+    for b in range(4):
+        ph[:, b] = ((idx >> (8 * (3 - b))) & 0xFF).to(torch.uint8) | 0x0A * (b == 0)
+        ph[:, 4 + b] = ((idx * 7 >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+    ph[:, 9] = 6
+    ph[:, 10] = L >> 8
+    ph[:, 11] = L & 0xFF
+    torch.cuda.synchronize()
+    return seg, ph.reshape(-1).contiguous(), L
+
+
+def test_full_size_c2_round_trip_and_sample():
+    n = 1 << 20
+    seg, ph, L = _c2_batch(n)
+    csum = _out(n, 0)
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, csum, 0)
+    torch.cuda.synchronize()
+    # sampled oracle comparison on host copies
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(n, size=4096, replace=False))
+    segs = seg.view(n, L)[torch.from_numpy(sample).to(DEV)].cpu().numpy().reshape(-1)
+    phs = ph.view(n, 12)[torch.from_numpy(sample).to(DEV)].cpu().numpy().reshape(-1)
+    want = oracle.batch_strided(segs, L, L, phs, 12, 12, len(sample), 0)
+    assert np.array_equal(_np_out(csum)[sample], want)
+    # Tx -> Rx round trip: zero the TCP checksum field (bytes 16-17), compute, store, verify all
+    s2 = seg.view(n, L)
+    s2[:, 16:18] = 0
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, csum, 0)
+    s2[:, 16:18] = csum.view(torch.uint8).view(n, 2)
+    ok = _out(n, 1)
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, ok, 1)
+    torch.cuda.synchronize()
+    assert bool(ok.all())
+    # corrupt one byte in every 1000th segment -> exactly those fail
+    bad = torch.arange(0, n, 1000, device=DEV)
+    s2[bad, 700] ^= 0x5A
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, ok, 1)
+    torch.cuda.synchronize()
+    failed = torch.nonzero(ok == 0).flatten()
+    assert torch.equal(failed, bad)

@@ -1,0 +1,366 @@
+// netcsum_abi.hip — extern "C" entry points of include/netcsum_mi355x.h groups (2) and (3):
+// argument checks, launch-geometry policy, per-thread device contexts for the host-memory paths.
+// Group (1) — the reference's four signatures — lives in ../host/net_util_mi355x.c (plain C) and
+// reaches the GPU through NetUtil_MI355X_StreamSum32 below.
+//
+// There is deliberately NO CPU fallback anywhere in this library: if the HIP runtime or device
+// fails, the caller gets NET_UTIL_ERR_MI355X_DEV and a message on stderr.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/netcsum_mi355x.h"
+#include "netcsum_kernels.h"
+
+namespace {
+
+constexpr int kMaxDev = 64;
+
+std::atomic<int> g_tune_grid{0};
+std::atomic<int> g_tune_group{0};
+std::atomic<int> g_tune_nt{0};
+std::atomic<int> g_tune_block{256};
+std::atomic<int> g_err_reports{0};
+
+NET_ERR dev_fail(const char* what, hipError_t e) {
+    if (g_err_reports.fetch_add(1) < 8) {
+        std::fprintf(stderr, "[netcsum-mi355x] %s failed: %s (%d) — no CPU fallback, returning "
+                             "NET_UTIL_ERR_MI355X_DEV\n", what, hipGetErrorString(e), (int)e);
+    }
+    return (NET_ERR)NET_UTIL_ERR_MI355X_DEV;
+}
+
+#define NC_HIP(call)                                    \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return dev_fail(#call, e_); \
+    } while (0)
+
+int cu_count(int dev) {
+    static std::atomic<int> cache[kMaxDev];
+    if (dev < 0 || dev >= kMaxDev) return 256;
+    int v = cache[dev].load();
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) {
+            v = 256;
+        }
+        cache[dev].store(v);
+    }
+    return v;
+}
+
+int pow2_group(uint32_t want) {                     // smallest supported group >= want
+    static const int gs[] = {1, 4, 8, 16, 32, 64};
+    for (int g : gs) {
+        if ((uint32_t)g >= want) return g;
+    }
+    return 64;
+}
+
+// Geometry policy. len_hint = typical segment length in bytes (0 = unknown / variable).
+netcsum::LaunchCfg choose_cfg(int dev, uint32_t len_hint, uint32_t n_seg, bool varlen) {
+    netcsum::LaunchCfg c{};
+    c.block = g_tune_block.load();
+    if (c.block < 64 || c.block > 1024 || (c.block & 63)) c.block = 256;
+    c.nt = g_tune_nt.load() != 0;
+
+    const uint32_t chunks = varlen ? 256u : (len_hint / 16u + 2u);   // incl. misaligned edges
+    int g = g_tune_group.load();
+    if (g == 0) {
+        g = varlen ? 64 : pow2_group((chunks + 3u) / 4u);
+    }
+    g = pow2_group((uint32_t)g);
+    c.group_lanes = g;
+    int k = (int)std::min<uint32_t>(4u, std::max<uint32_t>(1u, (chunks + (uint32_t)g - 1u) / (uint32_t)g));
+    c.chunks_per_pass = k;
+
+    const uint32_t gpb = (uint32_t)(c.block / g);
+    const uint64_t blocks_needed = ((uint64_t)n_seg + gpb - 1u) / gpb;
+    int grid = g_tune_grid.load();
+    if (grid <= 0) {
+        const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)(2048 / c.block);   // full residency
+        grid = (int)std::max<uint64_t>(1u, std::min<uint64_t>(blocks_needed, cap));
+    }
+    c.grid = grid;
+    return c;
+}
+
+NET_ERR check_op(NETCSUM_OP op, const void* d_pseudo, CPU_INT16U pseudo_len) {
+    if ((int)op < 0 || (int)op > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if ((op == NETCSUM_OP_HDR_CALC || op == NETCSUM_OP_HDR_VERIFY) && d_pseudo != nullptr && pseudo_len != 0) {
+        return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;     // header checksums take no pseudo-header
+    }
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR launch_batch(const netcsum::SegBatchArgs& a, uint32_t len_hint, hipStream_t s) {
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    const netcsum::LaunchCfg c = choose_cfg(dev, len_hint, a.n_seg, a.seg_off != nullptr);
+    NC_HIP(netcsum::launch_seg_batch(a, c, s));
+    return NET_UTIL_ERR_NONE;
+}
+
+// ----------------------------------------------------------- per-thread host-path contexts
+struct HostCtx {
+    bool                 ready = false;
+    hipStream_t          stream = nullptr;
+    uint8_t*             h_stage = nullptr;   // pinned
+    uint8_t*             d_stage = nullptr;
+    size_t               cap = 0;
+    unsigned long long*  d_sum = nullptr;
+    unsigned long long*  h_sum = nullptr;     // pinned
+    // pipelined host batch
+    hipStream_t          pstream[3] = {nullptr, nullptr, nullptr};
+    uint8_t*             d_pipe[3] = {nullptr, nullptr, nullptr};
+    size_t               pipe_cap = 0;
+};
+
+thread_local HostCtx tls_ctx[kMaxDev];
+
+NET_ERR host_ctx(HostCtx** out) {
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDev) return dev_fail("device index", hipErrorInvalidDevice);
+    HostCtx& c = tls_ctx[dev];
+    if (!c.ready) {
+        NC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        NC_HIP(hipMalloc(&c.d_sum, 16));
+        NC_HIP(hipHostMalloc(&c.h_sum, 16, hipHostMallocDefault));
+        c.ready = true;
+    }
+    *out = &c;
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR ensure_stage(HostCtx& c, size_t bytes) {
+    if (bytes <= c.cap) return NET_UTIL_ERR_NONE;
+    size_t cap = std::max<size_t>(bytes, 64u * 1024u);
+    cap = (cap + 4095u) & ~(size_t)4095u;
+    if (c.h_stage) { (void)hipHostFree(c.h_stage); c.h_stage = nullptr; }
+    if (c.d_stage) { (void)hipFree(c.d_stage); c.d_stage = nullptr; }
+    c.cap = 0;
+    NC_HIP(hipHostMalloc(&c.h_stage, cap, hipHostMallocDefault));
+    NC_HIP(hipMalloc(&c.d_stage, cap));
+    c.cap = cap;
+    return NET_UTIL_ERR_NONE;
+}
+
+}  // namespace
+
+extern "C" {
+
+NET_ERR NetUtil_MI355X_ChkSumBatchStrided(const void* d_seg, uint64_t seg_stride, CPU_INT16U seg_len,
+                                          const void* d_pseudo, uint32_t pseudo_stride, CPU_INT16U pseudo_len,
+                                          uint32_t n_seg, void* d_out, NETCSUM_OP op, void* hip_stream) {
+    NET_ERR e = check_op(op, d_pseudo, pseudo_len);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (d_out == nullptr || (d_seg == nullptr && seg_len != 0)) return NET_ERR_FAULT_NULL_PTR;
+    netcsum::SegBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_seg);
+    a.seg_stride = seg_stride;
+    a.seg_len = seg_len;
+    a.pseudo = (pseudo_len != 0) ? static_cast<const uint8_t*>(d_pseudo) : nullptr;
+    a.pseudo_stride = pseudo_stride;
+    a.pseudo_len = pseudo_len;
+    a.n_seg = n_seg;
+    a.verify = (op == NETCSUM_OP_DATA_VERIFY || op == NETCSUM_OP_HDR_VERIFY) ? 1u : 0u;
+    a.out = d_out;
+    return launch_batch(a, seg_len, static_cast<hipStream_t>(hip_stream));
+}
+
+NET_ERR NetUtil_MI355X_ChkSumBatchVarLen(const void* d_base, const uint64_t* d_seg_off, const uint16_t* d_seg_len,
+                                         const void* d_pseudo, uint32_t pseudo_stride, CPU_INT16U pseudo_len,
+                                         uint32_t n_seg, void* d_out, NETCSUM_OP op, void* hip_stream) {
+    NET_ERR e = check_op(op, d_pseudo, pseudo_len);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (d_out == nullptr || d_base == nullptr || d_seg_off == nullptr || d_seg_len == nullptr) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    netcsum::SegBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.seg_off = d_seg_off;
+    a.seg_len_v = d_seg_len;
+    a.pseudo = (pseudo_len != 0) ? static_cast<const uint8_t*>(d_pseudo) : nullptr;
+    a.pseudo_stride = pseudo_stride;
+    a.pseudo_len = pseudo_len;
+    a.n_seg = n_seg;
+    a.verify = (op == NETCSUM_OP_DATA_VERIFY || op == NETCSUM_OP_HDR_VERIFY) ? 1u : 0u;
+    a.out = d_out;
+    return launch_batch(a, 0u, static_cast<hipStream_t>(hip_stream));
+}
+
+NET_ERR NetUtil_MI355X_ChkSumBatchStridedHost(const void* h_seg, uint64_t seg_stride, CPU_INT16U seg_len,
+                                              const void* h_pseudo, uint32_t pseudo_stride, CPU_INT16U pseudo_len,
+                                              uint32_t n_seg, void* h_out, NETCSUM_OP op, uint32_t n_chunks) {
+    NET_ERR e = check_op(op, h_pseudo, pseudo_len);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (h_out == nullptr || (h_seg == nullptr && seg_len != 0)) return NET_ERR_FAULT_NULL_PTR;
+    HostCtx* cp = nullptr;
+    e = host_ctx(&cp);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    HostCtx& c = *cp;
+    const bool verify = (op == NETCSUM_OP_DATA_VERIFY || op == NETCSUM_OP_HDR_VERIFY);
+    const size_t out_elt = verify ? 1u : 2u;
+    const bool has_ph = (h_pseudo != nullptr && pseudo_len != 0);
+    if (n_chunks == 0) n_chunks = 1;
+    if (n_chunks > n_seg) n_chunks = n_seg;
+    const uint32_t per = (n_seg + n_chunks - 1u) / n_chunks;
+
+    // Device layout per in-flight chunk: [segment bytes | pseudo bytes | outputs], 256-B aligned.
+    auto al = [](size_t x) { return (x + 255u) & ~(size_t)255u; };
+    const size_t seg_bytes = (size_t)(per - 1u) * seg_stride + seg_len;
+    const size_t ph_bytes = has_ph ? (size_t)(per - 1u) * pseudo_stride + pseudo_len : 0u;
+    const size_t need = al(seg_bytes) + al(ph_bytes) + al((size_t)per * out_elt);
+    if (need > c.pipe_cap) {
+        for (int j = 0; j < 3; ++j) {
+            if (c.d_pipe[j]) { (void)hipFree(c.d_pipe[j]); c.d_pipe[j] = nullptr; }
+        }
+        c.pipe_cap = 0;
+        for (int j = 0; j < 3; ++j) {
+            if (!c.pstream[j]) NC_HIP(hipStreamCreateWithFlags(&c.pstream[j], hipStreamNonBlocking));
+            NC_HIP(hipMalloc(&c.d_pipe[j], need));
+        }
+        c.pipe_cap = need;
+    }
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    for (uint32_t k = 0; k < n_chunks; ++k) {
+        const uint32_t s0 = k * per;
+        if (s0 >= n_seg) break;
+        const uint32_t ns = std::min(per, n_seg - s0);
+        const int j = (int)(k % 3u);
+        hipStream_t st = c.pstream[j];
+        uint8_t* d_seg = c.d_pipe[j];
+        uint8_t* d_ph = d_seg + al(seg_bytes);
+        uint8_t* d_out = d_ph + al(ph_bytes);
+        const size_t sb = (size_t)(ns - 1u) * seg_stride + seg_len;
+        NC_HIP(hipMemcpyAsync(d_seg, static_cast<const uint8_t*>(h_seg) + (size_t)s0 * seg_stride, sb,
+                              hipMemcpyHostToDevice, st));
+        if (has_ph) {
+            const size_t pb = (size_t)(ns - 1u) * pseudo_stride + pseudo_len;
+            NC_HIP(hipMemcpyAsync(d_ph, static_cast<const uint8_t*>(h_pseudo) + (size_t)s0 * pseudo_stride, pb,
+                                  hipMemcpyHostToDevice, st));
+        }
+        netcsum::SegBatchArgs a{};
+        a.base = d_seg;
+        a.seg_stride = seg_stride;
+        a.seg_len = seg_len;
+        a.pseudo = has_ph ? d_ph : nullptr;
+        a.pseudo_stride = pseudo_stride;
+        a.pseudo_len = has_ph ? pseudo_len : 0u;
+        a.n_seg = ns;
+        a.verify = verify ? 1u : 0u;
+        a.out = d_out;
+        // Parity of each segment's start is derived in-kernel from the DEVICE address it reads,
+        // so re-basing the chunk at a 256-B aligned device buffer is transparent.
+        const netcsum::LaunchCfg cfg = choose_cfg(dev, seg_len, ns, false);
+        NC_HIP(netcsum::launch_seg_batch(a, cfg, st));
+        NC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(h_out) + (size_t)s0 * out_elt, d_out, (size_t)ns * out_elt,
+                              hipMemcpyDeviceToHost, st));
+    }
+    for (int j = 0; j < 3; ++j) {
+        NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    }
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_StreamSum32(const NETCSUM_SPAN* spans, uint32_t n_spans, uint32_t* p_sum32) {
+    if (p_sum32 == nullptr || (spans == nullptr && n_spans != 0)) return NET_ERR_FAULT_NULL_PTR;
+    HostCtx* cp = nullptr;
+    NET_ERR e = host_ctx(&cp);                 // the device must exist even for an empty stream
+    if (e != NET_UTIL_ERR_NONE) return e;
+    HostCtx& c = *cp;
+    size_t total = 0;
+    for (uint32_t i = 0; i < n_spans; ++i) total += spans[i].len;
+    *p_sum32 = 0u;
+    if (total == 0) return NET_UTIL_ERR_NONE;
+    const size_t padded = (total + 15u) & ~(size_t)15u;
+    if (padded / 16u > 0xFFFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    e = ensure_stage(c, padded);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    size_t pos = 0;
+    for (uint32_t i = 0; i < n_spans; ++i) {
+        if (spans[i].len) {
+            std::memcpy(c.h_stage + pos, spans[i].p, spans[i].len);
+            pos += spans[i].len;
+        }
+    }
+    std::memset(c.h_stage + pos, 0, padded - pos);
+    const uint32_t n16 = (uint32_t)(padded / 16u);
+    const int grid = (int)std::min<uint32_t>(256u, (n16 + 1023u) / 1024u);
+    NC_HIP(hipMemcpyAsync(c.d_stage, c.h_stage, padded, hipMemcpyHostToDevice, c.stream));
+    NC_HIP(hipMemsetAsync(c.d_sum, 0, sizeof(unsigned long long), c.stream));
+    NC_HIP(netcsum::launch_stream_exact(c.d_stage, n16, c.d_sum, std::max(grid, 1), c.stream));
+    NC_HIP(hipMemcpyAsync(c.h_sum, c.d_sum, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+    NC_HIP(hipStreamSynchronize(c.stream));
+    *p_sum32 = (uint32_t)(*c.h_sum);           // the reference's u32 accumulator wraps mod 2^32
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t seed, int pattern, void* hip_stream) {
+    if (n_bytes == 0) return NET_UTIL_ERR_NONE;
+    if (d_buf == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    if (((uintptr_t)d_buf & 7u) != 0u || pattern < 0 || pattern > 3) {
+        return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    }
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    const uint64_t words = (n_bytes >> 3) + 1u;
+    const uint64_t cap = (uint64_t)cu_count(dev) * 8u;
+    const int grid = (int)std::max<uint64_t>(1u, std::min<uint64_t>((words + 255u) / 256u, cap));
+    NC_HIP(netcsum::launch_fill(d_buf, n_bytes, seed, pattern, grid, static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_ReadStream(const void* d_buf, uint64_t n_bytes, uint64_t* d_sink, void* hip_stream) {
+    if (n_bytes == 0) return NET_UTIL_ERR_NONE;
+    if (d_buf == nullptr || d_sink == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    if (((uintptr_t)d_buf & 15u) != 0u || (n_bytes & 15u) != 0u) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    int grid = g_tune_grid.load();
+    if (grid <= 0) grid = cu_count(dev) * 8;
+    NC_HIP(netcsum::launch_read_stream(d_buf, n_bytes / 16u, reinterpret_cast<unsigned long long*>(d_sink), grid,
+                                       g_tune_nt.load() != 0, static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_Tune(int key, int value) {
+    switch (key) {
+    case NETCSUM_TUNE_GRID_BLOCKS:
+        if (value < 0) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_grid.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_GROUP_LANES:
+        if (!(value == 0 || value == 1 || value == 4 || value == 8 || value == 16 || value == 32 || value == 64)) {
+            return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        }
+        g_tune_group.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_NT_LOADS:
+        g_tune_nt.store(value != 0);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_BLOCK_THREADS:
+        if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)
+            return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        }
+        g_tune_block.store(value == 0 ? 256 : value);
+        return NET_UTIL_ERR_NONE;
+    default:
+        return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    }
+}
+
+const char* NetUtil_MI355X_Version(void) {
+    return "netcsum-mi355x 0.1.0 gfx950";
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+/*
+ * net_util_mi355x.c — drop-in host C for µC/TCP-IP's four public checksum functions
+ * (Source/net_util.h:422-438), with the byte summation done on an MI355X through the C ABI in
+ * include/netcsum_mi355x.h. Plain C11; no HIP headers.
+ *
+ * What stays on the host is what the reference does around the sum and cannot move to the GPU:
+ * the NET_BUF chain walk over host memory (net_util.c:1611-1687, per-buffer (ix, len) selection
+ * by ProtocolHdrType), the argument checks of NET_ERR_CFG_ARG_CHK_DBG_EN, and the 2-op epilogue
+ * on the returned 32-bit accumulator (fold :1690-1692, complement / compare :187-188, :275-276,
+ * :358, :443-444). The bytes themselves are summed by the gfx950 stream kernel
+ * (NetUtil_MI355X_StreamSum32). There is no CPU summation path: a device failure is reported as
+ * NET_UTIL_ERR_MI355X_DEV.
+ *
+ * Build modes:
+ *   standalone (this repo)  — NET_BUF comes from include/netcsum_netbuf.h (template-config
+ *                             mirror); exported from libnetcsum_mi355x.so.
+ *   inside a µC/TCP-IP tree — compile with -DNETCSUM_IN_STACK and the stack's include paths so
+ *                             the real net_util.h / net_buf.h (and its configured layout) are
+ *                             used; see INTEGRATION.md.
+ */
+#ifdef NETCSUM_IN_STACK
+#include <cpu_core.h>
+#include <net_util.h>
+#include <net_buf.h>
+#define NETCSUM_HAVE_MICRIUM_TYPES 1
+#include "../../include/netcsum_mi355x.h"
+#define NC_NET_TO_HOST_16(v) ((CPU_INT16U)NET_UTIL_NET_TO_HOST_16((CPU_INT16U)(v)))
+#ifndef NETCSUM_ARG_CHK_DBG_EN
+#define NETCSUM_ARG_CHK_DBG_EN (NET_ERR_CFG_ARG_CHK_DBG_EN == DEF_ENABLED)
+#endif
+#else
+#include "../../include/netcsum_mi355x.h"
+#include "../../include/netcsum_netbuf.h"
+/* Little-endian host: MEM_VAL_BIG_TO_HOST_16 is a byte swap (uC-LIB lib_mem.h semantics). */
+#define NC_NET_TO_HOST_16(v) ((CPU_INT16U)__builtin_bswap16((uint16_t)(v)))
+#ifndef NETCSUM_ARG_CHK_DBG_EN
+#define NETCSUM_ARG_CHK_DBG_EN 0          /* template default: DEF_DISABLED (net_cfg.h:184) */
+#endif
+#endif
+
+#include <stddef.h>
+
+#define NC_NEG_ZERO   0xFFFFu              /* NET_UTIL_16_BIT_ONES_CPL_NEG_ZERO (net_util.c:56) */
+#define NC_MAX_SPANS  64u                  /* pseudo-header + up to 63 chained buffers per call */
+
+static CPU_INT16U nc_fold(uint32_t sum)
+{
+    while (sum >> 16) {
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+    }
+    return (CPU_INT16U)sum;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * NET_BUF chain -> byte spans. Host-logic restatement of net_util.c:1589-1687.
+ * ---------------------------------------------------------------------------------------- */
+NET_ERR NetUtil_MI355X_ChainToSpans(const void *pdata_buf, const void *ppseudo_hdr,
+                                    CPU_INT16U pseudo_hdr_size, NETCSUM_SPAN *spans,
+                                    uint32_t max_spans, uint32_t *p_n_spans, int dbg_chk)
+{
+    const NET_BUF *pbuf = (const NET_BUF *)pdata_buf;
+    uint32_t n = 0u;
+    int first = 1;
+
+    if (p_n_spans == NULL || (spans == NULL && max_spans != 0u)) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    *p_n_spans = 0u;
+    if (dbg_chk && pdata_buf == NULL) {                       /* :1566-1570 */
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+
+    if (ppseudo_hdr != NULL && pseudo_hdr_size != 0u) {      /* :1591-1609 */
+        CPU_INT16U len = pseudo_hdr_size;
+        if (pbuf == NULL && (len & 1u) != 0u) {
+            /* The odd last pseudo-header octet is carried toward a first buffer that never
+             * comes (the while loop at :1611 does not run), so it is never summed. */
+            len = (CPU_INT16U)(len - 1u);
+        }
+        if (len != 0u) {
+            if (n >= max_spans) return NET_UTIL_ERR_BUF_TOO_SMALL;
+            spans[n].p = ppseudo_hdr;
+            spans[n].len = len;
+            spans[n].rsvd = 0u;
+            ++n;
+        }
+    }
+
+    while (pbuf != NULL) {                                    /* :1611-1687 */
+        const NET_BUF_HDR *h = &pbuf->Hdr;
+        CPU_INT16U ix, len;
+
+        switch ((int)h->ProtocolHdrType) {                    /* :1613-1640 */
+        case NET_PROTOCOL_TYPE_ICMP_V4:
+        case NET_PROTOCOL_TYPE_ICMP_V6:
+            ix  = h->ICMP_MsgIx;
+            len = (CPU_INT16U)(h->ICMP_HdrLen + (CPU_INT16U)h->DataLen);
+            break;
+        case NET_PROTOCOL_TYPE_UDP_V4:
+        case NET_PROTOCOL_TYPE_UDP_V6:
+        case NET_PROTOCOL_TYPE_TCP_V4:
+        case NET_PROTOCOL_TYPE_TCP_V6:
+            ix  = h->TransportHdrIx;
+            len = (CPU_INT16U)(h->TransportHdrLen + (CPU_INT16U)h->DataLen);
+            break;
+        case NET_PROTOCOL_TYPE_IP_V6_EXT_NONE:
+            ix  = (CPU_INT16U)(h->TotLen - h->DataLen);
+            len = (CPU_INT16U)h->DataLen;
+            break;
+        default:
+            *p_n_spans = 0u;
+            return NET_UTIL_ERR_INVALID_PROTOCOL;            /* :1637-1639 */
+        }
+        if (dbg_chk && ix == NET_BUF_IX_NONE) {               /* :1642-1647 */
+            *p_n_spans = 0u;
+            return NET_BUF_ERR_INVALID_IX;
+        }
+        if (dbg_chk && first) {                               /* :1660-1672 */
+            first = 0;
+            if (h->NextBufPtr == NULL && len == 0u) {
+                *p_n_spans = 0u;
+                return NET_UTIL_ERR_NULL_SIZE;
+            }
+        }
+        if (len != 0u) {                                      /* zero-length buffers only pass */
+            if (n >= max_spans) {                             /* the carried octet through     */
+                *p_n_spans = 0u;
+                return NET_UTIL_ERR_BUF_TOO_SMALL;
+            }
+            spans[n].p = pbuf->DataPtr + ix;
+            spans[n].len = len;
+            spans[n].rsvd = 0u;
+            ++n;
+        }
+        pbuf = (const NET_BUF *)h->NextBufPtr;
+    }
+    *p_n_spans = n;
+    return NET_UTIL_ERR_NONE;
+}
+
+/* The reference's u32 accumulator for one packet, summed on the GPU. */
+static NET_ERR nc_data_sum32(void *pdata_buf, void *ppseudo_hdr, CPU_INT16U pseudo_hdr_size,
+                             uint32_t *p_sum32)
+{
+    NETCSUM_SPAN spans[NC_MAX_SPANS];
+    uint32_t n = 0u;
+    NET_ERR err = NetUtil_MI355X_ChainToSpans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, spans,
+                                              NC_MAX_SPANS, &n, NETCSUM_ARG_CHK_DBG_EN);
+    if (err != NET_UTIL_ERR_NONE) {
+        return err;
+    }
+    return NetUtil_MI355X_StreamSum32(spans, n, p_sum32);
+}
+
+static NET_ERR nc_hdr_sum32(void *phdr, CPU_INT16U hdr_size, uint32_t *p_sum32)
+{
+    NETCSUM_SPAN span;
+#if NETCSUM_ARG_CHK_DBG_EN
+    if (phdr == NULL) {                                       /* :168-172, :255-259 */
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    if (hdr_size < 1u) {                                      /* :174-178, :261-265 */
+        return NET_UTIL_ERR_NULL_SIZE;
+    }
+#endif
+    span.p = phdr;
+    span.len = hdr_size;
+    span.rsvd = 0u;
+    return NetUtil_MI355X_StreamSum32(&span, hdr_size ? 1u : 0u, p_sum32);
+}
+
+/* Replaces Source/net_util.c:159-195. */
+NET_CHK_SUM NetUtil_16BitOnesCplChkSumHdrCalc(void *phdr, CPU_INT16U hdr_size, NET_ERR *p_err)
+{
+    uint32_t sum32 = 0u;
+    NET_ERR err = nc_hdr_sum32(phdr, hdr_size, &sum32);
+    if (err != NET_UTIL_ERR_NONE) {
+        *p_err = err;
+        return 0u;
+    }
+    *p_err = NET_UTIL_ERR_NONE;
+    return NC_NET_TO_HOST_16((CPU_INT16U)~nc_fold(sum32));
+}
+
+/* Replaces Source/net_util.c:245-284. */
+CPU_BOOLEAN NetUtil_16BitOnesCplChkSumHdrVerify(void *phdr, CPU_INT16U hdr_size, NET_ERR *p_err)
+{
+    uint32_t sum32 = 0u;
+    NET_ERR err = nc_hdr_sum32(phdr, hdr_size, &sum32);
+    if (err != NET_UTIL_ERR_NONE) {
+        *p_err = err;
+        return DEF_FAIL;
+    }
+    *p_err = NET_UTIL_ERR_NONE;
+    return (NC_NET_TO_HOST_16(nc_fold(sum32)) == NC_NEG_ZERO) ? DEF_OK : DEF_FAIL;
+}
+
+/* Replaces Source/net_util.c:344-363. */
+NET_CHK_SUM NetUtil_16BitOnesCplChkSumDataCalc(void *pdata_buf, void *ppseudo_hdr,
+                                               CPU_INT16U pseudo_hdr_size, NET_ERR *p_err)
+{
+    uint32_t sum32 = 0u;
+    NET_ERR err = nc_data_sum32(pdata_buf, ppseudo_hdr, pseudo_hdr_size, &sum32);
+    if (err != NET_UTIL_ERR_NONE) {
+        *p_err = err;
+        return 0u;
+    }
+    *p_err = NET_UTIL_ERR_NONE;
+    return (NET_CHK_SUM)~NC_NET_TO_HOST_16(nc_fold(sum32));
+}
+
+/* Replaces Source/net_util.c:428-449. */
+CPU_BOOLEAN NetUtil_16BitOnesCplChkSumDataVerify(void *pdata_buf, void *ppseudo_hdr,
+                                                 CPU_INT16U pseudo_hdr_size, NET_ERR *p_err)
+{
+    uint32_t sum32 = 0u;
+    NET_ERR err = nc_data_sum32(pdata_buf, ppseudo_hdr, pseudo_hdr_size, &sum32);
+    if (err != NET_UTIL_ERR_NONE) {
+        *p_err = err;
+        return DEF_FAIL;
+    }
+    *p_err = NET_UTIL_ERR_NONE;
+    return (NC_NET_TO_HOST_16(nc_fold(sum32)) == NC_NEG_ZERO) ? DEF_OK : DEF_FAIL;
+}

@@ -1,0 +1,310 @@
+"""ctypes binding of libnetcsum_mi355x.so (the C ABI in include/netcsum_mi355x.h).
+
+Mirrors the reference's interface for the checksum path (µC/TCP-IP V3.06.01 Source/net_util.h:
+422-438): the four per-packet functions keep their names, argument meaning and error behaviour
+(`(value, NET_ERR)` pairs here instead of the `p_err` out-parameter), and a NET_BUF ctypes mirror
+(`NetBuf`, layout of include/netcsum_netbuf.h / Source/net_buf.h:394-598 under the template
+configuration) lets Python build packet chains exactly as the stack would hand them over.
+
+The batch ABI is exposed for device-resident data: pass torch tensors (their data_ptr is used) or
+raw integer device addresses, plus a HIP stream handle (defaults to torch's current stream).
+
+There is no Python or CPU fallback: if the shared library is missing, import of the GPU entry
+points raises; if the device is missing, calls return NET_UTIL_ERR_MI355X_DEV (218).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libnetcsum_mi355x.so")
+HEADER_PATHS = [os.path.join(REPO, "include", "netcsum_mi355x.h")]
+
+# NET_ERR values (Source/net_err.h:73,122-126,193 + the MI355X additions in netcsum_types.h)
+NET_ERR_FAULT_NULL_PTR = 23
+NET_UTIL_ERR_NONE = 200
+NET_UTIL_ERR_NULL_SIZE = 210
+NET_UTIL_ERR_INVALID_PROTOCOL = 211
+NET_UTIL_ERR_BUF_TOO_SMALL = 212
+NET_UTIL_ERR_MI355X_DEV = 218
+NET_UTIL_ERR_MI355X_INVALID_ARG = 219
+NET_BUF_ERR_INVALID_IX = 622
+
+# NET_PROTOCOL_TYPE (Source/net_type.h:184-235)
+NET_PROTOCOL_TYPE_IP_V6_EXT_NONE = 48
+NET_PROTOCOL_TYPE_ICMP_V4 = 60
+NET_PROTOCOL_TYPE_ICMP_V6 = 61
+NET_PROTOCOL_TYPE_IGMP = 62
+NET_PROTOCOL_TYPE_UDP_V4 = 70
+NET_PROTOCOL_TYPE_TCP_V4 = 71
+NET_PROTOCOL_TYPE_UDP_V6 = 72
+NET_PROTOCOL_TYPE_TCP_V6 = 73
+
+DEF_OK, DEF_FAIL = 1, 0
+
+OP_DATA_CALC, OP_DATA_VERIFY, OP_HDR_CALC, OP_HDR_VERIFY = 0, 1, 2, 3
+TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
+
+
+# --------------------------------------------------------------------------- NET_BUF mirror
+class NetBufHdr(ctypes.Structure):
+    _fields_ = [
+        ("_rsvd_000", ctypes.c_uint8 * 6),
+        ("Flags", ctypes.c_uint16),
+        ("_rsvd_008", ctypes.c_uint8 * 64),
+        ("NextBufPtr", ctypes.c_void_p),
+        ("_rsvd_080", ctypes.c_uint8 * 24),
+        ("ProtocolHdrType", ctypes.c_int32),
+        ("_rsvd_108", ctypes.c_uint8 * 38),
+        ("ICMP_MsgIx", ctypes.c_uint16),
+        ("ICMP_MsgLen", ctypes.c_uint16),
+        ("ICMP_HdrLen", ctypes.c_uint16),
+        ("IGMP_MsgIx", ctypes.c_uint16),
+        ("IGMP_MsgLen", ctypes.c_uint16),
+        ("TransportHdrIx", ctypes.c_uint16),
+        ("TransportHdrLen", ctypes.c_uint16),
+        ("TransportTotLen", ctypes.c_uint16),
+        ("TransportDataLen", ctypes.c_uint16),
+        ("DataIx", ctypes.c_uint16),
+        ("DataLen", ctypes.c_uint16),
+        ("TotLen", ctypes.c_uint16),
+        ("_rsvd_170", ctypes.c_uint8 * 134),
+    ]
+
+
+class NetBuf(ctypes.Structure):
+    _fields_ = [("Hdr", NetBufHdr), ("DataPtr", ctypes.c_void_p)]
+
+
+assert ctypes.sizeof(NetBufHdr) == 304 and ctypes.sizeof(NetBuf) == 312
+assert NetBufHdr.NextBufPtr.offset == 72 and NetBufHdr.ProtocolHdrType.offset == 104
+assert NetBufHdr.ICMP_MsgIx.offset == 146 and NetBufHdr.ICMP_HdrLen.offset == 150
+assert NetBufHdr.TransportHdrIx.offset == 156 and NetBufHdr.TransportHdrLen.offset == 158
+assert NetBufHdr.DataLen.offset == 166 and NetBufHdr.TotLen.offset == 168
+
+
+class Span(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("len", ctypes.c_uint32), ("rsvd", ctypes.c_uint32)]
+
+
+class Chain:
+    """A NET_BUF chain over host byte arrays (kept alive by this object).
+
+    Each buffer: dict(data=bytes, proto=…, transport_ix=…, transport_hdr_len=…, data_len=…,
+    icmp_ix=…, icmp_hdr_len=…, tot_len=…) — the fields net_util.c:1613-1640 reads.
+    `offset` places the data area at an odd/unaligned address inside a larger allocation.
+    """
+
+    def __init__(self, bufs, offset: int = 0):
+        self._keep = []
+        self.bufs = (NetBuf * max(1, len(bufs)))()
+        for i, b in enumerate(bufs):
+            data = bytes(b.get("data", b""))
+            off = int(b.get("offset", offset))
+            arr = (ctypes.c_uint8 * (len(data) + off + 16))()
+            ctypes.memmove(ctypes.addressof(arr) + off, data, len(data))
+            self._keep.append(arr)
+            nb = self.bufs[i]
+            nb.DataPtr = ctypes.addressof(arr) + off
+            h = nb.Hdr
+            h.ProtocolHdrType = int(b.get("proto", NET_PROTOCOL_TYPE_TCP_V4))
+            h.TransportHdrIx = int(b.get("transport_ix", 0))
+            h.TransportHdrLen = int(b.get("transport_hdr_len", 0))
+            h.DataLen = int(b.get("data_len", len(data) - int(b.get("transport_ix", 0))))
+            h.ICMP_MsgIx = int(b.get("icmp_ix", 0))
+            h.ICMP_HdrLen = int(b.get("icmp_hdr_len", 0))
+            h.TotLen = int(b.get("tot_len", 0))
+            h.NextBufPtr = None
+        for i in range(len(bufs) - 1):
+            self.bufs[i].Hdr.NextBufPtr = ctypes.addressof(self.bufs[i + 1])
+        self.n = len(bufs)
+
+    @property
+    def ptr(self):
+        return ctypes.addressof(self.bufs[0]) if self.n else None
+
+
+class HostBytes:
+    """Bytes placed at a chosen misalignment in a ctypes buffer (for pseudo-headers / headers)."""
+
+    def __init__(self, data: bytes, offset: int = 0):
+        data = bytes(data)
+        self.arr = (ctypes.c_uint8 * (len(data) + offset + 16))()
+        ctypes.memmove(ctypes.addressof(self.arr) + offset, data, len(data))
+        self.ptr = ctypes.addressof(self.arr) + offset
+        self.len = len(data)
+
+
+# --------------------------------------------------------------------------- library loading
+_lib = None
+
+
+def exported_symbols_from_headers() -> list[str]:
+    """Every function name declared in include/netcsum_mi355x.h."""
+    names = []
+    for p in HEADER_PATHS:
+        txt = open(p).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names += re.findall(r"\b(NetUtil_\w+)\s*\(", txt)
+    return sorted(set(names))
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing — build it with `make -C {HERE}` (no fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    perr = ctypes.POINTER(ctypes.c_int32)
+    L.NetUtil_16BitOnesCplChkSumHdrCalc.argtypes = [vp, u16, perr]
+    L.NetUtil_16BitOnesCplChkSumHdrCalc.restype = u16
+    L.NetUtil_16BitOnesCplChkSumHdrVerify.argtypes = [vp, u16, perr]
+    L.NetUtil_16BitOnesCplChkSumHdrVerify.restype = ctypes.c_uint8
+    L.NetUtil_16BitOnesCplChkSumDataCalc.argtypes = [vp, vp, u16, perr]
+    L.NetUtil_16BitOnesCplChkSumDataCalc.restype = u16
+    L.NetUtil_16BitOnesCplChkSumDataVerify.argtypes = [vp, vp, u16, perr]
+    L.NetUtil_16BitOnesCplChkSumDataVerify.restype = ctypes.c_uint8
+    L.NetUtil_MI355X_ChkSumBatchStrided.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, vp]
+    L.NetUtil_MI355X_ChkSumBatchStrided.restype = i32
+    L.NetUtil_MI355X_ChkSumBatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, vp]
+    L.NetUtil_MI355X_ChkSumBatchVarLen.restype = i32
+    L.NetUtil_MI355X_ChkSumBatchStridedHost.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, u32]
+    L.NetUtil_MI355X_ChkSumBatchStridedHost.restype = i32
+    L.NetUtil_MI355X_StreamSum32.argtypes = [ctypes.POINTER(Span), u32, ctypes.POINTER(ctypes.c_uint32)]
+    L.NetUtil_MI355X_StreamSum32.restype = i32
+    L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
+                                              ctypes.POINTER(ctypes.c_uint32), i32]
+    L.NetUtil_MI355X_ChainToSpans.restype = i32
+    L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, i32, vp]
+    L.NetUtil_MI355X_Fill.restype = i32
+    L.NetUtil_MI355X_ReadStream.argtypes = [vp, u64, vp, vp]
+    L.NetUtil_MI355X_ReadStream.restype = i32
+    L.NetUtil_MI355X_Tune.argtypes = [i32, i32]
+    L.NetUtil_MI355X_Tune.restype = i32
+    L.NetUtil_MI355X_Version.argtypes = []
+    L.NetUtil_MI355X_Version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _p(x):
+    """Pointer from a torch tensor, numpy array, ctypes object, int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return ctypes.addressof(x)
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    return int(stream)
+
+
+def _check(err, what):
+    if err != NET_UTIL_ERR_NONE:
+        raise RuntimeError(f"{what} returned NET_ERR {err}")
+
+
+# --------------------------------------------------------------------- reference interface
+def HdrCalc(phdr, hdr_size):
+    err = ctypes.c_int32(0)
+    v = lib().NetUtil_16BitOnesCplChkSumHdrCalc(_p(phdr), hdr_size, ctypes.byref(err))
+    return int(v), int(err.value)
+
+
+def HdrVerify(phdr, hdr_size):
+    err = ctypes.c_int32(0)
+    v = lib().NetUtil_16BitOnesCplChkSumHdrVerify(_p(phdr), hdr_size, ctypes.byref(err))
+    return int(v), int(err.value)
+
+
+def DataCalc(pdata_buf, ppseudo_hdr, pseudo_hdr_size):
+    err = ctypes.c_int32(0)
+    v = lib().NetUtil_16BitOnesCplChkSumDataCalc(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size,
+                                                 ctypes.byref(err))
+    return int(v), int(err.value)
+
+
+def DataVerify(pdata_buf, ppseudo_hdr, pseudo_hdr_size):
+    err = ctypes.c_int32(0)
+    v = lib().NetUtil_16BitOnesCplChkSumDataVerify(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size,
+                                                   ctypes.byref(err))
+    return int(v), int(err.value)
+
+
+def chain_to_spans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, dbg=False, max_spans=64):
+    spans = (Span * max_spans)()
+    n = ctypes.c_uint32(0)
+    err = lib().NetUtil_MI355X_ChainToSpans(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size, spans,
+                                            max_spans, ctypes.byref(n), int(dbg))
+    out = [(spans[i].p, spans[i].len) for i in range(n.value)]
+    return out, int(err)
+
+
+def stream_sum32(spans):
+    arr = (Span * max(1, len(spans)))()
+    for i, (p, ln) in enumerate(spans):
+        arr[i].p = p
+        arr[i].len = ln
+    s = ctypes.c_uint32(0)
+    err = lib().NetUtil_MI355X_StreamSum32(arr, len(spans), ctypes.byref(s))
+    return int(s.value), int(err)
+
+
+# --------------------------------------------------------------------------- batch interface
+def batch_strided(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
+                  op=OP_DATA_CALC, stream=None, check=True):
+    err = lib().NetUtil_MI355X_ChkSumBatchStrided(_p(seg), seg_stride, seg_len, _p(pseudo), pseudo_stride,
+                                                  pseudo_len, n_seg, _p(out), op, _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_ChkSumBatchStrided")
+    return err
+
+
+def batch_varlen(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
+                 op=OP_DATA_CALC, stream=None, check=True):
+    err = lib().NetUtil_MI355X_ChkSumBatchVarLen(_p(base), _p(seg_off), _p(seg_len), _p(pseudo), pseudo_stride,
+                                                 pseudo_len, n_seg, _p(out), op, _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_ChkSumBatchVarLen")
+    return err
+
+
+def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
+                       op=OP_DATA_CALC, n_chunks=8, check=True):
+    err = lib().NetUtil_MI355X_ChkSumBatchStridedHost(_p(seg), seg_stride, seg_len, _p(pseudo), pseudo_stride,
+                                                      pseudo_len, n_seg, _p(out), op, n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_ChkSumBatchStridedHost")
+    return err
+
+
+def fill(buf, n_bytes, seed, pattern=0, stream=None):
+    _check(lib().NetUtil_MI355X_Fill(_p(buf), n_bytes, seed, pattern, _stream(stream)), "NetUtil_MI355X_Fill")
+
+
+def read_stream(buf, n_bytes, sink, stream=None):
+    _check(lib().NetUtil_MI355X_ReadStream(_p(buf), n_bytes, _p(sink), _stream(stream)),
+           "NetUtil_MI355X_ReadStream")
+
+
+def tune(key, value):
+    _check(lib().NetUtil_MI355X_Tune(key, value), "NetUtil_MI355X_Tune")
+
+
+def version() -> str:
+    return lib().NetUtil_MI355X_Version().decode()
