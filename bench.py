@@ -52,34 +52,48 @@ def parse():
     return ap.parse_args()
 
 
-def make_c2_batch(torch, netcsum, n, L, plen, rank, dev):
-    """Synthetic C2 shard: segment bytes from the device splitmix64 generator (distinct seed per
-    rank), IPv4 pseudo-headers src/dst from the global segment index, zero, proto 6, BE length."""
-    seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
-    netcsum.fill(seg, n * L, SEED + rank, 0)
-    gidx = torch.arange(n, device=dev, dtype=torch.int64) + rank * n
-    ph = torch.zeros(n, 16, dtype=torch.uint8, device=dev)
+def c2_pseudo_headers(start, n, L, plen):
+    """IPv4 TCP pseudo-headers (net_tcp.h:1545-1551 layout) for global segments [start, start+n):
+    src = 10.x.y.z from the index, dst from a hashed index, zero, protocol 6, big-endian length."""
+    import numpy as np
+    g = np.arange(start, start + n, dtype=np.uint64)
+    h = (g * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
+    ph = np.zeros((n, 12), np.uint8)
     for b in range(4):
-        ph[:, b] = ((gidx >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
-        ph[:, 4 + b] = (((gidx * 2654435761) >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+        ph[:, b] = ((g >> np.uint64(8 * (3 - b))) & np.uint64(0xFF)).astype(np.uint8)
+        ph[:, 4 + b] = ((h >> np.uint64(8 * (3 - b))) & np.uint64(0xFF)).astype(np.uint8)
     ph[:, 0] |= 0x0A
     ph[:, 9] = 6
-    ph[:, 10] = L >> 8
+    ph[:, 10] = (L >> 8) & 0xFF
     ph[:, 11] = L & 0xFF
-    ph = ph[:, :plen].contiguous().reshape(-1)
+    return np.ascontiguousarray(ph[:, :plen]).reshape(-1)
+
+
+def shard_range(rank, n_per_rank):
+    """Weak scaling: rank r owns global segments [r*n, (r+1)*n) of one global synthetic batch."""
+    return rank * n_per_rank, n_per_rank
+
+
+def make_c2_shard(torch, netcsum, start, n, L, plen, dev):
+    """Device-resident C2 shard: segment bytes generated ON the device as the slice
+    [start*L, (start+n)*L) of the global splitmix64 stream; pseudo-headers from the global index."""
+    seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(seg, n * L, SEED, 0, first_byte=start * L)
+    ph = torch.from_numpy(c2_pseudo_headers(start, n, L, plen)).to(dev) if plen else None
     torch.cuda.synchronize()
     return seg, ph
 
 
+def host_c2_shard(oracle, start, n, L, plen):
+    """The same shard regenerated on the host (test / parity use)."""
+    return oracle.fill(start * L, n * L, SEED, 0), (c2_pseudo_headers(start, n, L, plen) if plen else None)
+
+
 def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
     """Oracle (reference C path restatement, gcc -O2) on a bounded sample of the C2 workload."""
-    import numpy as np
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     n = 1 << 16                                                   # 64 Ki segments = 99 MB sample
-    seg = oracle.fill(0, n * L, SEED, 0)
-    ph = np.zeros((n, plen), np.uint8)
-    ph[:, 9 % max(plen, 1)] = 6
-    ph = ph.reshape(-1)
+    seg, ph = host_c2_shard(oracle, 0, n, L, plen)
     oracle.batch_strided(seg, L, L, ph, plen, plen, n, 0, n_threads=threads)   # warm
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -129,7 +143,8 @@ def main():
         netcsum.tune(keymap[k], int(v))
 
     n, L, plen = args.segments, args.seg_len, args.pseudo_len
-    seg, ph = make_c2_batch(torch, netcsum, n, L, plen, rank, dev)
+    start, n = shard_range(rank, n)
+    seg, ph = make_c2_shard(torch, netcsum, start, n, L, plen, dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -206,7 +221,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u16",
-            "data": "synthetic (device splitmix64 bytes, seed 0x5EED0001+rank; IPv4 pseudo-headers from index)",
+            "data": "synthetic (device-generated splitmix64 bytes, seed 0x5EED0001, rank shard = slice of one global stream; IPv4 pseudo-headers from the global index)",
             "config": {"workload": "C2: 1500 B TCP segments + 12 B IPv4 pseudo-header, device-resident, "
                                    "NetUtil_16BitOnesCplChkSumDataCalc per segment",
                        "segments_per_gpu": n, "seg_len": L, "pseudo_len": plen,

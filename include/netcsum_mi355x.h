@@ -164,11 +164,14 @@ NET_ERR  NetUtil_MI355X_ChainToSpans       (const void   *pdata_buf,
                                             uint32_t     *p_n_spans,
                                             int           dbg_chk);
 
-/* Deterministic synthetic bytes, generated on the device: byte k of the buffer is byte (k & 7)
- * of splitmix64(seed + (k >> 3)) for pattern 0; 1 = all 0x00; 2 = all 0xFF; 3 = 0xFF,0xFF,0x00,
- * 0x01 repeating (maximal carries). Asynchronous on hip_stream. */
+/* Deterministic synthetic bytes, generated on the device. Byte k of the buffer is byte g of one
+ * global stream, g = first_byte + k: pattern 0 = byte (g & 7) of splitmix64(seed + (g >> 3));
+ * 1 = all 0x00; 2 = all 0xFF; 3 = 0xFF,0xFF,0x00,0x01 repeating by g (maximal carries). Shards of
+ * one global batch are generated independently per GPU by passing their global byte offset.
+ * d_buf must be 8-byte aligned. Asynchronous on hip_stream. */
 NET_ERR  NetUtil_MI355X_Fill               (void      *d_buf,
                                             uint64_t   n_bytes,
+                                            uint64_t   first_byte,
                                             uint64_t   seed,
                                             int        pattern,
                                             void      *hip_stream);

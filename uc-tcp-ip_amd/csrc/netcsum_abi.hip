@@ -305,7 +305,8 @@ NET_ERR NetUtil_MI355X_StreamSum32(const NETCSUM_SPAN* spans, uint32_t n_spans, 
     return NET_UTIL_ERR_NONE;
 }
 
-NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t seed, int pattern, void* hip_stream) {
+NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern,
+                            void* hip_stream) {
     if (n_bytes == 0) return NET_UTIL_ERR_NONE;
     if (d_buf == nullptr) return NET_ERR_FAULT_NULL_PTR;
     if (((uintptr_t)d_buf & 7u) != 0u || pattern < 0 || pattern > 3) {
@@ -316,7 +317,7 @@ NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t seed, int pa
     const uint64_t words = (n_bytes >> 3) + 1u;
     const uint64_t cap = (uint64_t)cu_count(dev) * 8u;
     const int grid = (int)std::max<uint64_t>(1u, std::min<uint64_t>((words + 255u) / 256u, cap));
-    NC_HIP(netcsum::launch_fill(d_buf, n_bytes, seed, pattern, grid, static_cast<hipStream_t>(hip_stream)));
+    NC_HIP(netcsum::launch_fill(d_buf, n_bytes, first_byte, seed, pattern, grid, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
 

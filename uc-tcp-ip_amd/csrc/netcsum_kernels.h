@@ -31,7 +31,8 @@ struct LaunchCfg {
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s);
-hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t seed, int pattern, int grid, hipStream_t s);
+hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,
+                       hipStream_t s);
 hipError_t launch_read_stream(const void* d_p, uint64_t n16, unsigned long long* d_sink, int grid, bool nt,
                               hipStream_t s);
 

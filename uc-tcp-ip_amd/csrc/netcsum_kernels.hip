@@ -223,24 +223,32 @@ __device__ __forceinline__ uint64_t fill_word(uint64_t w, uint64_t seed, int pat
     switch (pattern) {
     case 1:  return 0ull;
     case 2:  return ~0ull;
-    case 3:  return 0x0100FFFF0100FFFFull;      // bytes FF FF 00 01 FF FF 00 01
+    case 3:  return 0x0100FFFF0100FFFFull;      // bytes FF FF 00 01 FF FF 00 01 (period 4 | 8)
     default: return splitmix64(seed + w);
     }
 }
 
-// buf is 8-byte aligned relative to the global byte index origin (the caller passes the
-// allocation start); full words are stored as u64, the tail byte-wise.
+// The 8 stream bytes starting at global byte g (any alignment), little-endian packed.
+__device__ __forceinline__ uint64_t fill_bytes8(uint64_t g, uint64_t seed, int pattern) {
+    const uint32_t r = (uint32_t)(g & 7u);
+    const uint64_t lo = fill_word(g >> 3, seed, pattern);
+    if (r == 0u) return lo;
+    const uint64_t hi = fill_word((g >> 3) + 1u, seed, pattern);
+    return (lo >> (8u * r)) | (hi << (64u - 8u * r));
+}
+
+// buf must be 8-byte aligned; full 8-byte words are stored as u64, the tail byte-wise.
 __global__ void __launch_bounds__(256) fill_kernel(uint8_t* __restrict__ buf, uint64_t n_bytes,
-                                                   uint64_t seed, int pattern) {
+                                                   uint64_t first_byte, uint64_t seed, int pattern) {
     const uint64_t nw = n_bytes >> 3;
     uint64_t* bw = reinterpret_cast<uint64_t*>(buf);
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw;
          w += (uint64_t)gridDim.x * blockDim.x) {
-        bw[w] = fill_word(w, seed, pattern);
+        bw[w] = fill_bytes8(first_byte + 8u * w, seed, pattern);
     }
     if (blockIdx.x == 0 && threadIdx.x < (n_bytes & 7u)) {
         const uint64_t k = (nw << 3) + threadIdx.x;
-        buf[k] = (uint8_t)(fill_word(nw, seed, pattern) >> (8u * threadIdx.x));
+        buf[k] = (uint8_t)fill_bytes8(first_byte + k, seed, pattern);
     }
 }
 
@@ -324,9 +332,10 @@ hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long
     return hipGetLastError();
 }
 
-hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t seed, int pattern, int grid, hipStream_t s) {
+hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,
+                       hipStream_t s) {
     hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(256), 0, s, static_cast<uint8_t*>(d_buf), n_bytes,
-                       seed, pattern);
+                       first_byte, seed, pattern);
     return hipGetLastError();
 }
 

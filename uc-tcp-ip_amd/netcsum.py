@@ -180,7 +180,7 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
                                               ctypes.POINTER(ctypes.c_uint32), i32]
     L.NetUtil_MI355X_ChainToSpans.restype = i32
-    L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, i32, vp]
+    L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, u64, i32, vp]
     L.NetUtil_MI355X_Fill.restype = i32
     L.NetUtil_MI355X_ReadStream.argtypes = [vp, u64, vp, vp]
     L.NetUtil_MI355X_ReadStream.restype = i32
@@ -293,8 +293,9 @@ def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_l
     return err
 
 
-def fill(buf, n_bytes, seed, pattern=0, stream=None):
-    _check(lib().NetUtil_MI355X_Fill(_p(buf), n_bytes, seed, pattern, _stream(stream)), "NetUtil_MI355X_Fill")
+def fill(buf, n_bytes, seed, pattern=0, stream=None, first_byte=0):
+    _check(lib().NetUtil_MI355X_Fill(_p(buf), n_bytes, first_byte, seed, pattern, _stream(stream)),
+           "NetUtil_MI355X_Fill")
 
 
 def read_stream(buf, n_bytes, sink, stream=None):
