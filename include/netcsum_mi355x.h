@@ -82,7 +82,7 @@ CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumDataVerify(void        *pdata_buf,
  *
  * (HDR ops take no pseudo-header: pass d_pseudo = NULL.) Lengths are CPU_INT16U as in the
  * reference (net_util.c:1617,1628: per-buffer data_len is 16-bit). The call is asynchronous
- * on `hip_stream`; returns NET_UTIL_ERR_NONE when the launch was queued.
+ * on `hip_stream`; returns NET_UTIL_ERR_NONE when the launch was queued. n_seg <= 2^31 - 1.
  * ============================================================================================ */
 typedef enum netcsum_op {
     NETCSUM_OP_DATA_CALC   = 0,
@@ -186,10 +186,16 @@ NET_ERR  NetUtil_MI355X_ReadStream         (const void *d_buf,
 
 /* Launch tuning knobs (process-wide; 0 = automatic). */
 typedef enum netcsum_tune_key {
-    NETCSUM_TUNE_GRID_BLOCKS   = 1,   /* workgroups per launch (0: derived from the CU count)    */
+    NETCSUM_TUNE_GRID_BLOCKS   = 1,   /* workgroups per launch (0: exactly fill the chip)        */
     NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */
     NETCSUM_TUNE_NT_LOADS      = 3,   /* 1: non-temporal loads on the segment stream             */
-    NETCSUM_TUNE_BLOCK_THREADS = 4    /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
+    NETCSUM_TUNE_BLOCK_THREADS = 4,   /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
+    NETCSUM_TUNE_KERNEL        = 5,   /* 1 simple, 2 pipelined register loads, 3 pipelined LDS-DMA */
+    NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
+    NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA           */
+    NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
+    NETCSUM_TUNE_TILE          = 9    /* J > 0: each block owns a contiguous tile of J segments per
+                                         group (grid = tiles); 0: persistent grid-stride          */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -107,3 +107,19 @@ def test_header_is_plain_c():
     r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-pedantic", "-I", inc, "-x", "c", "-",
                         "-fsyntax-only"], input=src, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_binding_rejects_undersized_buffers_before_launch():
+    """Host-side shape checks: an undersized tensor never reaches a kernel."""
+    import numpy as np
+    seg = np.zeros(1000, np.uint8)
+    out = np.zeros(10, np.uint16)
+    with pytest.raises(ValueError):
+        netcsum.batch_strided(seg, 100, 100, None, 0, 0, 11, out, 0, stream=0)      # 1100 B > 1000
+    with pytest.raises(ValueError):
+        netcsum.batch_strided(seg, 100, 100, None, 0, 0, 10, out[:9], 0, stream=0)  # out too small
+    ph = np.zeros(100, np.uint8)
+    with pytest.raises(ValueError):
+        netcsum.batch_strided(seg, 100, 100, ph, 12, 12, 10, out, 0, stream=0)      # 120 B pseudo > 100
+    with pytest.raises(ValueError):
+        netcsum.batch_varlen(seg, np.zeros(9, np.uint64), np.zeros(10, np.uint16), None, 0, 0, 10, out, 0, stream=0)

@@ -22,7 +22,8 @@ DEV = "cuda"
 
 
 def _reset_tuning():
-    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES, netcsum.TUNE_NT_LOADS, netcsum.TUNE_BLOCK_THREADS):
+    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES, netcsum.TUNE_NT_LOADS, netcsum.TUNE_BLOCK_THREADS,
+              netcsum.TUNE_KERNEL, netcsum.TUNE_CHUNKS, netcsum.TUNE_TILE, netcsum.TUNE_GRID_MULT):
         netcsum.tune(k, 0)
 
 
@@ -87,15 +88,20 @@ def test_strided_matrix_vs_oracle(L):
                         assert np.array_equal(got, want), (L, pattern, stride, base_off, plen, op)
 
 
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 @pytest.mark.parametrize("group", [1, 4, 8, 16, 32, 64])
-@pytest.mark.parametrize("nt", [0, 1])
-def test_every_group_width_and_load_policy(group, nt):
-    """Force each lane-group width / nt policy and a tiny grid (deep grid-stride loops)."""
+@pytest.mark.parametrize("nt,chunks,tile", [(0, 0, 0), (1, 0, 3), (0, 1, 1), (1, 8, 0), (1, 6, 7)])
+def test_every_group_width_and_load_policy(kernel, group, nt, chunks, tile):
+    """Force each kernel form, lane-group width, chunks-per-pass and nt policy, with a tiny grid
+    (deep grid-stride loops, multi-pass segments, pipelined stages running past the end)."""
     rng = np.random.default_rng(group * 2 + nt)
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
     netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+    netcsum.tune(netcsum.TUNE_CHUNKS, chunks)
+    netcsum.tune(netcsum.TUNE_TILE, tile)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 3)
-    for L, stride in ((1500, 1500), (20, 20), (4519, 4523), (77, 80)):
+    for L, stride in ((1500, 1500), (20, 20), (4519, 4523), (77, 80), (0, 5), (1, 1)):
         n = 700
         data = rng.integers(0, 256, size=n * stride + 64, dtype=np.uint8)
         ph = rng.integers(0, 256, size=n * 12 + 16, dtype=np.uint8)
@@ -103,7 +109,18 @@ def test_every_group_width_and_load_policy(group, nt):
         for op in (0, 1):
             got = _gpu_strided(data_d, 1, stride, L, ph_d.data_ptr(), 12, 12, n, op)
             want = oracle.batch_strided(data, stride, L, ph, 12, 12, n, op, seg_offset=1)
-            assert np.array_equal(got, want), (group, nt, L, op)
+            assert np.array_equal(got, want), (kernel, group, nt, chunks, tile, L, op)
+    # variable-length + long pseudo-header (> 16*G-15 B exercises the extra pseudo pass)
+    base, off, lens, _ = _packed_udp(rng, 300, 0, 3000)
+    ph = rng.integers(0, 256, size=300 * 1100 + 64, dtype=np.uint8)
+    b_d, o_d = torch.from_numpy(base).to(DEV), torch.from_numpy(off.view(np.int64)).to(DEV)
+    l_d, p_d = torch.from_numpy(lens.view(np.int16)).to(DEV), torch.from_numpy(ph).to(DEV)
+    for plen, pst in ((1033, 1100), (40, 41)):
+        out = _out(300, 0)
+        netcsum.batch_varlen(b_d, o_d, l_d, p_d.data_ptr() + 3, pst, plen, 300, out, 0)
+        torch.cuda.synchronize()
+        want = oracle.batch_varlen(base, off, lens, ph[3:], pst, plen, 0)
+        assert np.array_equal(_np_out(out), want), (kernel, group, plen)
 
 
 def _packed_udp(rng, n, lo=40, hi=9000, pattern="random"):

@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Launch-geometry sweep for the checksum kernels and the read-stream probe (GPU box only).
+
+Interleaves variants in ONE process (cdna_hip_programming.md §5.4 rule 24) and prints the
+median/min HIP-event time per variant as JSON lines. Config: C2 (1 M x 1500 B + 12 B pseudo) by
+default; --c3 adds 16 M x 20 B headers, --c4 adds 1 M packed 40-9000 B UDP datagrams.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "uc-tcp-ip_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import netcsum  # noqa: E402
+from bench import SEED, c2_pseudo_headers  # noqa: E402
+
+
+def timeit(fn, stream, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) for a, b in ev]
+    return statistics.median(ts), min(ts)
+
+
+def set_tune(grid=0, group=0, nt=0, block=0, kernel=0, k=0, probe=0, mult=0, tile=0):
+    netcsum.tune(netcsum.TUNE_GRID_MULT, mult)
+    netcsum.tune(netcsum.TUNE_TILE, tile)
+    netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+    netcsum.tune(netcsum.TUNE_BLOCK_THREADS, block)
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
+    netcsum.tune(netcsum.TUNE_CHUNKS, k)
+    netcsum.tune(netcsum.TUNE_PROBE, probe)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c3", action="store_true")
+    ap.add_argument("--c4", action="store_true")
+    ap.add_argument("--rounds", type=int, default=2)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n, L = 1 << 20, 1500
+    seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(seg, n * L, SEED, 0)
+    ph = torch.from_numpy(c2_pseudo_headers(0, n, L, 12)).to(dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    sink = torch.zeros(1, dtype=torch.int64, device=dev)
+    n16 = n * L // 16 * 16
+    algo = n * (L + 12 + 2)
+
+    variants = []
+    for probe in (0, 1):
+        variants.append(("read", dict(grid=8192, nt=1, probe=probe)))
+    for kernel, group, k in ((2, 16, 6), (3, 16, 6), (2, 32, 3), (3, 32, 3), (2, 64, 2), (3, 64, 2)):
+        variants.append(("c2", dict(kernel=kernel, group=group, k=k, nt=1, grid=16384)))
+        for tile in (1, 2, 4, 8, 16):
+            variants.append(("c2", dict(kernel=kernel, group=group, k=k, nt=1, tile=tile)))
+    res = {}
+    for r in range(args.rounds):
+        for kind, kw in variants:
+            set_tune(**kw)
+            if kind == "read":
+                fn = lambda: netcsum.read_stream(seg, n16, sink, stream=st)  # noqa: E731
+                byts = n16
+            else:
+                fn = lambda: netcsum.batch_strided(seg, L, L, ph, 12, 12, n, out, 0, stream=st)  # noqa: E731
+                byts = algo
+            med, mn = timeit(fn, st)
+            key = json.dumps([kind, kw], sort_keys=True)
+            res.setdefault(key, []).append((med, mn, byts))
+    set_tune()
+    for key, v in res.items():
+        med = statistics.median(x[0] for x in v)
+        mn = min(x[1] for x in v)
+        byts = v[0][2]
+        print(json.dumps({"variant": json.loads(key), "ms_med": round(med, 4), "ms_min": round(mn, 4),
+                          "GBps_med": round(byts / med / 1e6, 1), "GBps_best": round(byts / mn / 1e6, 1)}), flush=True)
+
+    if args.c3:
+        nh = 1 << 24
+        hdr = torch.empty(nh * 20 + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(hdr, nh * 20, SEED, 0)
+        o3 = torch.empty(nh, dtype=torch.int16, device=dev)
+        for kernel, group, k, nt in ((2, 1, 2, 0), (2, 1, 2, 1), (3, 1, 2, 1)):
+            for grid, tile in ((8192, 0), (0, 1), (0, 2), (0, 4), (0, 8)):
+                set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=nt, tile=tile)
+                med, mn = timeit(lambda: netcsum.batch_strided(hdr, 20, 20, None, 0, 0, nh, o3, 2, stream=st), st)
+                b = nh * (20 + 2)
+                print(json.dumps({"variant": ["c3", dict(kernel=kernel, group=group, k=k, nt=nt, grid=grid, tile=tile)], "ms_med": round(med, 4),
+                                  "GBps_med": round(b / med / 1e6, 1), "Mhdr_per_s": round(nh / med / 1e3, 1)}),
+                      flush=True)
+        set_tune()
+    if args.c4:
+        rng = np.random.default_rng(7)
+        nv = 1 << 20
+        lens = rng.integers(40, 9001, size=nv).astype(np.uint16)
+        off = np.zeros(nv, np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        tot = int(off[-1]) + int(lens[-1])
+        base = torch.empty(tot + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(base, tot, SEED, 0)
+        off_d = torch.from_numpy(off.view(np.int64)).to(dev)
+        len_d = torch.from_numpy(lens.view(np.int16)).to(dev)
+        ph4 = torch.zeros(nv * 12, dtype=torch.uint8, device=dev)
+        o4 = torch.empty(nv, dtype=torch.int16, device=dev)
+        for kernel, group, k in ((2, 32, 6), (3, 32, 4), (2, 64, 4), (3, 64, 4)):
+            for grid, tile in ((16384, 0), (0, 1), (0, 2), (0, 4)):
+                set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=1, tile=tile)
+                med, mn = timeit(lambda: netcsum.batch_varlen(base, off_d, len_d, ph4, 12, 12, nv, o4, 0, stream=st), st)
+                b = tot + nv * (12 + 2)
+                print(json.dumps({"variant": ["c4", dict(kernel=kernel, group=group, k=k, grid=grid, tile=tile)], "ms_med": round(med, 4),
+                                  "GBps_med": round(b / med / 1e6, 1), "GiBps_checksummed": round((tot + 12 * nv) / med / 1e6 / 1.073741824, 1)}),
+                      flush=True)
+        set_tune()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,6 +24,11 @@ std::atomic<int> g_tune_grid{0};
 std::atomic<int> g_tune_group{0};
 std::atomic<int> g_tune_nt{0};
 std::atomic<int> g_tune_block{256};
+std::atomic<int> g_tune_kernel{2};
+std::atomic<int> g_tune_chunks{0};
+std::atomic<int> g_tune_probe{0};
+std::atomic<int> g_tune_grid_mult{1};
+std::atomic<int> g_tune_tile{0};
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -61,6 +66,14 @@ int pow2_group(uint32_t want) {                     // smallest supported group 
     return 64;
 }
 
+int chunk_slots(uint32_t want) {                    // smallest supported K >= want
+    static const int ks[] = {1, 2, 3, 4, 6, 8};
+    for (int k : ks) {
+        if ((uint32_t)k >= want) return k;
+    }
+    return 8;
+}
+
 // Geometry policy. len_hint = typical segment length in bytes (0 = unknown / variable).
 netcsum::LaunchCfg choose_cfg(int dev, uint32_t len_hint, uint32_t n_seg, bool varlen) {
     netcsum::LaunchCfg c{};
@@ -68,23 +81,28 @@ netcsum::LaunchCfg choose_cfg(int dev, uint32_t len_hint, uint32_t n_seg, bool v
     if (c.block < 64 || c.block > 1024 || (c.block & 63)) c.block = 256;
     c.nt = g_tune_nt.load() != 0;
 
-    const uint32_t chunks = varlen ? 256u : (len_hint / 16u + 2u);   // incl. misaligned edges
+    c.kernel = g_tune_kernel.load();
+    // chunks per segment incl. misaligned edges; variable lengths assume the C4 mean (~4.5 KB)
+    const uint32_t chunks = varlen ? 288u : (len_hint / 16u + 2u);
+    const uint32_t kmax = (c.kernel == 2) ? 8u : 4u;
     int g = g_tune_group.load();
     if (g == 0) {
-        g = varlen ? 64 : pow2_group((chunks + 3u) / 4u);
+        g = varlen ? 64 : pow2_group((chunks + kmax - 1u) / kmax);
     }
     g = pow2_group((uint32_t)g);
     c.group_lanes = g;
-    int k = (int)std::min<uint32_t>(4u, std::max<uint32_t>(1u, (chunks + (uint32_t)g - 1u) / (uint32_t)g));
+    int k = g_tune_chunks.load();
+    if (k == 0) {
+        k = chunk_slots(std::min<uint32_t>(kmax, std::max<uint32_t>(1u, (chunks + (uint32_t)g - 1u) / (uint32_t)g)));
+    }
     c.chunks_per_pass = k;
 
     const uint32_t gpb = (uint32_t)(c.block / g);
-    const uint64_t blocks_needed = ((uint64_t)n_seg + gpb - 1u) / gpb;
-    int grid = g_tune_grid.load();
-    if (grid <= 0) {
-        const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)(2048 / c.block);   // full residency
-        grid = (int)std::max<uint64_t>(1u, std::min<uint64_t>(blocks_needed, cap));
-    }
+    c.blocks_needed = ((uint64_t)n_seg + gpb - 1u) / gpb;
+    c.cus = cu_count(dev);
+    c.grid_mult = g_tune_grid_mult.load();
+    c.tile = g_tune_tile.load();
+    int grid = g_tune_grid.load();                     // <= 0: residency-exact persistent grid
     c.grid = grid;
     return c;
 }
@@ -160,6 +178,7 @@ NET_ERR NetUtil_MI355X_ChkSumBatchStrided(const void* d_seg, uint64_t seg_stride
     NET_ERR e = check_op(op, d_pseudo, pseudo_len);
     if (e != NET_UTIL_ERR_NONE) return e;
     if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (n_seg > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_out == nullptr || (d_seg == nullptr && seg_len != 0)) return NET_ERR_FAULT_NULL_PTR;
     netcsum::SegBatchArgs a{};
     a.base = static_cast<const uint8_t*>(d_seg);
@@ -180,6 +199,7 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLen(const void* d_base, const uint64_t* d_s
     NET_ERR e = check_op(op, d_pseudo, pseudo_len);
     if (e != NET_UTIL_ERR_NONE) return e;
     if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (n_seg > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_out == nullptr || d_base == nullptr || d_seg_off == nullptr || d_seg_len == nullptr) {
         return NET_ERR_FAULT_NULL_PTR;
     }
@@ -330,7 +350,7 @@ NET_ERR NetUtil_MI355X_ReadStream(const void* d_buf, uint64_t n_bytes, uint64_t*
     int grid = g_tune_grid.load();
     if (grid <= 0) grid = cu_count(dev) * 8;
     NC_HIP(netcsum::launch_read_stream(d_buf, n_bytes / 16u, reinterpret_cast<unsigned long long*>(d_sink), grid,
-                                       g_tune_nt.load() != 0, static_cast<hipStream_t>(hip_stream)));
+                                       g_tune_nt.load() != 0, static_cast<hipStream_t>(hip_stream), g_tune_probe.load()));
     return NET_UTIL_ERR_NONE;
 }
 
@@ -348,6 +368,28 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_NT_LOADS:
         g_tune_nt.store(value != 0);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_KERNEL:
+        if (value < 0 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_kernel.store(value == 0 ? 2 : value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CHUNKS:
+        if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4 || value == 6 || value == 8)) {
+            return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        }
+        g_tune_chunks.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_GRID_MULT:
+        if (value < 0 || value > 64) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_grid_mult.store(value == 0 ? 1 : value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_TILE:
+        if (value < 0 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_tile.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_PROBE:
+        if (value != 0 && value != 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_probe.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:
         if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)

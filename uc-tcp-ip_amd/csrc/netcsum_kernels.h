@@ -17,15 +17,22 @@ struct SegBatchArgs {
     uint32_t        pseudo_len;
     uint32_t        n_seg;
     uint32_t        verify;        // 0: u16 checksum out, 1: u8 DEF_OK/DEF_FAIL out
+    uint32_t        tile;          // 0: grid-stride; J > 0: block b owns segments [b*gpb*J, (b+1)*gpb*J)
     void*           out;
 };
 
 struct LaunchCfg {
-    int  grid;             // workgroups
+    int  grid;             // workgroups; <= 0: fill the chip exactly (resident blocks x CUs x grid_mult)
+    int  grid_mult;        // residency multiple used when grid <= 0
+    int  cus;              // compute units of the device
+    uint64_t blocks_needed;  // upper bound: one group per segment
     int  block;            // threads per workgroup (multiple of 64)
     int  group_lanes;      // lanes per segment: 1, 4, 8, 16, 32, 64
     int  chunks_per_pass;  // 16-B chunks per lane per pass: 1..4
     bool nt;               // non-temporal segment loads
+    int  kernel;           // 1: seg_batch_kernel (one segment in flight per group), 2: seg_pipe_kernel,
+                           // 3: seg_lds_kernel
+    int  tile;             // segments per group per block in tile mode (0 = grid-stride)
 };
 
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
@@ -34,6 +41,6 @@ hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,
                        hipStream_t s);
 hipError_t launch_read_stream(const void* d_p, uint64_t n16, unsigned long long* d_sink, int grid, bool nt,
-                              hipStream_t s);
+                              hipStream_t s, int variant);
 
 }  // namespace netcsum

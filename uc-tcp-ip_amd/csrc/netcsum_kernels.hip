@@ -127,6 +127,32 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
     return s;
 }
 
+// Segment -> group mapping. Tile mode (P.tile = J > 0): block b owns the contiguous tile
+// [b*gpb*J, (b+1)*gpb*J) and its gpb groups step through it gpb segments at a time, so the blocks
+// in flight (dispatched in order) read one contiguous, advancing window of HBM. Grid-stride mode
+// (P.tile = 0): group i handles i, i + G_total, ... (persistent grids).
+struct SegRange {
+    uint32_t first;
+    uint32_t step;
+    uint32_t end;
+};
+
+__device__ __forceinline__ SegRange seg_range(const SegBatchArgs& P, uint32_t gpb, uint32_t grp) {
+    SegRange r;
+    if (P.tile) {
+        const uint64_t t0 = (uint64_t)blockIdx.x * gpb * P.tile;
+        const uint64_t t1 = t0 + (uint64_t)gpb * P.tile;
+        r.first = (uint32_t)(t0 + grp);
+        r.step = gpb;
+        r.end = (uint32_t)(t1 < P.n_seg ? t1 : P.n_seg);
+    } else {
+        r.first = blockIdx.x * gpb + grp;
+        r.step = gridDim.x * gpb;
+        r.end = P.n_seg;
+    }
+    return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Segment batch kernel. out[i] per NETCSUM_OP (include/netcsum_mi355x.h (2)).
 // ---------------------------------------------------------------------------------------------
@@ -134,11 +160,11 @@ template <int G, int K, bool VARLEN, bool NT>
 __global__ void __launch_bounds__(256) seg_batch_kernel(SegBatchArgs P) {
     const int      lane   = (int)(threadIdx.x & (G - 1));
     const uint32_t gpb    = blockDim.x / G;
-    const uint32_t step   = gridDim.x * gpb;
     const bool     has_ph = (P.pseudo != nullptr) && (P.pseudo_len != 0u);
     const bool     ph_odd = (P.pseudo_len & 1u) != 0u;
 
-    for (uint32_t seg = blockIdx.x * gpb + threadIdx.x / G; seg < P.n_seg; seg += step) {
+    const SegRange R = seg_range(P, gpb, threadIdx.x / G);
+    for (uint32_t seg = R.first; seg < R.end; seg += R.step) {
         uint64_t off;
         uint32_t len;
         if constexpr (VARLEN) {
@@ -170,6 +196,430 @@ __global__ void __launch_bounds__(256) seg_batch_kernel(SegBatchArgs P) {
                 static_cast<uint16_t*>(P.out)[seg] = (uint16_t)(~s);
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// v2: software-pipelined segment batch kernel.
+//
+// Each group keeps TWO segments in flight: while it masks, sums, folds and stores segment i, the
+// K chunk loads (+ its pseudo-header chunk) of segment i+step are already issued. All loads are
+// unconditional — a chunk slot past the end of its span reads a 16-byte zero chunk that lives in
+// this code object (always mapped, L1/L2 resident) — so every load sits in straight-line code and
+// the compiler's counted s_waitcnt vmcnt(N) waits only for the stage being consumed. For
+// variable-length batches the (offset, length) descriptors are prefetched two segments ahead and
+// issued BEFORE the data loads they gate, so waiting for a descriptor never drains the data
+// stream (vmcnt retires in issue order).
+// ---------------------------------------------------------------------------------------------
+__device__ u32x4 g_zero_chunk[4];
+
+__device__ __forceinline__ uintptr_t zero_addr() {
+    return reinterpret_cast<uintptr_t>(&g_zero_chunk[0]);
+}
+
+template <int K>
+struct SegStage {
+    u32x4    v[K];
+    u32x4    pv;
+    uint32_t lead;      // segment start offset inside its first 16-B chunk (bit 0 = address parity)
+    uint32_t len;
+    uint32_t plead;     // same for the pseudo-header
+    uint32_t plen;      // pseudo-header bytes of THIS stage (0 for a dummy / past-the-end stage)
+};
+
+__device__ __forceinline__ uint32_t span_chunks(uintptr_t a, uint32_t len) {
+    return len ? (uint32_t)((a + len - (a & ~(uintptr_t)15) + 15) >> 4) : 0u;
+}
+
+template <int G, int K, bool NT>
+__device__ __forceinline__ void stage_issue(SegStage<K>& st, uintptr_t a, uint32_t len, uintptr_t pa,
+                                            uint32_t plen, int lane) {
+    st.lead = (uint32_t)(a & 15u);
+    st.len = len;
+    st.plead = (uint32_t)(pa & 15u);
+    st.plen = plen;
+    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uint32_t nch = (len + st.lead + 15u) >> 4;            // 0 when len == 0 (lead < 16)
+    const uintptr_t z = zero_addr();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        const uintptr_t addr = (c < nch) ? (q0 + 16u * (uintptr_t)c) : z;
+        st.v[k] = load16<NT>(reinterpret_cast<gu32x4*>(addr));
+    }
+    const uint32_t pnch = (plen + st.plead + 15u) >> 4;
+    const uintptr_t paddr = ((uint32_t)lane < pnch) ? ((pa & ~(uintptr_t)15) + 16u * (uintptr_t)lane) : z;
+    st.pv = load16<false>(reinterpret_cast<gu32x4*>(paddr));
+}
+
+// Mask chunk c of a span given in span-relative terms: the span covers bytes [lead, rend) of its
+// 16-B-aligned chunk sequence (rend = lead + len). 32-bit arithmetic only.
+__device__ __forceinline__ u32x4 edge_mask_rel(u32x4 v, uint32_t c, uint32_t lead, uint32_t rend) {
+    const uint32_t q = 16u * c;
+    const int lo = (c == 0u) ? (int)lead : 0;
+    const int hi = (rend - q < 16u) ? (int)(rend - q) : 16;
+    if (lo != 0 || hi != 16) {
+        v = mask_chunk(v, lo, hi);
+    }
+    return v;
+}
+
+// Folded 16-bit contribution of (pseudo ‖ segment) held by this lane, stream parity applied.
+// `a`/`pa` (full addresses) are only needed for passes beyond the pipelined first one.
+// Every address touched here derives from the STAGE's own (len, plen): a dummy stage (len = plen = 0)
+// reads nothing beyond its zero-chunk slots.
+template <int G, int K, bool NT>
+__device__ __forceinline__ uint32_t stage_consume(const SegStage<K>& st, uintptr_t a, uintptr_t pa,
+                                                  bool ph_odd, int lane) {
+    const uint32_t plen = st.plen;
+    const uint32_t lead = st.lead;
+    const uint32_t rend = lead + st.len;
+    const uint32_t nch = (rend + 15u) >> 4;
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        u32x4 v = st.v[k];
+        if (c < nch) {
+            v = edge_mask_rel(v, c, lead, rend);
+        }
+        acc = sum4(v, acc);
+    }
+    if (nch > (uint32_t)(G * K)) {                   // segments longer than one pass
+        const uintptr_t q0 = a & ~(uintptr_t)15;
+        for (uint32_t c0 = (uint32_t)(G * K); c0 < nch; c0 += (uint32_t)(G * K)) {
+            u32x4 w[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * G + lane);
+                const uintptr_t addr = (c < nch) ? (q0 + 16u * (uintptr_t)c) : zero_addr();
+                w[k] = load16<NT>(reinterpret_cast<gu32x4*>(addr));
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * G + lane);
+                u32x4 v = w[k];
+                if (c < nch) {
+                    v = edge_mask_rel(v, c, lead, rend);
+                }
+                acc = sum4(v, acc);
+            }
+        }
+    }
+    uint32_t s = fold16(acc);
+    if (((lead & 1u) != 0u) != ph_odd) {
+        s = rot8(s);
+    }
+    if (plen != 0u) {
+        const uint32_t plead = st.plead;
+        const uint32_t prend = plead + plen;
+        const uint32_t pnch = (prend + 15u) >> 4;
+        u32x4 v = st.pv;
+        if ((uint32_t)lane < pnch) {
+            v = edge_mask_rel(v, (uint32_t)lane, plead, prend);
+        }
+        uint32_t pacc = sum4(v, 0u);
+        if (pnch > (uint32_t)G) {                    // pseudo-header longer than 16*G - 15 B
+            const uintptr_t pq0 = pa & ~(uintptr_t)15;
+            for (uint32_t c = (uint32_t)(lane + G); c < pnch; c += (uint32_t)G) {
+                const u32x4 w = load16<false>(reinterpret_cast<gu32x4*>(pq0 + 16u * (uintptr_t)c));
+                pacc = sum4(edge_mask_rel(w, c, plead, prend), pacc);
+            }
+        }
+        uint32_t ps = fold16(pacc);
+        if (plead & 1u) {
+            ps = rot8(ps);
+        }
+        s += ps;
+    }
+    return s;
+}
+
+template <int G>
+__device__ __forceinline__ void group_store(const SegBatchArgs& P, uint32_t seg, uint32_t s, int lane) {
+    s = fold16(group_sum<G>(s));
+    if (lane == 0) {
+        if (P.verify) {
+            static_cast<uint8_t*>(P.out)[seg] = (s == 0xFFFFu) ? 1u : 0u;
+        } else {
+            static_cast<uint16_t*>(P.out)[seg] = (uint16_t)(~s);
+        }
+    }
+}
+
+template <bool VARLEN>
+struct SegDesc {
+    uint64_t off;
+    uint32_t len;
+};
+
+template <bool VARLEN>
+__device__ __forceinline__ SegDesc<VARLEN> seg_desc(const SegBatchArgs& P, uint32_t seg) {
+    SegDesc<VARLEN> d;
+    if constexpr (VARLEN) {
+        const uint32_t sc = (seg < P.n_seg) ? seg : 0u;          // clamped, branch-free prefetch
+        d.off = P.seg_off[sc];
+        d.len = P.seg_len_v[sc];
+    } else {
+        d.off = (uint64_t)seg * P.seg_stride;
+        d.len = P.seg_len;
+    }
+    return d;
+}
+
+template <int G, int K, bool VARLEN, bool NT>
+__global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
+    const int      lane = (int)(threadIdx.x & (G - 1));
+    const uint32_t gpb  = blockDim.x / G;
+    const uint32_t plen = (P.pseudo != nullptr) ? P.pseudo_len : 0u;
+    const bool     ph_odd = (plen & 1u) != 0u;
+    const uintptr_t base = (uintptr_t)P.base;
+    const uintptr_t pbase = (uintptr_t)P.pseudo;
+    const uintptr_t z = zero_addr();
+
+    const SegRange R = seg_range(P, gpb, threadIdx.x / G);
+    const uint32_t step = R.step;
+    uint32_t seg = R.first;
+    if (seg >= R.end) {
+        return;
+    }
+    SegStage<K> A, B;
+    SegDesc<VARLEN> dn = seg_desc<VARLEN>(P, seg);
+    SegDesc<VARLEN> dnn = seg_desc<VARLEN>(P, seg + step);      // two ahead
+    uintptr_t aA = base + dn.off, paA = pbase + (uint64_t)seg * P.pseudo_stride;
+    uintptr_t aB = z, paB = z;
+    stage_issue<G, K, NT>(A, aA, dn.len, paA, plen, lane);
+    dn = dnn;
+    for (;;) {
+        // ---- consume A (segment `seg`) with B (seg + step) in flight. Past the end, B reads the
+        //      zero chunk: branch-free issue keeps the compiler's vmcnt counting exact.
+        uint32_t nxt = seg + step;
+        bool has_next = nxt < R.end;
+        dnn = seg_desc<VARLEN>(P, nxt + step);
+        aB = has_next ? base + dn.off : z;
+        paB = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        stage_issue<G, K, NT>(B, aB, has_next ? dn.len : 0u, paB, has_next ? plen : 0u, lane);
+        dn = dnn;
+        group_store<G>(P, seg, stage_consume<G, K, NT>(A, aA, paA, ph_odd, lane), lane);
+        if (!has_next) {
+            break;
+        }
+        seg = nxt;
+        // ---- consume B with A in flight
+        nxt = seg + step;
+        has_next = nxt < R.end;
+        dnn = seg_desc<VARLEN>(P, nxt + step);
+        aA = has_next ? base + dn.off : z;
+        paA = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        stage_issue<G, K, NT>(A, aA, has_next ? dn.len : 0u, paA, has_next ? plen : 0u, lane);
+        dn = dnn;
+        group_store<G>(P, seg, stage_consume<G, K, NT>(B, aB, paB, ph_odd, lane), lane);
+        if (!has_next) {
+            break;
+        }
+        seg = nxt;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// v3: the v2 pipeline with the segment stream moved onto LDS-DMA.
+//
+// Segment chunks are fetched by global_load_lds_dwordx4 (per-lane source address = the same
+// clamped chunk addressing as v2; destination = this wave's slot in an LDS ring, lane i's 16 B at
+// slot + 16*i) with the non-temporal policy, and read back by the same lane with ds_read_b128
+// (conflict-free: 64 consecutive 16-B slots). On gfx950 this path streams HBM measurably faster
+// than register-destination loads (bench: read_stream_lds probe vs read_stream probe). The
+// pseudo-header chunk rides in slot K the same way, so no VGPR-destination load is ever in flight
+// across an iteration (a pending VGPR load whose register the allocator re-uses forces a full
+// vmcnt(0) drain). Nothing orders a ds_read behind an LDS-DMA except the issuing wave's vmcnt, so
+// the waits are hand-counted: every stage issues exactly K+1 DMA, and consuming stage X while
+// stage Y (issued after X) is in flight waits vmcnt(K+1) — conservative if anything else (stores,
+// descriptor loads) was issued after Y.
+// LDS: 2 stages x (K+1) slots x 1 KiB per wave.
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 9, "extend wait_vmcnt");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int K>
+struct LdsStage {
+    uint32_t lead;
+    uint32_t len;
+    uint32_t plead;
+    uint32_t plen;
+};
+
+template <int G, int K, bool NT>
+__device__ __forceinline__ void lds_stage_issue(LdsStage<K>& st, u32x4 (*slots)[64], uintptr_t a, uint32_t len,
+                                                uintptr_t pa, uint32_t plen, int lane) {
+    st.lead = (uint32_t)(a & 15u);
+    st.len = len;
+    st.plead = (uint32_t)(pa & 15u);
+    st.plen = plen;
+    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uint32_t nch = (len + st.lead + 15u) >> 4;
+    const uintptr_t z = zero_addr();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // prior ds_reads of these slots done
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        const uintptr_t addr = (c < nch) ? (q0 + 16u * (uintptr_t)c) : z;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(addr),
+                                         (lds_void*)(&slots[k][0]), 16, 0, NT ? 2 : 0);
+    }
+    const uint32_t pnch = (plen + st.plead + 15u) >> 4;
+    const uintptr_t paddr = ((uint32_t)lane < pnch) ? ((pa & ~(uintptr_t)15) + 16u * (uintptr_t)lane) : z;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const __attribute__((address_space(1))) void*>(paddr),
+                                     (lds_void*)(&slots[K][0]), 16, 0, 0);
+}
+
+template <int G, int K, bool NT>
+__device__ __forceinline__ uint32_t lds_stage_consume(const LdsStage<K>& st, u32x4 (*slots)[64], uintptr_t a,
+                                                      uintptr_t pa, bool ph_odd, int lane, int lane64) {
+    SegStage<K> r;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        r.v[k] = slots[k][lane64];
+    }
+    r.pv = slots[K][lane64];
+    r.lead = st.lead;
+    r.len = st.len;
+    r.plead = st.plead;
+    r.plen = st.plen;
+    return stage_consume<G, K, NT>(r, a, pa, ph_odd, lane);
+}
+
+template <int G, int K, bool VARLEN, bool NT>
+__global__ void __launch_bounds__(256) seg_lds_kernel(SegBatchArgs P) {
+    __shared__ u32x4 ring[4][2][K + 1][64];
+    const int      w = (int)(threadIdx.x >> 6);
+    const int      lane64 = (int)(threadIdx.x & 63);
+    const int      lane = (int)(threadIdx.x & (G - 1));
+    const uint32_t gpb  = blockDim.x / G;
+    const uint32_t plen = (P.pseudo != nullptr) ? P.pseudo_len : 0u;
+    const bool     ph_odd = (plen & 1u) != 0u;
+    const uintptr_t base = (uintptr_t)P.base;
+    const uintptr_t pbase = (uintptr_t)P.pseudo;
+    const uintptr_t z = zero_addr();
+    u32x4 (*sA)[64] = ring[w][0];
+    u32x4 (*sB)[64] = ring[w][1];
+
+    const SegRange R = seg_range(P, gpb, threadIdx.x / G);
+    const uint32_t step = R.step;
+    uint32_t seg = R.first;
+    // Groups of one wave may run out of segments at different iterations; a finished group keeps
+    // issuing zero-chunk stages (len 0) so every lane of the wave executes the same DMA sequence
+    // and the hand-counted waits stay exact, and leaves only when the whole wave is done.
+    const SegRange Rw = seg_range(P, gpb, (uint32_t)(w * 64) / G);
+    if (Rw.first >= Rw.end) {
+        return;
+    }
+    LdsStage<K> A, B;
+    bool live = seg < R.end;
+    SegDesc<VARLEN> dn = seg_desc<VARLEN>(P, seg);
+    SegDesc<VARLEN> dnn = seg_desc<VARLEN>(P, seg + step);
+    uintptr_t aA = live ? base + dn.off : z, paA = live ? pbase + (uint64_t)seg * P.pseudo_stride : z;
+    uintptr_t aB = z, paB = z;
+    lds_stage_issue<G, K, NT>(A, sA, aA, live ? dn.len : 0u, paA, live ? plen : 0u, lane);
+    dn = dnn;
+    for (;;) {
+        uint32_t nxt = seg + step;
+        bool has_next = nxt < R.end;
+        dnn = seg_desc<VARLEN>(P, nxt + step);
+        aB = has_next ? base + dn.off : z;
+        paB = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        lds_stage_issue<G, K, NT>(B, sB, aB, has_next ? dn.len : 0u, paB, has_next ? plen : 0u, lane);
+        dn = dnn;
+        wait_vmcnt<K + 1>();
+        {
+            const uint32_t r = lds_stage_consume<G, K, NT>(A, sA, aA, paA, ph_odd, lane, lane64);
+            if (live) {
+                group_store<G>(P, seg, r, lane);
+            }
+        }
+        live = has_next;
+        if (!__any(has_next)) {
+            break;
+        }
+        seg = nxt;
+        nxt = seg + step;
+        has_next = nxt < R.end;
+        dnn = seg_desc<VARLEN>(P, nxt + step);
+        aA = has_next ? base + dn.off : z;
+        paA = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        lds_stage_issue<G, K, NT>(A, sA, aA, has_next ? dn.len : 0u, paA, has_next ? plen : 0u, lane);
+        dn = dnn;
+        wait_vmcnt<K + 1>();
+        {
+            const uint32_t r = lds_stage_consume<G, K, NT>(B, sB, aB, paB, ph_odd, lane, lane64);
+            if (live) {
+                group_store<G>(P, seg, r, lane);
+            }
+        }
+        live = has_next;
+        if (!__any(has_next)) {
+            break;
+        }
+        seg = nxt;
+    }
+    wait_vmcnt<0>();                                           // drain the trailing stage's DMA
+}
+
+// ---------------------------------------------------------------------------------------------
+// Roofline probe, LDS-DMA form: global_load_lds_dwordx4 pieces (1 KiB per wave-instruction)
+// into a per-wave double-buffered LDS ring, counted vmcnt, ds_read_b128 + v_sad_u16 consumers.
+// ---------------------------------------------------------------------------------------------
+template <bool NT>
+__global__ void __launch_bounds__(256) read_stream_lds_kernel(gu32x4* __restrict__ p, uint64_t n16,
+                                                              unsigned long long* __restrict__ sink) {
+    constexpr int P4 = 4;                                  // pieces per batch per wave
+    __shared__ u32x4 ring[4][2][P4][64];
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const uint64_t per_batch = (uint64_t)gridDim.x * 4u * P4 * 64u;   // chunks per grid-wide batch
+    uint64_t c = ((uint64_t)blockIdx.x * 4u + (uint64_t)w) * (P4 * 64u) + (uint64_t)lane;
+    const uint64_t nb = n16 / per_batch;                   // full batches only (probe)
+    uint32_t acc = 0u;
+    constexpr int aux = NT ? 2 : 0;
+    auto issue = [&](uint64_t cc, int slot) {
+#pragma unroll
+        for (int j = 0; j < P4; ++j) {
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + cc + 64u * j),
+                                             (__attribute__((address_space(3))) void*)&ring[w][slot][j][0], 16, 0, aux);
+        }
+    };
+    if (nb > 0) {
+        issue(c, 0);
+    }
+    for (uint64_t b = 0; b < nb; ++b) {
+        const int slot = (int)(b & 1u);
+        if (b + 1 < nb) {
+            issue(c + per_batch, slot ^ 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int j = 0; j < P4; ++j) {
+            acc = sum4(ring[w][slot][j][lane], acc);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        c += per_batch;
+    }
+    if (acc == 0x5EEDF00Du) {
+        atomicAdd(sink, 1ull);
     }
 }
 
@@ -285,44 +735,151 @@ __global__ void __launch_bounds__(256) read_stream_kernel(gu32x4* __restrict__ p
 
 namespace netcsum {
 
+// Persistent-grid sizing: blocks = (resident blocks per CU for this instantiation) x CUs x mult,
+// so every workgroup is co-resident and they finish together (a partial last "round" of blocks
+// leaves CUs idle for a whole block lifetime). Residency is cached per (instantiation, block).
+template <typename Kern>
+static int pick_grid(Kern kern, const LaunchCfg& c) {
+    if (c.tile > 0) {                                    // one block per tile of gpb*tile segments
+        const uint64_t per = (uint64_t)(c.block / c.group_lanes) * (uint64_t)c.tile;
+        const uint64_t nseg = c.blocks_needed * (uint64_t)(c.block / c.group_lanes);
+        return (int)((nseg + per - 1u) / per);
+    }
+    if (c.grid > 0) return c.grid;
+    static int occ_cache[3] = {0, 0, 0};                 // block 64 / 128 / 256
+    const int slot = c.block == 64 ? 0 : (c.block == 128 ? 1 : 2);
+    int occ = occ_cache[slot];
+    if (occ <= 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, c.block, 0) != hipSuccess || occ <= 0) {
+            occ = 1;
+        }
+        occ_cache[slot] = occ;
+    }
+    uint64_t g = (uint64_t)occ * (uint64_t)c.cus * (uint64_t)(c.grid_mult > 0 ? c.grid_mult : 1);
+    if (g > c.blocks_needed) g = c.blocks_needed;
+    return (int)(g ? g : 1);
+}
+
 template <int G, int K, bool VARLEN, bool NT>
-static hipError_t launch_seg(const SegBatchArgs& a, int grid, int block, hipStream_t s) {
-    hipLaunchKernelGGL((seg_batch_kernel<G, K, VARLEN, NT>), dim3(grid), dim3(block), 0, s, a);
+static hipError_t launch_seg(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    const int grid = pick_grid(seg_batch_kernel<G, K, VARLEN, NT>, c);
+    hipLaunchKernelGGL((seg_batch_kernel<G, K, VARLEN, NT>), dim3(grid), dim3(c.block), 0, s, a);
     return hipGetLastError();
 }
 
 template <int G, int K, bool VARLEN>
-static hipError_t launch_seg_nt(const SegBatchArgs& a, int grid, int block, bool nt, hipStream_t s) {
-    return nt ? launch_seg<G, K, VARLEN, true>(a, grid, block, s)
-              : launch_seg<G, K, VARLEN, false>(a, grid, block, s);
+static hipError_t launch_seg_nt(const SegBatchArgs& a, const LaunchCfg& c, bool nt, hipStream_t s) {
+    return nt ? launch_seg<G, K, VARLEN, true>(a, c, s)
+              : launch_seg<G, K, VARLEN, false>(a, c, s);
 }
 
 template <int G, bool VARLEN>
-static hipError_t launch_seg_k(const SegBatchArgs& a, int k, int grid, int block, bool nt, hipStream_t s) {
+static hipError_t launch_seg_k(const SegBatchArgs& a, int k, const LaunchCfg& c, bool nt, hipStream_t s) {
     switch (k) {
-    case 1:  return launch_seg_nt<G, 1, VARLEN>(a, grid, block, nt, s);
-    case 2:  return launch_seg_nt<G, 2, VARLEN>(a, grid, block, nt, s);
-    case 3:  return launch_seg_nt<G, 3, VARLEN>(a, grid, block, nt, s);
-    default: return launch_seg_nt<G, 4, VARLEN>(a, grid, block, nt, s);
+    case 1:  return launch_seg_nt<G, 1, VARLEN>(a, c, nt, s);
+    case 2:  return launch_seg_nt<G, 2, VARLEN>(a, c, nt, s);
+    case 3:  return launch_seg_nt<G, 3, VARLEN>(a, c, nt, s);
+    default: return launch_seg_nt<G, 4, VARLEN>(a, c, nt, s);
     }
 }
 
 template <bool VARLEN>
-static hipError_t launch_seg_g(const SegBatchArgs& a, int g, int k, int grid, int block, bool nt,
+static hipError_t launch_seg_g(const SegBatchArgs& a, int g, int k, const LaunchCfg& c, bool nt,
                                hipStream_t s) {
     switch (g) {
-    case 1:  return launch_seg_k<1, VARLEN>(a, k, grid, block, nt, s);
-    case 4:  return launch_seg_k<4, VARLEN>(a, k, grid, block, nt, s);
-    case 8:  return launch_seg_k<8, VARLEN>(a, k, grid, block, nt, s);
-    case 16: return launch_seg_k<16, VARLEN>(a, k, grid, block, nt, s);
-    case 32: return launch_seg_k<32, VARLEN>(a, k, grid, block, nt, s);
-    default: return launch_seg_k<64, VARLEN>(a, k, grid, block, nt, s);
+    case 1:  return launch_seg_k<1, VARLEN>(a, k, c, nt, s);
+    case 4:  return launch_seg_k<4, VARLEN>(a, k, c, nt, s);
+    case 8:  return launch_seg_k<8, VARLEN>(a, k, c, nt, s);
+    case 16: return launch_seg_k<16, VARLEN>(a, k, c, nt, s);
+    case 32: return launch_seg_k<32, VARLEN>(a, k, c, nt, s);
+    default: return launch_seg_k<64, VARLEN>(a, k, c, nt, s);
     }
 }
 
-hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
-    return a.seg_off ? launch_seg_g<true>(a, c.group_lanes, c.chunks_per_pass, c.grid, c.block, c.nt, s)
-                     : launch_seg_g<false>(a, c.group_lanes, c.chunks_per_pass, c.grid, c.block, c.nt, s);
+template <int G, int K, bool VARLEN, bool NT>
+static hipError_t launch_pipe(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    const int grid = pick_grid(seg_pipe_kernel<G, K, VARLEN, NT>, c);
+    hipLaunchKernelGGL((seg_pipe_kernel<G, K, VARLEN, NT>), dim3(grid), dim3(c.block), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int G, bool VARLEN, bool NT>
+static hipError_t launch_pipe_k(const SegBatchArgs& a, int k, const LaunchCfg& c, hipStream_t s) {
+    switch (k) {
+    case 1:  return launch_pipe<G, 1, VARLEN, NT>(a, c, s);
+    case 2:  return launch_pipe<G, 2, VARLEN, NT>(a, c, s);
+    case 3:  return launch_pipe<G, 3, VARLEN, NT>(a, c, s);
+    case 4:  return launch_pipe<G, 4, VARLEN, NT>(a, c, s);
+    case 6:  return launch_pipe<G, 6, VARLEN, NT>(a, c, s);
+    default: return launch_pipe<G, 8, VARLEN, NT>(a, c, s);
+    }
+}
+
+template <bool VARLEN, bool NT>
+static hipError_t launch_pipe_g(const SegBatchArgs& a, int g, int k, const LaunchCfg& c, hipStream_t s) {
+    switch (g) {
+    case 1:  return launch_pipe_k<1, VARLEN, NT>(a, k, c, s);
+    case 4:  return launch_pipe_k<4, VARLEN, NT>(a, k, c, s);
+    case 8:  return launch_pipe_k<8, VARLEN, NT>(a, k, c, s);
+    case 16: return launch_pipe_k<16, VARLEN, NT>(a, k, c, s);
+    case 32: return launch_pipe_k<32, VARLEN, NT>(a, k, c, s);
+    default: return launch_pipe_k<64, VARLEN, NT>(a, k, c, s);
+    }
+}
+
+template <int G, int K, bool VARLEN, bool NT>
+static hipError_t launch_lds(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    const int grid = pick_grid(seg_lds_kernel<G, K, VARLEN, NT>, c);
+    hipLaunchKernelGGL((seg_lds_kernel<G, K, VARLEN, NT>), dim3(grid), dim3(c.block), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int G, bool VARLEN, bool NT>
+static hipError_t launch_lds_k(const SegBatchArgs& a, int k, const LaunchCfg& c, hipStream_t s) {
+    switch (k) {
+    case 1:  return launch_lds<G, 1, VARLEN, NT>(a, c, s);
+    case 2:  return launch_lds<G, 2, VARLEN, NT>(a, c, s);
+    case 3:  return launch_lds<G, 3, VARLEN, NT>(a, c, s);
+    case 4:  return launch_lds<G, 4, VARLEN, NT>(a, c, s);
+    case 6:  return launch_lds<G, 6, VARLEN, NT>(a, c, s);
+    default: return launch_lds<G, 8, VARLEN, NT>(a, c, s);
+    }
+}
+
+template <bool VARLEN, bool NT>
+static hipError_t launch_lds_g(const SegBatchArgs& a, int g, int k, const LaunchCfg& c, hipStream_t s) {
+    switch (g) {
+    case 1:  return launch_lds_k<1, VARLEN, NT>(a, k, c, s);
+    case 4:  return launch_lds_k<4, VARLEN, NT>(a, k, c, s);
+    case 8:  return launch_lds_k<8, VARLEN, NT>(a, k, c, s);
+    case 16: return launch_lds_k<16, VARLEN, NT>(a, k, c, s);
+    case 32: return launch_lds_k<32, VARLEN, NT>(a, k, c, s);
+    default: return launch_lds_k<64, VARLEN, NT>(a, k, c, s);
+    }
+}
+
+hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStream_t s) {
+    SegBatchArgs a = args;
+    a.tile = c.tile > 0 ? (uint32_t)c.tile : 0u;
+    if (c.kernel == 3) {
+        if (a.seg_off) {
+            return c.nt ? launch_lds_g<true, true>(a, c.group_lanes, c.chunks_per_pass, c, s)
+                        : launch_lds_g<true, false>(a, c.group_lanes, c.chunks_per_pass, c, s);
+        }
+        return c.nt ? launch_lds_g<false, true>(a, c.group_lanes, c.chunks_per_pass, c, s)
+                    : launch_lds_g<false, false>(a, c.group_lanes, c.chunks_per_pass, c, s);
+    }
+    if (c.kernel == 2) {
+        if (a.seg_off) {
+            return c.nt ? launch_pipe_g<true, true>(a, c.group_lanes, c.chunks_per_pass, c, s)
+                        : launch_pipe_g<true, false>(a, c.group_lanes, c.chunks_per_pass, c, s);
+        }
+        return c.nt ? launch_pipe_g<false, true>(a, c.group_lanes, c.chunks_per_pass, c, s)
+                    : launch_pipe_g<false, false>(a, c.group_lanes, c.chunks_per_pass, c, s);
+    }
+    const int k = c.chunks_per_pass > 4 ? 4 : c.chunks_per_pass;
+    return a.seg_off ? launch_seg_g<true>(a, c.group_lanes, k, c, c.nt, s)
+                     : launch_seg_g<false>(a, c.group_lanes, k, c, c.nt, s);
 }
 
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
@@ -340,7 +897,17 @@ hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint6
 }
 
 hipError_t launch_read_stream(const void* d_p, uint64_t n16, unsigned long long* d_sink, int grid, bool nt,
-                              hipStream_t s) {
+                              hipStream_t s, int variant) {
+    if (variant == 1) {
+        if (nt) {
+            hipLaunchKernelGGL(read_stream_lds_kernel<true>, dim3(grid), dim3(256), 0, s,
+                               reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sink);
+        } else {
+            hipLaunchKernelGGL(read_stream_lds_kernel<false>, dim3(grid), dim3(256), 0, s,
+                               reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sink);
+        }
+        return hipGetLastError();
+    }
     if (nt) {
         hipLaunchKernelGGL(read_stream_kernel<true>, dim3(grid), dim3(256), 0, s,
                            reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sink);

@@ -47,6 +47,7 @@ DEF_OK, DEF_FAIL = 1, 0
 
 OP_DATA_CALC, OP_DATA_VERIFY, OP_HDR_CALC, OP_HDR_VERIFY = 0, 1, 2, 3
 TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
+TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
@@ -214,6 +215,21 @@ def _stream(stream):
     return int(stream)
 
 
+def _nbytes(x):
+    if hasattr(x, "numel") and hasattr(x, "element_size"):
+        return int(x.numel()) * int(x.element_size())
+    if hasattr(x, "nbytes"):
+        return int(x.nbytes)
+    return None
+
+
+def _require(x, need, what):
+    """Host-side bounds check before any launch (a device fault can take the GPU down)."""
+    have = _nbytes(x)
+    if have is not None and have < need:
+        raise ValueError(f"{what}: buffer holds {have} B but the launch would touch {need} B")
+
+
 def _check(err, what):
     if err != NET_UTIL_ERR_NONE:
         raise RuntimeError(f"{what} returned NET_ERR {err}")
@@ -268,6 +284,11 @@ def stream_sum32(spans):
 # --------------------------------------------------------------------------- batch interface
 def batch_strided(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
                   op=OP_DATA_CALC, stream=None, check=True):
+    if n_seg:
+        _require(seg, (n_seg - 1) * seg_stride + seg_len, "segments")
+        if pseudo is not None and pseudo_len:
+            _require(pseudo, (n_seg - 1) * pseudo_stride + pseudo_len, "pseudo-headers")
+        _require(out, n_seg * (2 if op in (OP_DATA_CALC, OP_HDR_CALC) else 1), "out")
     err = lib().NetUtil_MI355X_ChkSumBatchStrided(_p(seg), seg_stride, seg_len, _p(pseudo), pseudo_stride,
                                                   pseudo_len, n_seg, _p(out), op, _stream(stream))
     if check:
@@ -277,6 +298,12 @@ def batch_strided(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n
 
 def batch_varlen(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
                  op=OP_DATA_CALC, stream=None, check=True):
+    if n_seg:
+        _require(seg_off, 8 * n_seg, "segment offsets")
+        _require(seg_len, 2 * n_seg, "segment lengths")
+        if pseudo is not None and pseudo_len:
+            _require(pseudo, (n_seg - 1) * pseudo_stride + pseudo_len, "pseudo-headers")
+        _require(out, n_seg * (2 if op in (OP_DATA_CALC, OP_HDR_CALC) else 1), "out")
     err = lib().NetUtil_MI355X_ChkSumBatchVarLen(_p(base), _p(seg_off), _p(seg_len), _p(pseudo), pseudo_stride,
                                                  pseudo_len, n_seg, _p(out), op, _stream(stream))
     if check:
@@ -286,6 +313,11 @@ def batch_varlen(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_se
 
 def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
                        op=OP_DATA_CALC, n_chunks=8, check=True):
+    if n_seg:
+        _require(seg, (n_seg - 1) * seg_stride + seg_len, "segments")
+        if pseudo is not None and pseudo_len:
+            _require(pseudo, (n_seg - 1) * pseudo_stride + pseudo_len, "pseudo-headers")
+        _require(out, n_seg * (2 if op in (OP_DATA_CALC, OP_HDR_CALC) else 1), "out")
     err = lib().NetUtil_MI355X_ChkSumBatchStridedHost(_p(seg), seg_stride, seg_len, _p(pseudo), pseudo_stride,
                                                       pseudo_len, n_seg, _p(out), op, n_chunks)
     if check:
@@ -294,11 +326,14 @@ def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_l
 
 
 def fill(buf, n_bytes, seed, pattern=0, stream=None, first_byte=0):
+    _require(buf, n_bytes, "fill buffer")
     _check(lib().NetUtil_MI355X_Fill(_p(buf), n_bytes, first_byte, seed, pattern, _stream(stream)),
            "NetUtil_MI355X_Fill")
 
 
 def read_stream(buf, n_bytes, sink, stream=None):
+    _require(buf, n_bytes, "read-stream buffer")
+    _require(sink, 8, "sink")
     _check(lib().NetUtil_MI355X_ReadStream(_p(buf), n_bytes, _p(sink), _stream(stream)),
            "NetUtil_MI355X_ReadStream")
 
