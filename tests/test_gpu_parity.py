@@ -64,8 +64,12 @@ LENGTHS = [0, 1, 2, 3, 4, 5, 7, 15, 16, 17, 19, 20, 21, 31, 33, 40, 63, 64, 65, 
            1023, 1499, 1500, 1501, 4520, 8999, 9000, 16385, 65535]
 
 
+@pytest.mark.parametrize("kernel", [0, 2, 4])
 @pytest.mark.parametrize("L", LENGTHS)
-def test_strided_matrix_vs_oracle(L):
+def test_strided_matrix_vs_oracle(L, kernel):
+    """Every length class x stride x base misalignment x pseudo-header shape x op, per kernel form
+    (0 = library default; 4 = wave-tile LDS image where it fits, else its fallback)."""
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
     rng = np.random.default_rng(L + 11)
     n = 37 if L < 20000 else 5
     for pattern in ("random", "zero", "ff", "carry"):
@@ -88,7 +92,7 @@ def test_strided_matrix_vs_oracle(L):
                         assert np.array_equal(got, want), (L, pattern, stride, base_off, plen, op)
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("kernel", [1, 2, 3, 4])
 @pytest.mark.parametrize("group", [1, 4, 8, 16, 32, 64])
 @pytest.mark.parametrize("nt,chunks,tile", [(0, 0, 0), (1, 0, 3), (0, 1, 1), (1, 8, 0), (1, 6, 7)])
 def test_every_group_width_and_load_policy(kernel, group, nt, chunks, tile):

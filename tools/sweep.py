@@ -67,10 +67,11 @@ def main():
     variants = []
     for probe in (0, 1):
         variants.append(("read", dict(grid=8192, nt=1, probe=probe)))
-    for kernel, group, k in ((2, 16, 6), (3, 16, 6), (2, 32, 3), (3, 32, 3), (2, 64, 2), (3, 64, 2)):
-        variants.append(("c2", dict(kernel=kernel, group=group, k=k, nt=1, grid=16384)))
-        for tile in (1, 2, 4, 8, 16):
-            variants.append(("c2", dict(kernel=kernel, group=group, k=k, nt=1, tile=tile)))
+    variants.append(("c2", dict(kernel=2, group=16, k=6, nt=1, grid=16384)))
+    for group in (16, 32, 64):
+        for nt in (0, 1):
+            for grid, mult, tile in ((0, 1, 0), (0, 2, 0), (0, 4, 0), (16384, 0, 0), (0, 0, 2), (0, 0, 8)):
+                variants.append(("c2", dict(kernel=4, group=group, nt=nt, grid=grid, mult=mult, tile=tile)))
     res = {}
     for r in range(args.rounds):
         for kind, kw in variants:
@@ -97,8 +98,8 @@ def main():
         hdr = torch.empty(nh * 20 + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(hdr, nh * 20, SEED, 0)
         o3 = torch.empty(nh, dtype=torch.int16, device=dev)
-        for kernel, group, k, nt in ((2, 1, 2, 0), (2, 1, 2, 1), (3, 1, 2, 1)):
-            for grid, tile in ((8192, 0), (0, 1), (0, 2), (0, 4), (0, 8)):
+        for kernel, group, k, nt in ((2, 1, 2, 0), (4, 1, 0, 0), (4, 1, 0, 1), (4, 4, 0, 1)):
+            for grid, tile in ((8192, 0), (0, 0), (16384, 0), (0, 2), (0, 8)):
                 set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=nt, tile=tile)
                 med, mn = timeit(lambda: netcsum.batch_strided(hdr, 20, 20, None, 0, 0, nh, o3, 2, stream=st), st)
                 b = nh * (20 + 2)

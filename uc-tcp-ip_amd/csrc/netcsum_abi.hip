@@ -74,17 +74,79 @@ int chunk_slots(uint32_t want) {                    // smallest supported K >= w
     return 8;
 }
 
+uint32_t gcd_u32(uint32_t a, uint32_t b) {
+    while (b) {
+        const uint32_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+// v4 (wave-tile LDS image) geometry for a strided batch, if one compiled instantiation fits:
+// G lanes per segment (S = 64/G segments per wave-tile), P KiB image per stage, K chunks per lane.
+bool choose_tile(const netcsum::SegBatchArgs& a, int g_force, int k_force, int* g_out, int* p_out, int* k_out) {
+    if (a.seg_off != nullptr || a.seg_stride < a.seg_len || a.seg_stride > 0xFFFFFFFFull) return false;
+    const uint32_t stride = (uint32_t)a.seg_stride;
+    const uint32_t g16 = stride ? gcd_u32(stride, 16u) : 16u;
+    const uint32_t maxlead = (uint32_t)((uintptr_t)a.base % g16) + (16u - g16);   // worst first-chunk offset
+    const uint32_t nchmax = (maxlead + a.seg_len + 15u) >> 4;
+    static const int gs[] = {1, 4, 8, 16, 32, 64};
+    static const int ps[] = {1, 2, 4, 6, 8};
+    static const int ks[] = {1, 2, 3, 4, 6, 8};
+    for (int g : gs) {
+        if (g_force && g != g_force) continue;
+        const uint32_t S = 64u / (uint32_t)g;
+        const uint64_t img = (uint64_t)(S - 1u) * stride + a.seg_len + 127u;
+        const uint64_t pimg = a.pseudo ? (uint64_t)(S - 1u) * a.pseudo_stride + a.pseudo_len + 15u : 0u;
+        if (pimg > 1024u) continue;
+        const uint32_t kneed = (nchmax + (uint32_t)g - 1u) / (uint32_t)g;
+        if (!g_force && kneed > 8u) continue;            // prefer the narrowest group that fits
+        for (int p : ps) {
+            if ((uint64_t)p * 1024u < img) continue;
+            for (int k : ks) {
+                if (k_force && k != k_force) continue;
+                if ((uint32_t)k < kneed) continue;
+                if (netcsum::tile_supported(g, p, k)) {
+                    *g_out = g;
+                    *p_out = p;
+                    *k_out = k;
+                    return true;
+                }
+            }
+        }
+    }
+    return false;
+}
+
 // Geometry policy. len_hint = typical segment length in bytes (0 = unknown / variable).
-netcsum::LaunchCfg choose_cfg(int dev, uint32_t len_hint, uint32_t n_seg, bool varlen) {
+netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t len_hint) {
+    const bool varlen = a.seg_off != nullptr;
     netcsum::LaunchCfg c{};
     c.block = g_tune_block.load();
     if (c.block < 64 || c.block > 1024 || (c.block & 63)) c.block = 256;
     c.nt = g_tune_nt.load() != 0;
-
     c.kernel = g_tune_kernel.load();
+    c.cus = cu_count(dev);
+    c.grid_mult = g_tune_grid_mult.load();
+    c.tile = g_tune_tile.load();
+    c.grid = g_tune_grid.load();                       // <= 0: derived below / in the launcher
+
+    if (c.kernel == 4) {
+        int g = 0, p = 0, k = 0;
+        if (choose_tile(a, g_tune_group.load(), g_tune_chunks.load(), &g, &p, &k)) {
+            c.group_lanes = g;
+            c.tile_pieces = p;
+            c.chunks_per_pass = k;
+            c.block = 256;                             // 4 independent waves per block
+            c.blocks_needed = 0;
+            return c;
+        }
+        c.kernel = 2;                                  // varlen, or no instantiation fits
+    }
     // chunks per segment incl. misaligned edges; variable lengths assume the C4 mean (~4.5 KB)
     const uint32_t chunks = varlen ? 288u : (len_hint / 16u + 2u);
-    const uint32_t kmax = (c.kernel == 2) ? 8u : 4u;
+    const uint32_t kmax = (c.kernel == 2 || c.kernel == 3) ? 8u : 4u;
     int g = g_tune_group.load();
     if (g == 0) {
         g = varlen ? 64 : pow2_group((chunks + kmax - 1u) / kmax);
@@ -96,14 +158,8 @@ netcsum::LaunchCfg choose_cfg(int dev, uint32_t len_hint, uint32_t n_seg, bool v
         k = chunk_slots(std::min<uint32_t>(kmax, std::max<uint32_t>(1u, (chunks + (uint32_t)g - 1u) / (uint32_t)g)));
     }
     c.chunks_per_pass = k;
-
     const uint32_t gpb = (uint32_t)(c.block / g);
-    c.blocks_needed = ((uint64_t)n_seg + gpb - 1u) / gpb;
-    c.cus = cu_count(dev);
-    c.grid_mult = g_tune_grid_mult.load();
-    c.tile = g_tune_tile.load();
-    int grid = g_tune_grid.load();                     // <= 0: residency-exact persistent grid
-    c.grid = grid;
+    c.blocks_needed = ((uint64_t)a.n_seg + gpb - 1u) / gpb;
     return c;
 }
 
@@ -118,7 +174,7 @@ NET_ERR check_op(NETCSUM_OP op, const void* d_pseudo, CPU_INT16U pseudo_len) {
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a, uint32_t len_hint, hipStream_t s) {
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
-    const netcsum::LaunchCfg c = choose_cfg(dev, len_hint, a.n_seg, a.seg_off != nullptr);
+    const netcsum::LaunchCfg c = choose_cfg(dev, a, len_hint);
     NC_HIP(netcsum::launch_seg_batch(a, c, s));
     return NET_UTIL_ERR_NONE;
 }
@@ -281,7 +337,7 @@ NET_ERR NetUtil_MI355X_ChkSumBatchStridedHost(const void* h_seg, uint64_t seg_st
         a.out = d_out;
         // Parity of each segment's start is derived in-kernel from the DEVICE address it reads,
         // so re-basing the chunk at a 256-B aligned device buffer is transparent.
-        const netcsum::LaunchCfg cfg = choose_cfg(dev, seg_len, ns, false);
+        const netcsum::LaunchCfg cfg = choose_cfg(dev, a, seg_len);
         NC_HIP(netcsum::launch_seg_batch(a, cfg, st));
         NC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(h_out) + (size_t)s0 * out_elt, d_out, (size_t)ns * out_elt,
                               hipMemcpyDeviceToHost, st));
@@ -370,7 +426,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_nt.store(value != 0);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
-        if (value < 0 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_kernel.store(value == 0 ? 2 : value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CHUNKS:

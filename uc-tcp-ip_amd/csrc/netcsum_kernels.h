@@ -31,9 +31,12 @@ struct LaunchCfg {
     int  chunks_per_pass;  // 16-B chunks per lane per pass: 1..4
     bool nt;               // non-temporal segment loads
     int  kernel;           // 1: seg_batch_kernel (one segment in flight per group), 2: seg_pipe_kernel,
-                           // 3: seg_lds_kernel
+                           // 3: seg_lds_kernel, 4: seg_tile_kernel (strided only)
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
+    int  tile_pieces;      // v4: KiB of LDS image per stage (P)
 };
+
+bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation
 
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,

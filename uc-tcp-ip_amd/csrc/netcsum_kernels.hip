@@ -579,6 +579,153 @@ __global__ void __launch_bounds__(256) seg_lds_kernel(SegBatchArgs P) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// v4: wave-tile streaming through an LDS image (strided batches with stride >= length).
+//
+// A wave owns a TILE of S = 64/G consecutive segments. Their bytes — one contiguous range of
+// HBM — are fetched as P whole 1-KiB LDS-DMA pieces starting at the 128-B line below the first
+// segment, so every wave-instruction reads 8 full, aligned cache lines (the read-probe pattern)
+// instead of G-lane pieces at 16-B alignment. The tile's pseudo-headers (contiguous too) ride in
+// one extra piece. Each G-lane group then reads ITS segment's 16-B chunks back from the LDS
+// image (aligned ds_read_b128), masks the edges and sums exactly as v2. Two stages per wave
+// (ping-pong), hand-counted vmcnt(P+1). Host guarantees (S-1)*stride + len + 127 <= P*1024,
+// K*G >= chunks per segment and (S-1)*pstride + plen + 15 <= 1024.
+// ---------------------------------------------------------------------------------------------
+struct TileStage {
+    uint32_t seg0;       // first segment of the tile
+    uint32_t nseg;       // segments of this tile (< S only for the last tile; 0 = dummy)
+    uint32_t img_lead;   // tile start - image start (image start is 128-B aligned)
+    uint32_t pimg_lead;  // pseudo-header range start - its 16-B aligned image start
+};
+
+template <int G, int P, bool NT>
+__device__ __forceinline__ void tile_issue(TileStage& st, u32x4 (*img)[64], const SegBatchArgs& A, uint32_t tile,
+                                           uint32_t ntiles, uint32_t plen, int lane64) {
+    constexpr uint32_t S = 64 / G;
+    const uintptr_t z = zero_addr();
+    const bool live = tile < ntiles;
+    st.seg0 = tile * S;
+    st.nseg = live ? min(S, A.n_seg - st.seg0) : 0u;
+    const uintptr_t a0 = (uintptr_t)A.base + (uint64_t)st.seg0 * A.seg_stride;
+    const uintptr_t aend = live ? a0 + (uint64_t)(st.nseg - 1u) * A.seg_stride + A.seg_len : 0u;
+    const uintptr_t img0 = a0 & ~(uintptr_t)127;
+    st.img_lead = (uint32_t)(a0 - img0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // prior ds_reads of this stage done
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const uintptr_t src = img0 + 1024u * (uintptr_t)p + 16u * (uintptr_t)lane64;
+        __builtin_amdgcn_global_load_lds(
+            reinterpret_cast<const __attribute__((address_space(1))) void*>(src < aend ? src : z),
+            (lds_void*)(&img[p][0]), 16, 0, NT ? 2 : 0);
+    }
+    const uintptr_t p0 = (uintptr_t)A.pseudo + (uint64_t)st.seg0 * A.pseudo_stride;
+    const uintptr_t pend = (live && plen) ? p0 + (uint64_t)(st.nseg - 1u) * A.pseudo_stride + plen : 0u;
+    const uintptr_t pimg0 = p0 & ~(uintptr_t)15;
+    st.pimg_lead = (uint32_t)(p0 - pimg0);
+    const uintptr_t psrc = pimg0 + 16u * (uintptr_t)lane64;
+    __builtin_amdgcn_global_load_lds(
+        reinterpret_cast<const __attribute__((address_space(1))) void*>(psrc < pend ? psrc : z),
+        (lds_void*)(&img[P][0]), 16, 0, 0);
+}
+
+template <int G, int P, int K>
+__device__ __forceinline__ void tile_consume(const TileStage& st, u32x4 (*img)[64], const SegBatchArgs& A,
+                                             uint32_t plen, bool ph_odd, int lane64) {
+    const int g = lane64 / G;
+    const int lane = lane64 & (G - 1);
+    const u32x4* flat = &img[0][0];
+    const uint32_t so = st.img_lead + (uint32_t)g * (uint32_t)A.seg_stride;   // < P*1024 (host check)
+    const uint32_t lead = so & 15u;
+    const uint32_t rend = lead + A.seg_len;
+    const uint32_t nch = (rend + 15u) >> 4;
+    const uint32_t cb = so >> 4;
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        if (c < nch) {
+            acc = sum4(edge_mask_rel(flat[cb + c], c, lead, rend), acc);
+        }
+    }
+    uint32_t s = fold16(acc);
+    if (((lead & 1u) != 0u) != ph_odd) {
+        s = rot8(s);
+    }
+    if (plen != 0u) {
+        const u32x4* pflat = &img[P][0];
+        const uint32_t pso = st.pimg_lead + (uint32_t)g * A.pseudo_stride;   // < 1024 (host check)
+        const uint32_t plead = pso & 15u;
+        const uint32_t prend = plead + plen;
+        const uint32_t pnch = (prend + 15u) >> 4;
+        uint32_t pacc = 0u;
+        for (uint32_t c = (uint32_t)lane; c < pnch; c += (uint32_t)G) {
+            pacc = sum4(edge_mask_rel(pflat[(pso >> 4) + c], c, plead, prend), pacc);
+        }
+        uint32_t ps = fold16(pacc);
+        if (plead & 1u) {
+            ps = rot8(ps);
+        }
+        s += ps;
+    }
+    s = fold16(group_sum<G>(s));
+    if (lane == 0 && (uint32_t)g < st.nseg) {
+        const uint32_t seg = st.seg0 + (uint32_t)g;
+        if (A.verify) {
+            static_cast<uint8_t*>(A.out)[seg] = (s == 0xFFFFu) ? 1u : 0u;
+        } else {
+            static_cast<uint16_t*>(A.out)[seg] = (uint16_t)(~s);
+        }
+    }
+}
+
+template <int G, int P, int K, bool NT>
+__global__ void __launch_bounds__(256) seg_tile_kernel(SegBatchArgs A) {
+    constexpr uint32_t S = 64 / G;
+    __shared__ u32x4 img[4][2][P + 1][64];
+    const int w = (int)(threadIdx.x >> 6);
+    const int lane64 = (int)(threadIdx.x & 63);
+    const uint32_t plen = (A.pseudo != nullptr) ? A.pseudo_len : 0u;
+    const bool ph_odd = (plen & 1u) != 0u;
+    const uint32_t ntiles = (A.n_seg + S - 1u) / S;
+    uint32_t t, tstep, tend;                                    // wave-uniform tile walk
+    if (A.tile) {
+        const uint64_t t0 = (uint64_t)blockIdx.x * 4u * A.tile;
+        t = (uint32_t)t0 + (uint32_t)w;
+        tstep = 4u;
+        tend = (uint32_t)min<uint64_t>(t0 + 4ull * A.tile, ntiles);
+    } else {
+        t = blockIdx.x * 4u + (uint32_t)w;
+        tstep = gridDim.x * 4u;
+        tend = ntiles;
+    }
+    if (t >= tend) {
+        return;
+    }
+    u32x4 (*sA)[64] = img[w][0];
+    u32x4 (*sB)[64] = img[w][1];
+    TileStage A0, B0;
+    tile_issue<G, P, NT>(A0, sA, A, t, tend, plen, lane64);
+    for (;;) {
+        uint32_t nt = t + tstep;
+        tile_issue<G, P, NT>(B0, sB, A, nt, tend, plen, lane64);   // dummy (reads zero chunk) past end
+        wait_vmcnt<P + 1>();
+        tile_consume<G, P, K>(A0, sA, A, plen, ph_odd, lane64);
+        if (nt >= tend) {
+            break;
+        }
+        t = nt;
+        nt = t + tstep;
+        tile_issue<G, P, NT>(A0, sA, A, nt, tend, plen, lane64);
+        wait_vmcnt<P + 1>();
+        tile_consume<G, P, K>(B0, sB, A, plen, ph_odd, lane64);
+        if (nt >= tend) {
+            break;
+        }
+        t = nt;
+    }
+    wait_vmcnt<0>();                                            // drain the trailing dummy stage
+}
+
+// ---------------------------------------------------------------------------------------------
 // Roofline probe, LDS-DMA form: global_load_lds_dwordx4 pieces (1 KiB per wave-instruction)
 // into a per-wave double-buffered LDS ring, counted vmcnt, ds_read_b128 + v_sad_u16 consumers.
 // ---------------------------------------------------------------------------------------------
@@ -858,9 +1005,52 @@ static hipError_t launch_lds_g(const SegBatchArgs& a, int g, int k, const Launch
     }
 }
 
+template <int G, int P, int K, bool NT>
+static hipError_t launch_tile(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    int grid;
+    if (c.tile > 0) {
+        const uint64_t tiles = ((uint64_t)a.n_seg + (64 / G) - 1u) / (64 / G);
+        const uint64_t per = 4ull * (uint64_t)c.tile;
+        grid = (int)((tiles + per - 1u) / per);
+    } else if (c.grid > 0) {
+        grid = c.grid;
+    } else {
+        LaunchCfg c2 = c;
+        c2.blocks_needed = (((uint64_t)a.n_seg + (64 / G) - 1u) / (64 / G) + 3u) / 4u;
+        grid = pick_grid(seg_tile_kernel<G, P, K, NT>, c2);
+    }
+    hipLaunchKernelGGL((seg_tile_kernel<G, P, K, NT>), dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// The v4 instantiations: (G lanes per segment, P KiB image pieces, K chunks per lane).
+#define NETCSUM_TILE_TABLE(X)                                                                       \
+    X(1, 2, 3) X(1, 4, 6) X(4, 1, 1) X(4, 2, 2) X(8, 2, 2) X(8, 4, 4) X(16, 4, 4) X(16, 6, 6)       \
+    X(16, 8, 8) X(32, 2, 2) X(32, 4, 3) X(32, 4, 4) X(32, 8, 8) X(64, 2, 2) X(64, 4, 4) X(64, 8, 8)
+
+bool tile_supported(int g, int p, int k) {
+#define X(G_, P_, K_) if (g == G_ && p == P_ && k == K_) return true;
+    NETCSUM_TILE_TABLE(X)
+#undef X
+    return false;
+}
+
+static hipError_t launch_tile_dispatch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+#define X(G_, P_, K_)                                                                                \
+    if (c.group_lanes == G_ && c.tile_pieces == P_ && c.chunks_per_pass == K_) {                     \
+        return c.nt ? launch_tile<G_, P_, K_, true>(a, c, s) : launch_tile<G_, P_, K_, false>(a, c, s); \
+    }
+    NETCSUM_TILE_TABLE(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStream_t s) {
     SegBatchArgs a = args;
     a.tile = c.tile > 0 ? (uint32_t)c.tile : 0u;
+    if (c.kernel == 4) {
+        return launch_tile_dispatch(a, c, s);
+    }
     if (c.kernel == 3) {
         if (a.seg_off) {
             return c.nt ? launch_lds_g<true, true>(a, c.group_lanes, c.chunks_per_pass, c, s)

@@ -98,8 +98,10 @@ NET_ERR NetUtil_MI355X_ChainToSpans(const void *pdata_buf, const void *ppseudo_h
             break;
         case NET_PROTOCOL_TYPE_UDP_V4:
         case NET_PROTOCOL_TYPE_UDP_V6:
+#if !defined(NETCSUM_IN_STACK) || defined(NET_TCP_MODULE_EN)     /* as net_util.c:1625-1628 */
         case NET_PROTOCOL_TYPE_TCP_V4:
         case NET_PROTOCOL_TYPE_TCP_V6:
+#endif
             ix  = h->TransportHdrIx;
             len = (CPU_INT16U)(h->TransportHdrLen + (CPU_INT16U)h->DataLen);
             break;
