@@ -154,6 +154,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    kernel_desc = "netcsum::" + netcsum.last_launch()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -229,7 +230,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": "netcsum::seg_batch_kernel (strided)",
+                         "kernel": kernel_desc,
                          "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "traffic_source": traffic_src,

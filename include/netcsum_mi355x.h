@@ -188,18 +188,21 @@ NET_ERR  NetUtil_MI355X_ReadStream         (const void *d_buf,
 typedef enum netcsum_tune_key {
     NETCSUM_TUNE_GRID_BLOCKS   = 1,   /* workgroups per launch (0: exactly fill the chip)        */
     NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */
-    NETCSUM_TUNE_NT_LOADS      = 3,   /* 1: non-temporal loads on the segment stream             */
+    NETCSUM_TUNE_NT_LOADS      = 3,   /* -1 auto (default), 0 plain, 1 non-temporal segment loads */
     NETCSUM_TUNE_BLOCK_THREADS = 4,   /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
     NETCSUM_TUNE_KERNEL        = 5,   /* 1 simple, 2 pipelined register loads, 3 pipelined LDS-DMA,
                                          4 wave-tile LDS image (strided; else falls back to 2)     */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
-    NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA           */
+    NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
     NETCSUM_TUNE_TILE          = 9    /* J > 0: each block owns a contiguous tile of J segments per
-                                         group (grid = tiles); 0: persistent grid-stride          */
+                                         group (grid = tiles); 0: grid-stride; -1: auto (J = 4)    */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);
+
+/* The calling thread's last batch launch: kernel form and geometry (for profiling / logs). */
+const char *NetUtil_MI355X_LastLaunch      (void);
 
 /* Version / build identification string ("netcsum-mi355x <ver> gfx950"). */
 const char *NetUtil_MI355X_Version         (void);

@@ -22,9 +22,11 @@ DEV = "cuda"
 
 
 def _reset_tuning():
-    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES, netcsum.TUNE_NT_LOADS, netcsum.TUNE_BLOCK_THREADS,
-              netcsum.TUNE_KERNEL, netcsum.TUNE_CHUNKS, netcsum.TUNE_TILE, netcsum.TUNE_GRID_MULT):
+    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES, netcsum.TUNE_BLOCK_THREADS,
+              netcsum.TUNE_KERNEL, netcsum.TUNE_CHUNKS, netcsum.TUNE_GRID_MULT):
         netcsum.tune(k, 0)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+    netcsum.tune(netcsum.TUNE_TILE, -1)
 
 
 @pytest.fixture(autouse=True)

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Secondary measurements for DESIGN.md (not the bench.py line): configs C3 and C4 with the library's
+default launch policy, the host-memory (PCIe-inclusive) C2 rate, and the per-packet drop-in latency.
+Every measured batch is spot-checked against the oracle."""
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("uc-tcp-ip_amd", "oracle", ""):
+    sys.path.insert(0, os.path.join(REPO, sub))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import netcsum  # noqa: E402
+import oracle  # noqa: E402
+from bench import SEED, c2_pseudo_headers  # noqa: E402
+
+
+def events_ms(fn, st, reps=20, warm=3):
+    for _ in range(warm):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(st)
+        fn()
+        b.record(st)
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in ev)
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    out = {}
+    # ---- C3: 16 M x 20 B IPv4 headers, HdrCalc
+    nh = 1 << 24
+    hdr = torch.empty(nh * 20 + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(hdr, nh * 20, SEED, 0)
+    o3 = torch.empty(nh, dtype=torch.int16, device=dev)
+    ms = events_ms(lambda: netcsum.batch_strided(hdr, 20, 20, None, 0, 0, nh, o3, netcsum.OP_HDR_CALC, stream=st), st)
+    idx = np.random.default_rng(0).choice(nh, 512, replace=False)
+    host = hdr[: nh * 20].view(nh, 20)[torch.from_numpy(idx).to(dev)].cpu().numpy().reshape(-1)
+    ok = np.array_equal(o3.cpu().numpy().view(np.uint16)[idx], oracle.batch_strided(host, 20, 20, None, 0, 0, 512, 2))
+    out["C3"] = {"headers": nh, "ms": round(ms, 4), "Ghdr_per_s": round(nh / ms / 1e6, 2), "kernel": netcsum.last_launch(),
+                 "GiB_per_s_checksummed": round(nh * 20 / ms / 1e6 / 1.073741824, 1),
+                 "GB_per_s_algorithmic": round(nh * 22 / ms / 1e6, 1), "parity_sample_ok": ok}
+    del hdr, o3
+    # ---- C4: 1 M packed UDP datagrams, 40..9000 B (seed 7), 12-B pseudo each
+    rng = np.random.default_rng(7)
+    nv = 1 << 20
+    lens = rng.integers(40, 9001, size=nv).astype(np.uint16)
+    off = np.zeros(nv, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    tot = int(off[-1]) + int(lens[-1])
+    base = torch.empty(tot + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(base, tot, SEED, 0)
+    ph = np.zeros((nv, 12), np.uint8)
+    ph[:, 9] = 17
+    ph[:, 10] = (lens >> 8).astype(np.uint8)
+    ph[:, 11] = (lens & 0xFF).astype(np.uint8)
+    ph_d = torch.from_numpy(ph.reshape(-1)).to(dev)
+    off_d = torch.from_numpy(off.view(np.int64)).to(dev)
+    len_d = torch.from_numpy(lens.view(np.int16)).to(dev)
+    o4 = torch.empty(nv, dtype=torch.int16, device=dev)
+    ms = events_ms(lambda: netcsum.batch_varlen(base, off_d, len_d, ph_d, 12, 12, nv, o4, 0, stream=st), st)
+    sel = np.arange(0, nv, nv // 256)
+    got = o4.cpu().numpy().view(np.uint16)[sel]
+    bh = base.cpu().numpy()
+    want = oracle.batch_varlen(bh, off[sel], lens[sel], ph[sel].reshape(-1), 12, 12, 0)
+    out["C4"] = {"datagrams": nv, "bytes": tot, "odd_starts": int((off & 1).sum()), "ms": round(ms, 4),
+                 "GiB_per_s_checksummed": round((tot + 12 * nv) / ms / 1e6 / 1.073741824, 1),
+                 "GB_per_s_algorithmic": round((tot + 14 * nv) / ms / 1e6, 1),
+                 "descriptor_bytes_per_launch": 10 * nv, "kernel": netcsum.last_launch(), "parity_sample_ok": bool(np.array_equal(got, want))}
+    del base, o4, bh
+    # ---- host-memory (PCIe-inclusive) C2 rate: pinned NIC/socket buffers -> GPU -> pinned results
+    n, L = 1 << 20, 1500
+    seg_h = torch.empty(n * L, dtype=torch.uint8).pin_memory()
+    seg_h.numpy()[:] = oracle.fill(0, n * L, SEED, 0)
+    ph_h = torch.from_numpy(c2_pseudo_headers(0, n, L, 12)).pin_memory()
+    res_h = torch.empty(n, dtype=torch.int16).pin_memory()
+    rates = {}
+    for chunks in (1, 4, 16, 64):
+        netcsum.batch_strided_host(seg_h, L, L, ph_h, 12, 12, n, res_h, 0, n_chunks=chunks)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            netcsum.batch_strided_host(seg_h, L, L, ph_h, 12, 12, n, res_h, 0, n_chunks=chunks)
+            ts.append(time.perf_counter() - t0)
+        rates[chunks] = round(n * (L + 12) / statistics.median(ts) / 2 ** 30, 2)
+    sel = np.arange(0, n, n // 256)
+    want = oracle.batch_strided(seg_h.numpy(), L, L, ph_h.numpy(), 12, 12, n, 0, n_threads=8)
+    out["C2_host_memory"] = {"GiB_per_s_by_chunks": rates, "parity_ok": bool(np.array_equal(
+        res_h.numpy().view(np.uint16), want)), "note": "pinned host in/out, H2D + kernel + D2H pipelined"}
+    # ---- per-packet drop-in latency (C1 shape: 72-B UDP datagram + 12-B pseudo)
+    ch = netcsum.Chain([{"data": bytes(range(92)), "proto": netcsum.NET_PROTOCOL_TYPE_UDP_V4, "transport_ix": 20,
+                         "transport_hdr_len": 8, "data_len": 64}])
+    phb = netcsum.HostBytes(bytes(12))
+    for _ in range(50):
+        netcsum.DataCalc(ch.ptr, phb.ptr, 12)
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        netcsum.DataCalc(ch.ptr, phb.ptr, 12)
+    us = (time.perf_counter() - t0) / 2000 * 1e6
+    out["C1_dropin_call_us"] = round(us, 2)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

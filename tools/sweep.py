@@ -35,7 +35,7 @@ def timeit(fn, stream, reps=20, warm=3):
     return statistics.median(ts), min(ts)
 
 
-def set_tune(grid=0, group=0, nt=0, block=0, kernel=0, k=0, probe=0, mult=0, tile=0):
+def set_tune(grid=0, group=0, nt=-1, block=0, kernel=0, k=0, probe=1, mult=0, tile=-1):
     netcsum.tune(netcsum.TUNE_GRID_MULT, mult)
     netcsum.tune(netcsum.TUNE_TILE, tile)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)

@@ -22,13 +22,13 @@ constexpr int kMaxDev = 64;
 
 std::atomic<int> g_tune_grid{0};
 std::atomic<int> g_tune_group{0};
-std::atomic<int> g_tune_nt{0};
+std::atomic<int> g_tune_nt{-1};                   // -1: auto (nt when groups share no chunks)
 std::atomic<int> g_tune_block{256};
 std::atomic<int> g_tune_kernel{2};
 std::atomic<int> g_tune_chunks{0};
-std::atomic<int> g_tune_probe{0};
+std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
-std::atomic<int> g_tune_tile{0};
+std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -119,18 +119,25 @@ bool choose_tile(const netcsum::SegBatchArgs& a, int g_force, int k_force, int* 
     return false;
 }
 
-// Geometry policy. len_hint = typical segment length in bytes (0 = unknown / variable).
+// Geometry policy (round-1 measurements on MI355X, profiles/r1_sweep_*.jsonl):
+//  * kernel 2 (pipelined register loads) is the fastest form for C2, C3 and C4;
+//  * G = narrowest lane group whose 8 chunk slots per lane cover a segment (1500 B -> G 16, K 6;
+//    20-B headers -> G 1, K 2), from the exact worst-case chunk count of the batch's alignment;
+//  * contiguous block tiles of 4 segments per group (grid = n / (groups per block * 4));
+//  * non-temporal loads when G >= 8 (lane groups share no 16-B chunks); plain loads for narrow
+//    groups, whose neighbouring lanes re-read shared chunks through L1/L2.
 netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t len_hint) {
     const bool varlen = a.seg_off != nullptr;
     netcsum::LaunchCfg c{};
     c.block = g_tune_block.load();
     if (c.block < 64 || c.block > 1024 || (c.block & 63)) c.block = 256;
-    c.nt = g_tune_nt.load() != 0;
     c.kernel = g_tune_kernel.load();
     c.cus = cu_count(dev);
     c.grid_mult = g_tune_grid_mult.load();
-    c.tile = g_tune_tile.load();
-    c.grid = g_tune_grid.load();                       // <= 0: derived below / in the launcher
+    c.grid = g_tune_grid.load();                       // > 0: fixed grid (grid-stride mode)
+    const int tile = g_tune_tile.load();
+    c.tile = tile >= 0 ? tile : (c.grid > 0 ? 0 : 4);
+    const int nt = g_tune_nt.load();
 
     if (c.kernel == 4) {
         int g = 0, p = 0, k = 0;
@@ -140,16 +147,25 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
             c.chunks_per_pass = k;
             c.block = 256;                             // 4 independent waves per block
             c.blocks_needed = 0;
+            c.nt = nt != 0;
             return c;
         }
         c.kernel = 2;                                  // varlen, or no instantiation fits
     }
-    // chunks per segment incl. misaligned edges; variable lengths assume the C4 mean (~4.5 KB)
-    const uint32_t chunks = varlen ? 288u : (len_hint / 16u + 2u);
+    uint32_t chunks;                                   // worst-case 16-B chunks per segment
+    if (varlen) {
+        chunks = 288u;                                 // assume the C4 mean (~4.5 KB)
+    } else {
+        const uint32_t stride = (uint32_t)a.seg_stride;
+        const uint32_t g16 = stride ? gcd_u32(stride, 16u) : 16u;
+        const uint32_t maxlead = (uint32_t)((uintptr_t)a.base % g16) + (16u - g16);
+        chunks = (maxlead + len_hint + 15u) >> 4;
+        if (chunks == 0u) chunks = 1u;
+    }
     const uint32_t kmax = (c.kernel == 2 || c.kernel == 3) ? 8u : 4u;
     int g = g_tune_group.load();
     if (g == 0) {
-        g = varlen ? 64 : pow2_group((chunks + kmax - 1u) / kmax);
+        g = varlen ? 32 : pow2_group((chunks + kmax - 1u) / kmax);
     }
     g = pow2_group((uint32_t)g);
     c.group_lanes = g;
@@ -158,6 +174,7 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
         k = chunk_slots(std::min<uint32_t>(kmax, std::max<uint32_t>(1u, (chunks + (uint32_t)g - 1u) / (uint32_t)g)));
     }
     c.chunks_per_pass = k;
+    c.nt = nt >= 0 ? (nt != 0) : (g >= 8);
     const uint32_t gpb = (uint32_t)(c.block / g);
     c.blocks_needed = ((uint64_t)a.n_seg + gpb - 1u) / gpb;
     return c;
@@ -404,7 +421,7 @@ NET_ERR NetUtil_MI355X_ReadStream(const void* d_buf, uint64_t n_bytes, uint64_t*
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
     int grid = g_tune_grid.load();
-    if (grid <= 0) grid = cu_count(dev) * 8;
+    if (grid <= 0) grid = cu_count(dev) * 32;
     NC_HIP(netcsum::launch_read_stream(d_buf, n_bytes / 16u, reinterpret_cast<unsigned long long*>(d_sink), grid,
                                        g_tune_nt.load() != 0, static_cast<hipStream_t>(hip_stream), g_tune_probe.load()));
     return NET_UTIL_ERR_NONE;
@@ -423,7 +440,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_group.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_NT_LOADS:
-        g_tune_nt.store(value != 0);
+        g_tune_nt.store(value < 0 ? -1 : (value != 0));
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
         if (value < 0 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
@@ -440,7 +457,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_grid_mult.store(value == 0 ? 1 : value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_TILE:
-        if (value < 0 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tile.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:
@@ -456,6 +473,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     default:
         return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     }
+}
+
+const char* NetUtil_MI355X_LastLaunch(void) {
+    return netcsum::last_launch();
 }
 
 const char* NetUtil_MI355X_Version(void) {

@@ -37,6 +37,7 @@ struct LaunchCfg {
 };
 
 bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation
+const char* last_launch();                  // description of this thread's last batch launch
 
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,

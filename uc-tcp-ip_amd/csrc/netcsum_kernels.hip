@@ -31,6 +31,7 @@
 // folds its lane partials with cross-lane shuffles. Groups grid-stride over segments.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "netcsum_kernels.h"
 
@@ -606,7 +607,8 @@ __device__ __forceinline__ void tile_issue(TileStage& st, u32x4 (*img)[64], cons
     st.seg0 = tile * S;
     st.nseg = live ? min(S, A.n_seg - st.seg0) : 0u;
     const uintptr_t a0 = (uintptr_t)A.base + (uint64_t)st.seg0 * A.seg_stride;
-    const uintptr_t aend = live ? a0 + (uint64_t)(st.nseg - 1u) * A.seg_stride + A.seg_len : 0u;
+    // zero-length segments read nothing (the "buffer" may not exist at all)
+    const uintptr_t aend = (live && A.seg_len) ? a0 + (uint64_t)(st.nseg - 1u) * A.seg_stride + A.seg_len : 0u;
     const uintptr_t img0 = a0 & ~(uintptr_t)127;
     st.img_lead = (uint32_t)(a0 - img0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // prior ds_reads of this stage done
@@ -764,6 +766,11 @@ __global__ void __launch_bounds__(256) read_stream_lds_kernel(gu32x4* __restrict
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         c += per_batch;
+    }
+    // tail past the last whole batch: plain grid-stride loads, so the probe reads every byte
+    const uint64_t tstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = nb * per_batch + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n16; t += tstride) {
+        acc = sum4(load16<NT>(p + t), acc);
     }
     if (acc == 0x5EEDF00Du) {
         atomicAdd(sink, 1ull);
@@ -1045,7 +1052,22 @@ static hipError_t launch_tile_dispatch(const SegBatchArgs& a, const LaunchCfg& c
     return hipErrorInvalidValue;
 }
 
+thread_local char g_last_launch[160];
+
+const char* last_launch() {
+    return g_last_launch;
+}
+
+static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
+    static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel"};
+    const int kid = (c.kernel >= 1 && c.kernel <= 4) ? c.kernel : 0;
+    snprintf(g_last_launch, sizeof(g_last_launch), "%s<G=%d,K=%d%s%s%s> block=%d tile=%d grid=%d P=%d",
+             names[kid], c.group_lanes, c.chunks_per_pass, a.seg_off ? ",varlen" : ",strided",
+             c.nt ? ",nt" : "", "", c.block, c.tile, c.grid, c.tile_pieces);
+}
+
 hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStream_t s) {
+    note_launch(c, args);
     SegBatchArgs a = args;
     a.tile = c.tile > 0 ? (uint32_t)c.tile : 0u;
     if (c.kernel == 4) {

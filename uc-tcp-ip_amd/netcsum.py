@@ -187,6 +187,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ReadStream.restype = i32
     L.NetUtil_MI355X_Tune.argtypes = [i32, i32]
     L.NetUtil_MI355X_Tune.restype = i32
+    L.NetUtil_MI355X_LastLaunch.argtypes = []
+    L.NetUtil_MI355X_LastLaunch.restype = ctypes.c_char_p
     L.NetUtil_MI355X_Version.argtypes = []
     L.NetUtil_MI355X_Version.restype = ctypes.c_char_p
     _lib = L
@@ -340,6 +342,10 @@ def read_stream(buf, n_bytes, sink, stream=None):
 
 def tune(key, value):
     _check(lib().NetUtil_MI355X_Tune(key, value), "NetUtil_MI355X_Tune")
+
+
+def last_launch() -> str:
+    return lib().NetUtil_MI355X_LastLaunch().decode()
 
 
 def version() -> str:
