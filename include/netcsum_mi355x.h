@@ -131,6 +131,53 @@ NET_ERR  NetUtil_MI355X_ChkSumBatchStridedHost(const void  *h_seg,
                                                uint32_t     n_chunks);
 
 /* ============================================================================================
+ * (2b) IPv4 packet batches. Packet i = one IPv4 datagram starting at
+ * its IP header: d_base + d_off[i] with d_len[i] bytes present (d_off/d_len non-NULL), or
+ * d_base + i*stride with pkt_len bytes present (d_off = d_len = NULL). Any alignment.
+ *
+ * RxValidateIPv4 — one HBM pass per packet, d_flags[i] = NETCSUM_PKT_* bits:
+ *   IP_OK       NetUtil_16BitOnesCplChkSumHdrVerify(ip_hdr, IHL*4) == DEF_OK      (net_ipv4.c:5247)
+ *   L4_CHECKED  a transport checksum was verified: TCP (6), UDP (17) with a non-zero checksum
+ *               field, ICMP (1), IGMP (2); pseudo-header {src, dst, 0, proto, len} built from
+ *               the IP header (net_tcp.c:7851-7857, net_udp.c:1918-1934)
+ *   L4_OK       that verification passed (also set for UDP_NO_CSUM: accepted, net_udp.c:1971)
+ *   UDP_NO_CSUM UDP checksum field 0 (no checksum transmitted)
+ *   MALFORMED   IP version/IHL/total length inconsistent with the bytes present: no verdict
+ *   FRAGMENT    MF or fragment offset set: IP verdict only
+ *   L4_MALFORMED transport length invalid (TCP < 20 B, UDP length != IP datagram length)
+ * TxFinalizeIPv4 — computes and writes back, IN PLACE, the IPv4 header checksum and the
+ *   TCP/UDP/ICMP/IGMP checksum (fields treated as zero; UDP 0x0000 sent as 0xFFFF, RFC 768;
+ *   udp_tx_csum = 0 writes 0 = no UDP checksum, NET_UDP_CFG_TX_CHK_SUM_EN); d_flags optional
+ *   (IP_OK = IP checksum written, L4_CHECKED = transport checksum written).
+ * ============================================================================================ */
+#define NETCSUM_PKT_IP_OK         0x01u
+#define NETCSUM_PKT_L4_OK         0x02u
+#define NETCSUM_PKT_L4_CHECKED    0x04u
+#define NETCSUM_PKT_UDP_NO_CSUM   0x08u
+#define NETCSUM_PKT_MALFORMED     0x10u
+#define NETCSUM_PKT_FRAGMENT      0x20u
+#define NETCSUM_PKT_L4_MALFORMED  0x40u
+
+NET_ERR  NetUtil_MI355X_RxValidateIPv4     (const void      *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            void            *hip_stream);
+
+NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            int              udp_tx_csum,
+                                            void            *hip_stream);
+
+/* ============================================================================================
  * (3) Support entry points.
  * ============================================================================================ */
 

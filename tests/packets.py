@@ -1,0 +1,86 @@
+"""Random IPv4 packet generator for the packet-batch tests (TCP, UDP, UDP without checksum, ICMP,
+IGMP, other protocols, fragments, IP options, malformed headers/lengths, corrupted checksums)."""
+from __future__ import annotations
+
+import random
+import struct
+
+import numpy as np
+
+import oracle_packets as op
+
+KINDS = ["tcp", "tcp", "udp", "udp", "udp0", "icmp", "igmp", "other", "frag", "bad_ver", "bad_ihl",
+         "bad_tot", "udp_badlen", "tcp_short", "corrupt_ip", "corrupt_l4"]
+
+
+def make_packet(rng: random.Random, kind: str, payload: int | None = None) -> bytes:
+    ihl = rng.choice([5, 5, 5, 6, 8, 15])
+    opts = bytes(rng.getrandbits(8) for _ in range(ihl * 4 - 20))
+    payload = rng.randint(0, 1600) if payload is None else payload
+    data = bytes(rng.getrandbits(8) for _ in range(payload))
+    if kind in ("tcp", "tcp_short", "corrupt_l4", "frag", "corrupt_ip"):
+        proto = 6
+        thl = rng.choice([20, 20, 32, 60])
+        l4 = struct.pack("!HHIIBBHHH", rng.getrandbits(16), rng.getrandbits(16), rng.getrandbits(32),
+                         rng.getrandbits(32), (thl // 4) << 4, 0x18, 0xFFFF, 0, 0) + bytes(thl - 20) + data
+        if kind == "tcp_short":
+            l4 = l4[:rng.randint(0, 19)]
+    elif kind in ("udp", "udp0", "udp_badlen"):
+        proto = 17
+        ulen = 8 + len(data)
+        if kind == "udp_badlen":
+            ulen = (ulen + rng.choice([-3, -1, 1, 5])) & 0xFFFF
+        l4 = struct.pack("!HHHH", rng.getrandbits(16), rng.getrandbits(16), ulen, 0) + data
+    elif kind == "icmp":
+        proto = 1
+        l4 = struct.pack("!BBHHH", 8, 0, 0, rng.getrandbits(16), rng.getrandbits(16)) + data
+    elif kind == "igmp":
+        proto = 2
+        l4 = struct.pack("!BBH4s", 0x16, 0, 0, bytes(rng.getrandbits(8) for _ in range(4)))
+    else:
+        proto = rng.choice([41, 47, 50, 89, 132])
+        l4 = data
+    tot = ihl * 4 + len(l4)
+    frag = 0x4000
+    if kind == "frag":
+        frag = rng.choice([0x2000, 0x2000 | rng.randint(1, 0x1FFF), rng.randint(1, 0x1FFF)])
+    ver_ihl = (4 << 4) | ihl
+    if kind == "bad_ver":
+        ver_ihl = (rng.choice([0, 6, 15]) << 4) | ihl
+    if kind == "bad_ihl":
+        ver_ihl = (4 << 4) | rng.randint(0, 4)
+    hdr = struct.pack("!BBHHHBBH4s4s", ver_ihl, 0, tot & 0xFFFF, rng.getrandbits(16), frag, 64, proto, 0,
+                      bytes(rng.getrandbits(8) for _ in range(4)), bytes(rng.getrandbits(8) for _ in range(4)))
+    pkt = hdr + opts + l4
+    if kind not in ("bad_ver", "bad_ihl", "bad_tot"):
+        pkt, _ = op.tx_finalize(pkt, udp_tx_csum=(kind != "udp0"))
+    if kind == "bad_tot":
+        b = bytearray(pkt)
+        b[2:4] = struct.pack("!H", len(pkt) + rng.randint(1, 40))
+        pkt = bytes(b)
+    if kind == "corrupt_ip":
+        b = bytearray(pkt)
+        b[8] ^= 1 << rng.randint(0, 7)
+        pkt = bytes(b)
+    if kind == "corrupt_l4" and len(pkt) > ihl * 4 + 20:
+        b = bytearray(pkt)
+        k = rng.randint(ihl * 4, len(b) - 1)
+        b[k] ^= 1 << rng.randint(0, 7)
+        pkt = bytes(b)
+    return pkt
+
+
+def packed_batch(pkts, rng: random.Random, trailer=True, lead=1):
+    """Pack packets back to back (odd starts) with optional trailing bytes (e.g. Ethernet padding).
+    -> (buffer uint8, offsets uint64, lengths uint16 = bytes present per packet)."""
+    offs, lens, parts = [], [], [bytes(lead)]
+    pos = lead
+    for p in pkts:
+        extra = bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 5))) if trailer else b""
+        offs.append(pos)
+        lens.append(len(p) + len(extra))
+        parts.append(p + extra)
+        pos += len(p) + len(extra)
+    parts.append(bytes(64))
+    buf = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    return buf, np.array(offs, np.uint64), np.array(lens, np.uint16)

@@ -1,0 +1,103 @@
+"""GPU parity of the IPv4 packet batches (fused Rx validation, Tx finalize with write-back) against
+the packet oracle, which composes the C oracle's reference functions per packet."""
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle_packets as op
+from packets import KINDS, make_packet, packed_batch
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _defaults():
+    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES):
+        netcsum.tune(k, 0)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+    netcsum.tune(netcsum.TUNE_TILE, -1)
+    yield
+    for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES):
+        netcsum.tune(k, 0)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+    netcsum.tune(netcsum.TUNE_TILE, -1)
+
+
+def _rx_gpu(buf, offs, lens):
+    b = torch.from_numpy(buf).to(DEV)
+    o = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    f = torch.zeros(len(offs), dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv4(b, len(offs), f, off=o, lens=ln)
+    torch.cuda.synchronize()
+    return f.cpu().numpy()
+
+
+@pytest.mark.parametrize("group", [0, 8, 16, 32, 64])
+@pytest.mark.parametrize("grid,tile", [(0, -1), (3, 0)])
+def test_rx_validate_mixed_varlen(group, grid, tile):
+    rng = random.Random(group * 7 + grid)
+    pkts = [make_packet(rng, rng.choice(KINDS)) for _ in range(1500)]
+    buf, offs, lens = packed_batch(pkts, rng)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+    netcsum.tune(netcsum.TUNE_TILE, tile)
+    got = _rx_gpu(buf, offs, lens)
+    want = np.array([op.rx_validate(bytes(buf[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(pkts[i][:24].hex(), int(got[i]), int(want[i])) for i in bad[:5]]
+
+
+def test_rx_validate_strided_c2_shape():
+    """1500-B TCP datagrams in a strided batch (the C2 shape with real IP/TCP headers)."""
+    rng = random.Random(11)
+    n = 4000
+    pkts = [make_packet(rng, rng.choice(["tcp", "tcp", "corrupt_l4", "corrupt_ip"]), payload=1500 - 40)
+            for _ in range(n)]
+    L = 1500
+    buf = np.zeros(n * L + 64, np.uint8)
+    for i, p in enumerate(pkts):
+        p = p[:L]
+        buf[i * L:i * L + len(p)] = np.frombuffer(p, np.uint8)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv4(b, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    want = np.array([op.rx_validate(bytes(buf[i * L:(i + 1) * L])) for i in range(n)], np.uint8)
+    assert np.array_equal(f.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("udp_tx_csum", [True, False])
+def test_tx_finalize_writes_reference_checksums_then_rx_accepts(udp_tx_csum):
+    rng = random.Random(21 + udp_tx_csum)
+    kinds = ["tcp", "udp", "udp", "icmp", "igmp", "other", "frag", "udp_badlen", "tcp_short", "bad_ver"]
+    pkts = []
+    for _ in range(2000):
+        p = bytearray(make_packet(rng, rng.choice(kinds)))
+        if len(p) >= 12 and rng.random() < 0.5:
+            p[10:12] = bytes([rng.getrandbits(8), rng.getrandbits(8)])   # stale checksum fields
+        pkts.append(bytes(p))
+    buf, offs, lens = packed_batch(pkts, rng)
+    b = torch.from_numpy(buf).to(DEV)
+    o = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    f = torch.zeros(len(pkts), dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b, len(pkts), f, off=o, lens=ln, udp_tx_csum=udp_tx_csum)
+    torch.cuda.synchronize()
+    out = b.cpu().numpy()
+    flags = f.cpu().numpy()
+    for i, (off, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        pkt = bytes(buf[off:off + n])
+        want_pkt, want_f = op.tx_finalize(pkt, udp_tx_csum)
+        assert bytes(out[off:off + n]) == want_pkt, (i, pkt[:24].hex())
+        assert flags[i] == want_f, (i, flags[i], want_f)
+    # the finalized batch validates on the GPU Rx path
+    got = _rx_gpu(out, offs, lens)
+    ok = ((got & op.MALFORMED) == 0)
+    assert ((got[ok] & op.IP_OK) != 0).all()
+    checked = ok & ((got & op.L4_CHECKED) != 0)
+    assert ((got[checked] & op.L4_OK) != 0).all()

@@ -398,6 +398,54 @@ NET_ERR NetUtil_MI355X_StreamSum32(const NETCSUM_SPAN* spans, uint32_t n_spans, 
     return NET_UTIL_ERR_NONE;
 }
 
+static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
+                         CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum, bool tx,
+                         void* hip_stream) {
+    if (n_pkt == 0) return NET_UTIL_ERR_NONE;
+    if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr)) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    netcsum::PktBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.off = d_off;
+    a.len = d_len;
+    a.stride = stride;
+    a.len_u = pkt_len;
+    a.n = n_pkt;
+    a.flags_out = d_flags;
+    a.udp_tx_csum = udp_tx_csum ? 1u : 0u;
+    netcsum::LaunchCfg c{};
+    const uint32_t chunks = d_off ? 288u : ((uint32_t)pkt_len + 30u) / 16u;
+    int g = g_tune_group.load();
+    if (g < 8) {
+        g = d_off ? 32 : std::max(8, pow2_group((chunks + 5u) / 6u));
+    }
+    c.group_lanes = pow2_group((uint32_t)g);
+    c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks + c.group_lanes - 1u) / c.group_lanes));
+    const int nt = g_tune_nt.load();
+    c.nt = nt >= 0 ? (nt != 0) : true;
+    c.grid = g_tune_grid.load();
+    const int tile = g_tune_tile.load();
+    a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 4u);
+    NC_HIP(netcsum::launch_pkt_batch(a, c, tx, static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_RxValidateIPv4(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
+                                      uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags,
+                                      void* hip_stream) {
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, hip_stream);
+}
+
+NET_ERR NetUtil_MI355X_TxFinalizeIPv4(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
+                                      CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
+                                      void* hip_stream) {
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, hip_stream);
+}
+
 NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern,
                             void* hip_stream) {
     if (n_bytes == 0) return NET_UTIL_ERR_NONE;

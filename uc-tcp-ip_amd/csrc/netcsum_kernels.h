@@ -36,6 +36,20 @@ struct LaunchCfg {
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
 };
 
+struct PktBatchArgs {
+    const uint8_t*  base;          // packet i starts at base + off[i] (varlen) or base + i*stride
+    const uint64_t* off;           // nullptr => strided
+    const uint16_t* len;           // varlen: bytes of packet i present in the buffer
+    uint64_t        stride;
+    uint32_t        len_u;         // strided: bytes present per packet
+    uint32_t        n;
+    uint8_t*        flags_out;     // NETCSUM_PKT_* per packet (optional for Tx)
+    uint32_t        tile;          // segments (packets) per group per block tile (0 = grid-stride)
+    uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
+};
+
+hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s);
+
 bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation
 const char* last_launch();                  // description of this thread's last batch launch
 

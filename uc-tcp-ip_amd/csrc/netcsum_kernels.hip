@@ -33,59 +33,10 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include "netcsum_device.h"
 #include "netcsum_kernels.h"
 
 namespace netcsum {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-// Global-address-space view: addresses are computed as integers (absolute 16-B frame), and an
-// explicit addrspace(1) pointer keeps the loads on global_load_* (not flat_load_*, which would
-// also count on lgkmcnt and add a flat-aperture check).
-typedef const __attribute__((address_space(1))) u32x4 gu32x4;
-
-__device__ __forceinline__ uint32_t fold16(uint32_t s) {
-    s = (s & 0xFFFFu) + (s >> 16);
-    s = (s & 0xFFFFu) + (s >> 16);
-    return s;                                   // in [0, 0xFFFF]; 0 iff the input was 0
-}
-
-__device__ __forceinline__ uint32_t rot8(uint32_t s16) {   // x * 256 mod 65535 on a 16-bit value
-    return ((s16 << 8) | (s16 >> 8)) & 0xFFFFu;
-}
-
-template <bool NT>
-__device__ __forceinline__ u32x4 load16(gu32x4* p) {
-    if constexpr (NT) {
-        return __builtin_nontemporal_load(p);
-    } else {
-        return *p;
-    }
-}
-
-__device__ __forceinline__ uint32_t sum4(u32x4 v, uint32_t acc) {
-    acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
-    acc = __builtin_amdgcn_sad_u16(v.w, 0u, acc);
-    return acc;
-}
-
-// Keep bytes [lo, hi) of a dword whose first byte is byte `base` of its chunk.
-__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int base) {
-    int l = min(max(lo - base, 0), 4);
-    int h = min(max(hi - base, 0), 4);
-    uint32_t mh = (h >= 4) ? 0xFFFFFFFFu : ((1u << (8 * h)) - 1u);
-    uint32_t ml = (l >= 4) ? 0u : (0xFFFFFFFFu << (8 * l));
-    return mh & ml;
-}
-
-__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi) {
-    v.x &= dword_mask(lo, hi, 0);
-    v.y &= dword_mask(lo, hi, 4);
-    v.z &= dword_mask(lo, hi, 8);
-    v.w &= dword_mask(lo, hi, 12);
-    return v;
-}
 
 // Sum (in the absolute LE frame) of the byte span [a, a+len) by the G lanes of a group; K chunks
 // per lane per pass. Returns the lane's 32-bit partial.
@@ -117,15 +68,6 @@ __device__ __forceinline__ uint32_t span_partial(uintptr_t a, uint32_t len, int 
         }
     }
     return acc;
-}
-
-template <int G>
-__device__ __forceinline__ uint32_t group_sum(uint32_t s) {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1) {
-        s += __shfl_xor(s, m, 64);
-    }
-    return s;
 }
 
 // Segment -> group mapping. Tile mode (P.tile = J > 0): block b owns the contiguous tile
@@ -212,12 +154,6 @@ __global__ void __launch_bounds__(256) seg_batch_kernel(SegBatchArgs P) {
 // issued BEFORE the data loads they gate, so waiting for a descriptor never drains the data
 // stream (vmcnt retires in issue order).
 // ---------------------------------------------------------------------------------------------
-__device__ u32x4 g_zero_chunk[4];
-
-__device__ __forceinline__ uintptr_t zero_addr() {
-    return reinterpret_cast<uintptr_t>(&g_zero_chunk[0]);
-}
-
 template <int K>
 struct SegStage {
     u32x4    v[K];
@@ -227,10 +163,6 @@ struct SegStage {
     uint32_t plead;     // same for the pseudo-header
     uint32_t plen;      // pseudo-header bytes of THIS stage (0 for a dummy / past-the-end stage)
 };
-
-__device__ __forceinline__ uint32_t span_chunks(uintptr_t a, uint32_t len) {
-    return len ? (uint32_t)((a + len - (a & ~(uintptr_t)15) + 15) >> 4) : 0u;
-}
 
 template <int G, int K, bool NT>
 __device__ __forceinline__ void stage_issue(SegStage<K>& st, uintptr_t a, uint32_t len, uintptr_t pa,
@@ -251,18 +183,6 @@ __device__ __forceinline__ void stage_issue(SegStage<K>& st, uintptr_t a, uint32
     const uint32_t pnch = (plen + st.plead + 15u) >> 4;
     const uintptr_t paddr = ((uint32_t)lane < pnch) ? ((pa & ~(uintptr_t)15) + 16u * (uintptr_t)lane) : z;
     st.pv = load16<false>(reinterpret_cast<gu32x4*>(paddr));
-}
-
-// Mask chunk c of a span given in span-relative terms: the span covers bytes [lead, rend) of its
-// 16-B-aligned chunk sequence (rend = lead + len). 32-bit arithmetic only.
-__device__ __forceinline__ u32x4 edge_mask_rel(u32x4 v, uint32_t c, uint32_t lead, uint32_t rend) {
-    const uint32_t q = 16u * c;
-    const int lo = (c == 0u) ? (int)lead : 0;
-    const int hi = (rend - q < 16u) ? (int)(rend - q) : 16;
-    if (lo != 0 || hi != 16) {
-        v = mask_chunk(v, lo, hi);
-    }
-    return v;
 }
 
 // Folded 16-bit contribution of (pseudo ‖ segment) held by this lane, stream parity applied.
@@ -438,23 +358,6 @@ __global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
 // descriptor loads) was issued after Y.
 // LDS: 2 stages x (K+1) slots x 1 KiB per wave.
 // ---------------------------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 9, "extend wait_vmcnt");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-}
-
-typedef __attribute__((address_space(3))) void lds_void;
-
 template <int K>
 struct LdsStage {
     uint32_t lead;

@@ -1,0 +1,385 @@
+// netcsum_packets.hip — gfx950 IPv4 packet-batch kernels.
+//
+// RX (fused validation, one HBM pass per packet): for every received IPv4 datagram
+//   ip_ok = NetUtil_16BitOnesCplChkSumHdrVerify(ip_hdr, IHL*4)               net_ipv4.c:5247
+//   l4_ok = TCP : DataVerify(seg, {src,dst,0,6,  IP datagram len}, 12)        net_tcp.c:7857
+//           UDP : checksum field 0 -> "no checksum", accepted                 net_udp.c:1916-1920,1971
+//                 else DataVerify(dgram, {src,dst,0,17, UDP len}, 12)         net_udp.c:1934
+//           ICMP: DataVerify(msg, NULL, 0)                                    net_icmpv4.c:1676
+//           IGMP: HdrVerify(msg, msg len)                                     net_igmp.c:1332
+//   with the pseudo-header built in registers from the IP header, instead of two passes
+//   (header verify, then transport verify) over HBM.
+// TX (finalize, in place): the same sums with the checksum fields treated as zero (callers zero
+//   them first, net_ipv4.c:9573), then the checksums are written back:
+//   IP header (offset 10)                 NetUtil_16BitOnesCplChkSumHdrCalc   net_ipv4.c:9578,9586
+//   TCP (hlen+16)                         DataCalc + pseudo-header            net_tcp.c:29824,29862
+//   UDP (hlen+6), 0x0000 -> 0xFFFF        DataCalc + pseudo-header            net_udp.c:2891,2929-2937
+//       (or 0 when UDP Tx checksums are disabled, NET_UDP_CFG_TX_CHK_SUM_EN, net_udp.c:2935)
+//   ICMP / IGMP (hlen+2)                  DataCalc / HdrCalc                  net_icmpv4.c:2204, net_igmp.c:1692
+//
+// Validation order follows the reference: a malformed IPv4 header (version, IHL, total length
+// vs. bytes received; net_ipv4.c:5123-5254) or transport length (net_tcp.c:7808-7818,
+// net_udp.c:1893-1907) means no checksum verdict for that layer. Fragments (MF or offset != 0)
+// get the IP verdict only: their transport checksum covers the reassembled datagram
+// (net_ipv4.c:6523), which a per-packet batch does not have.
+//
+// Work decomposition: the pipelined v2 structure of netcsum_kernels.hip (G >= 8 lanes per
+// packet, K chunks per lane per pass, the next packet's loads in flight while the current one is
+// reduced). Header fields are extracted from the loaded chunks with cross-lane shuffles and
+// v_alignbyte_b32, so no load depends on packet contents. Two region sums (IP header, transport
+// part) per packet; each region starts at an even packet offset, so the packet's address parity
+// decides the rotation of both.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "netcsum_device.h"
+#include "netcsum_kernels.h"
+
+namespace netcsum {
+
+namespace {
+
+constexpr uint32_t F_IP_OK = 0x01u, F_L4_OK = 0x02u, F_L4_CHECKED = 0x04u, F_UDP_NO_CSUM = 0x08u,
+                   F_MALFORMED = 0x10u, F_FRAGMENT = 0x20u, F_L4_MALFORMED = 0x40u;
+
+template <int K>
+struct PktStage {
+    u32x4     v[K];
+    uint32_t  lead;      // packet start offset inside its first 16-B chunk
+    uint32_t  avail;     // bytes of the packet present in the buffer
+    uintptr_t a;         // packet start address
+};
+
+template <int G, int K, bool NT>
+__device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane) {
+    st.a = a;
+    st.lead = (uint32_t)(a & 15u);
+    st.avail = avail;
+    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uint32_t nch = (avail + st.lead + 15u) >> 4;
+    const uintptr_t z = zero_addr();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        st.v[k] = load16<NT>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z));
+    }
+}
+
+__device__ __forceinline__ uint32_t pick4(u32x4 v, uint32_t comp) {
+    uint32_t r = v.x;
+    r = (comp == 1u) ? v.y : r;
+    r = (comp == 2u) ? v.z : r;
+    r = (comp == 3u) ? v.w : r;
+    return r;
+}
+
+// Little-endian dword at packet offset i (lead + i + 7 < 16*G: the bytes sit in chunk slot 0 of
+// the group's lanes). All lanes of the group get the same value.
+__device__ __forceinline__ uint32_t pkt_dword(u32x4 v0, uint32_t lead, uint32_t i, int gbase) {
+    const uint32_t r = lead + i;
+    const uint32_t t = r >> 2;
+    const uint32_t lo = (uint32_t)__shfl((int)pick4(v0, t & 3u), gbase + (int)(t >> 2), 64);
+    const uint32_t hi = (uint32_t)__shfl((int)pick4(v0, (t + 1u) & 3u), gbase + (int)((t + 1u) >> 2), 64);
+    const uint32_t b = r & 3u;
+    return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+}
+
+__device__ __forceinline__ uint32_t be16_at(uint32_t dw, int byte) {   // bytes byte, byte+1 of dw, BE
+    return (((dw >> (8 * byte)) & 0xFFu) << 8) | ((dw >> (8 * byte + 8)) & 0xFFu);
+}
+
+// Bytes of chunk c (span-relative: the packet occupies frame bytes [lead, ...)) that fall in the
+// packet-offset range [r0, r1), minus the 2-byte hole at packet offset h (h = ~0u: no hole).
+__device__ __forceinline__ u32x4 region_chunk(u32x4 v, uint32_t c, uint32_t lead, uint32_t r0, uint32_t r1,
+                                              uint32_t h) {
+    const int q = (int)(16u * c) - (int)lead;                  // packet offset of the chunk's byte 0
+    int lo = (int)r0 - q, hi = (int)r1 - q;
+    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
+    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
+    if (hi <= lo) {
+        return u32x4{0u, 0u, 0u, 0u};
+    }
+    if (lo != 0 || hi != 16) {
+        v = mask_chunk(v, lo, hi);
+    }
+    const int hh = (int)h - q;
+    if (h != ~0u && hh > -2 && hh < 16) {                       // punch the checksum-field hole
+        const int h0 = hh < 0 ? 0 : hh, h1 = hh + 2 > 16 ? 16 : hh + 2;
+        const u32x4 keep_lo = mask_chunk(v, 0, h0);
+        const u32x4 keep_hi = mask_chunk(v, h1, 16);
+        v = keep_lo | keep_hi;
+    }
+    return v;
+}
+
+struct PktInfo {
+    uint32_t flags;
+    uint32_t hlen;
+    uint32_t l4_end;       // packet offset one past the transport part
+    uint32_t l4_csum_off;  // packet offset of the transport checksum field (~0u: none)
+    uint32_t pseudo_le;    // little-endian word sum of the pseudo-header (0: none)
+    uint32_t proto;
+    bool     check_l4;
+};
+
+template <bool TX>
+__device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
+    PktInfo p{};
+    p.l4_csum_off = ~0u;
+    const uint32_t d0 = pkt_dword(v0, lead, 0u, gbase);
+    const uint32_t d1 = pkt_dword(v0, lead, 4u, gbase);
+    const uint32_t d2 = pkt_dword(v0, lead, 8u, gbase);
+    const uint32_t d3 = pkt_dword(v0, lead, 12u, gbase);
+    const uint32_t d4 = pkt_dword(v0, lead, 16u, gbase);
+    const uint32_t ver = (d0 >> 4) & 0xFu;
+    p.hlen = (d0 & 0xFu) * 4u;
+    const uint32_t tot = be16_at(d0, 2);
+    const uint32_t frag = be16_at(d1, 2) & 0x3FFFu;              // MF | fragment offset
+    p.proto = (d2 >> 8) & 0xFFu;
+    if (avail < 20u || ver != 4u || p.hlen < 20u || tot < p.hlen || tot > avail) {
+        p.flags = F_MALFORMED;
+        p.l4_end = 0u;
+        p.hlen = 0u;
+        return p;
+    }
+    p.l4_end = tot;
+    if (frag != 0u) {
+        p.flags |= F_FRAGMENT;
+        return p;
+    }
+    const uint32_t l4len = tot - p.hlen;
+    const uint32_t src_dst = __builtin_amdgcn_sad_u16(d3, 0u, __builtin_amdgcn_sad_u16(d4, 0u, 0u));
+    switch (p.proto) {
+    case 6u:                                                     // TCP: length = IP datagram length
+        if (l4len < 20u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = p.hlen + 16u;
+        p.pseudo_le = src_dst + (6u << 8) + (((l4len & 0xFFu) << 8) | (l4len >> 8));
+        break;
+    case 17u: {                                                  // UDP
+        if (l4len < 8u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        const uint32_t du = pkt_dword(v0, lead, p.hlen + 4u, gbase);
+        const uint32_t udp_len = be16_at(du, 0);
+        if (udp_len != l4len) {                                  // net_udp.c:1903-1907 (also < 8)
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = p.hlen + 6u;
+        if (!TX && (du >> 16) == 0u) {                           // no checksum transmitted
+            p.flags |= F_UDP_NO_CSUM | F_L4_OK;
+            return p;
+        }
+        if (TX && !udp_tx_csum) {
+            p.flags |= F_UDP_NO_CSUM;                            // write 0 (NET_UDP_HDR_CHK_SUM_NONE)
+            p.check_l4 = false;
+            return p;
+        }
+        p.check_l4 = true;
+        p.pseudo_le = src_dst + (17u << 8) + (((udp_len & 0xFFu) << 8) | (udp_len >> 8));
+        break;
+    }
+    case 1u:                                                     // ICMPv4, no pseudo-header
+    case 2u:                                                     // IGMP
+        if (l4len < 4u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = p.hlen + 2u;
+        break;
+    default:
+        break;
+    }
+    return p;
+}
+
+template <int G>
+__device__ __forceinline__ void store_csum(uintptr_t a, uint32_t off, uint32_t host_val) {
+    uint8_t* p = reinterpret_cast<uint8_t*>(a + off);          // memcpy of the host-order value
+    p[0] = (uint8_t)(host_val & 0xFFu);
+    p[1] = (uint8_t)(host_val >> 8);
+}
+
+template <int G, int K, bool NT, bool TX>
+__device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, int lane,
+                                            int gbase) {
+    const uint32_t lead = st.lead;
+    PktInfo p = pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
+    const uint32_t hole_ip = TX ? 10u : ~0u;
+    const uint32_t hole_l4 = TX ? p.l4_csum_off : ~0u;
+    const uint32_t l4_begin = p.check_l4 ? p.hlen : p.l4_end;     // empty transport region if unchecked
+    uint32_t acc_ip = 0u, acc_l4 = 0u;
+    const uint32_t nch = (p.l4_end + lead + 15u) >> 4;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t c = (uint32_t)(k * G + lane);
+        if (c < nch) {
+            acc_ip = sum4(region_chunk(st.v[k], c, lead, 0u, p.hlen, hole_ip), acc_ip);
+            acc_l4 = sum4(region_chunk(st.v[k], c, lead, l4_begin, p.l4_end, hole_l4), acc_l4);
+        }
+    }
+    if (nch > (uint32_t)(G * K)) {                               // packets longer than one pass
+        const uintptr_t q0 = st.a & ~(uintptr_t)15;
+        for (uint32_t c0 = (uint32_t)(G * K); c0 < nch; c0 += (uint32_t)(G * K)) {
+            u32x4 w[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * G + lane);
+                w[k] = load16<NT>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : zero_addr()));
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * G + lane);
+                if (c < nch) {
+                    acc_l4 = sum4(region_chunk(w[k], c, lead, l4_begin, p.l4_end, hole_l4), acc_l4);
+                }
+            }
+        }
+    }
+    uint32_t sip = fold16(acc_ip), sl4 = fold16(acc_l4);
+    if (lead & 1u) {                                              // both regions start at even offsets
+        sip = rot8(sip);
+        sl4 = rot8(sl4);
+    }
+    sip = fold16(group_sum<G>(sip));
+    sl4 = fold16(group_sum<G>(sl4) + p.pseudo_le);
+    if (lane != 0) {
+        return;
+    }
+    uint32_t f = p.flags;
+    if (!(f & F_MALFORMED)) {
+        if (!TX) {
+            f |= (sip == 0xFFFFu) ? F_IP_OK : 0u;
+            if (p.check_l4) {
+                f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
+            }
+        } else {
+            store_csum<G>(st.a, 10u, (~sip) & 0xFFFFu);
+            f |= F_IP_OK;
+            if (p.check_l4) {
+                uint32_t c = (~sl4) & 0xFFFFu;
+                if (p.proto == 17u && c == 0u) {
+                    c = 0xFFFFu;                                 // RFC 768 (net_udp.c:2929-2931)
+                }
+                store_csum<G>(st.a, p.l4_csum_off, c);
+                f |= F_L4_CHECKED | F_L4_OK;
+            } else if ((f & F_UDP_NO_CSUM) && p.l4_csum_off != ~0u) {
+                store_csum<G>(st.a, p.l4_csum_off, 0u);
+            }
+        }
+    }
+    if (A.flags_out) {
+        A.flags_out[idx] = (uint8_t)f;
+    }
+}
+
+template <bool VARLEN>
+__device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint64_t& off, uint32_t& avail) {
+    if constexpr (VARLEN) {
+        const uint32_t ic = (i < A.n) ? i : 0u;
+        off = A.off[ic];
+        avail = A.len[ic];
+    } else {
+        off = (uint64_t)i * A.stride;
+        avail = A.len_u;
+    }
+}
+
+template <int G, int K, bool VARLEN, bool NT, bool TX>
+__global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
+    static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
+    const int lane = (int)(threadIdx.x & (G - 1));
+    const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+    const uint32_t gpb = blockDim.x / G;
+    const uint32_t grp = threadIdx.x / G;
+    uint32_t first, step, end;
+    if (A.tile) {
+        const uint64_t t0 = (uint64_t)blockIdx.x * gpb * A.tile;
+        first = (uint32_t)t0 + grp;
+        step = gpb;
+        end = (uint32_t)min<uint64_t>(t0 + (uint64_t)gpb * A.tile, A.n);
+    } else {
+        first = blockIdx.x * gpb + grp;
+        step = gridDim.x * gpb;
+        end = A.n;
+    }
+    if (first >= end) {
+        return;
+    }
+    const uintptr_t base = (uintptr_t)A.base;
+    const uintptr_t z = zero_addr();
+    PktStage<K> S0, S1;
+    uint64_t off;
+    uint32_t avail;
+    uint32_t i = first;
+    pkt_desc<VARLEN>(A, i, off, avail);
+    pkt_issue<G, K, NT>(S0, base + off, avail, lane);
+    for (;;) {
+        uint32_t nx = i + step;
+        bool more = nx < end;
+        pkt_desc<VARLEN>(A, nx, off, avail);
+        pkt_issue<G, K, NT>(S1, more ? base + off : z, more ? avail : 0u, lane);
+        pkt_consume<G, K, NT, TX>(S0, A, i, lane, gbase);
+        if (!more) {
+            break;
+        }
+        i = nx;
+        nx = i + step;
+        more = nx < end;
+        pkt_desc<VARLEN>(A, nx, off, avail);
+        pkt_issue<G, K, NT>(S0, more ? base + off : z, more ? avail : 0u, lane);
+        pkt_consume<G, K, NT, TX>(S1, A, i, lane, gbase);
+        if (!more) {
+            break;
+        }
+        i = nx;
+    }
+}
+
+template <int G, int K, bool VARLEN, bool TX>
+hipError_t launch_pkt_gk(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    const uint32_t gpb = 256u / G;
+    int grid;
+    if (a.tile) {
+        const uint64_t per = (uint64_t)gpb * a.tile;
+        grid = (int)(((uint64_t)a.n + per - 1u) / per);
+    } else {
+        grid = c.grid > 0 ? c.grid : (int)(((uint64_t)a.n + gpb - 1u) / gpb);
+    }
+    if (c.nt) {
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, true, TX>), dim3(grid), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, false, TX>), dim3(grid), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+template <bool VARLEN, bool TX>
+hipError_t launch_pkt_v(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
+    switch (c.group_lanes) {
+    case 8:  return c.chunks_per_pass <= 4 ? launch_pkt_gk<8, 4, VARLEN, TX>(a, c, s)
+                                           : launch_pkt_gk<8, 8, VARLEN, TX>(a, c, s);
+    case 16: return c.chunks_per_pass <= 3 ? launch_pkt_gk<16, 3, VARLEN, TX>(a, c, s)
+                                           : launch_pkt_gk<16, 6, VARLEN, TX>(a, c, s);
+    case 32: return c.chunks_per_pass <= 3 ? launch_pkt_gk<32, 3, VARLEN, TX>(a, c, s)
+                                           : launch_pkt_gk<32, 6, VARLEN, TX>(a, c, s);
+    default: return launch_pkt_gk<64, 4, VARLEN, TX>(a, c, s);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
+    if (a.off) {
+        return tx ? launch_pkt_v<true, true>(a, c, s) : launch_pkt_v<true, false>(a, c, s);
+    }
+    return tx ? launch_pkt_v<false, true>(a, c, s) : launch_pkt_v<false, false>(a, c, s);
+}
+
+}  // namespace netcsum

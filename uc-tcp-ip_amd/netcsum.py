@@ -46,6 +46,8 @@ NET_PROTOCOL_TYPE_TCP_V6 = 73
 DEF_OK, DEF_FAIL = 1, 0
 
 OP_DATA_CALC, OP_DATA_VERIFY, OP_HDR_CALC, OP_HDR_VERIFY = 0, 1, 2, 3
+PKT_IP_OK, PKT_L4_OK, PKT_L4_CHECKED, PKT_UDP_NO_CSUM = 0x01, 0x02, 0x04, 0x08
+PKT_MALFORMED, PKT_FRAGMENT, PKT_L4_MALFORMED = 0x10, 0x20, 0x40
 TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
 TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
 
@@ -181,6 +183,10 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
                                               ctypes.POINTER(ctypes.c_uint32), i32]
     L.NetUtil_MI355X_ChainToSpans.restype = i32
+    L.NetUtil_MI355X_RxValidateIPv4.argtypes = [vp, vp, vp, u64, u16, u32, vp, vp]
+    L.NetUtil_MI355X_RxValidateIPv4.restype = i32
+    L.NetUtil_MI355X_TxFinalizeIPv4.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, vp]
+    L.NetUtil_MI355X_TxFinalizeIPv4.restype = i32
     L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, u64, i32, vp]
     L.NetUtil_MI355X_Fill.restype = i32
     L.NetUtil_MI355X_ReadStream.argtypes = [vp, u64, vp, vp]
@@ -324,6 +330,37 @@ def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_l
                                                       pseudo_len, n_seg, _p(out), op, n_chunks)
     if check:
         _check(err, "NetUtil_MI355X_ChkSumBatchStridedHost")
+    return err
+
+
+def _pkt_bounds(base, off, lens, stride, pkt_len, n, flags):
+    if not n:
+        return
+    if off is not None:
+        _require(off, 8 * n, "packet offsets")
+        _require(lens, 2 * n, "packet lengths")
+    else:
+        _require(base, (n - 1) * stride + pkt_len, "packets")
+    if flags is not None:
+        _require(flags, n, "flags")
+
+
+def rx_validate_ipv4(base, n, flags, off=None, lens=None, stride=0, pkt_len=0, stream=None, check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_RxValidateIPv4(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
+                                              _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_RxValidateIPv4")
+    return err
+
+
+def tx_finalize_ipv4(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, udp_tx_csum=True,
+                     stream=None, check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_TxFinalizeIPv4(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
+                                              int(bool(udp_tx_csum)), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_TxFinalizeIPv4")
     return err
 
 
