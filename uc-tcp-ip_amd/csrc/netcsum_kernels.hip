@@ -687,8 +687,11 @@ __global__ void __launch_bounds__(256) read_stream_lds_kernel(gu32x4* __restrict
 // v_sad_u16 adds the two big-endian words: exact, no modular folding (the u32 wrap of the
 // reference's cross-buffer `sum` is applied by the caller).
 // ---------------------------------------------------------------------------------------------
+// direct != 0 (single-block launches): thread 0 STORES the block total (no pre-zeroed accumulator
+// needed — the per-packet path reads pinned host memory zero-copy and writes the result straight
+// back into pinned host memory, one launch per call).
 __global__ void __launch_bounds__(256) stream_exact_kernel(gu32x4* __restrict__ p, uint32_t n16,
-                                                           unsigned long long* __restrict__ sum) {
+                                                           unsigned long long* __restrict__ sum, int direct) {
     __shared__ unsigned long long wsum[4];
     uint32_t acc = 0u;
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += gridDim.x * blockDim.x) {
@@ -712,7 +715,11 @@ __global__ void __launch_bounds__(256) stream_exact_kernel(gu32x4* __restrict__ 
         for (uint32_t i = 0; i < (blockDim.x >> 6); ++i) {
             t += wsum[i];
         }
-        atomicAdd(sum, t);
+        if (direct) {
+            *sum = t;
+        } else {
+            atomicAdd(sum, t);
+        }
     }
 }
 
@@ -1000,7 +1007,7 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s) {
     hipLaunchKernelGGL(stream_exact_kernel, dim3(grid), dim3(256), 0, s,
-                       reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sum);
+                       reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sum, grid == 1 ? 1 : 0);
     return hipGetLastError();
 }
 
