@@ -178,6 +178,32 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
                                             void            *hip_stream);
 
 /* ============================================================================================
+ * (2c) Batched NET_BUF chains. Chain i = its pseudo-header
+ * (d_pseudo + i*pseudo_stride, pseudo_len bytes; none if pseudo_len = 0) followed by pieces
+ * [d_chain_first[i], d_chain_first[i+1]) in order, piece j = d_base + d_piece_off[j] with
+ * d_piece_len[j] bytes (any alignment; d_chain_first holds n_chains + 1 entries). Each chain is
+ * checksummed as the single byte stream NetUtil_16BitOnesCplChkSumDataCalc / DataVerify
+ * (net_util.c:590, :716) walks for a NET_BUF chain whose buffers' (DataPtr + ix, len) are the
+ * pieces (NetUtil_MI355X_ChainToSpans resolves them): an odd-length piece carries its dangling
+ * octet into the next (net_util.c:1385-1393), the u32 accumulator wraps like the reference's
+ * (net_util.c:1685), so chains of any total length are bit-exact. A chain with NO pieces is the
+ * reference's pdata_buf == NULL case (an odd pseudo-header loses its last octet,
+ * net_util.c:1601-1611); describe a chain of empty buffers with one zero-length piece.
+ * op: NETCSUM_OP_DATA_CALC (u16 out) or NETCSUM_OP_DATA_VERIFY (u8 DEF_OK/DEF_FAIL out).
+ * ============================================================================================ */
+NET_ERR  NetUtil_MI355X_ChkSumBatchChains  (const void      *d_base,
+                                            const uint64_t  *d_piece_off,
+                                            const uint16_t  *d_piece_len,
+                                            const uint32_t  *d_chain_first,
+                                            const void      *d_pseudo,
+                                            uint32_t         pseudo_stride,
+                                            CPU_INT16U       pseudo_len,
+                                            uint32_t         n_chains,
+                                            void            *d_out,
+                                            NETCSUM_OP       op,
+                                            void            *hip_stream);
+
+/* ============================================================================================
  * (3) Support entry points.
  * ============================================================================================ */
 

@@ -10,6 +10,7 @@
 #include "net_util_oracle.h"
 
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -361,6 +362,44 @@ void Oracle_BatchVarLen(const uint8_t *base, const uint64_t *seg_off, const uint
         orc_one_segment(base + seg_off[i], seg_len[i],
                         pseudo ? pseudo + (uint64_t)i * pseudo_stride : NULL, pseudo_len,
                         out, (uint32_t)i, op);
+    }
+}
+
+/* Chain i = pieces [chain_first[i], chain_first[i+1]) linked as a NET_BUF chain (TCP_V4 buffers,
+ * DataPtr = base + piece_off[j], DataLen = piece_len[j]) and walked by Oracle_DataCalc/Verify with
+ * its pseudo-header — the reference's multi-buffer call (net_util.c:1611-1687). No pieces => the
+ * pdata_buf == NULL call. ops 0/1 only. */
+void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const uint16_t *piece_len,
+                        const uint32_t *chain_first, const uint8_t *pseudo, uint32_t pseudo_stride,
+                        uint16_t pseudo_len, uint32_t n_chains, void *out, int op, int n_threads)
+{
+    int64_t i;
+#ifdef _OPENMP
+    int nt = (n_threads > 0) ? n_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nt)
+#else
+    (void)n_threads;
+#endif
+    for (i = 0; i < (int64_t)n_chains; ++i) {
+        uint32_t p0 = chain_first[i], p1 = chain_first[i + 1], j, err;
+        uint32_t n = p1 - p0;
+        NET_BUF *bufs = (n != 0u) ? (NET_BUF *)malloc((size_t)n * sizeof(NET_BUF)) : NULL;
+        const uint8_t *ph = pseudo ? pseudo + (uint64_t)i * pseudo_stride : NULL;
+        for (j = 0; j < n; ++j) {
+            NET_BUF *b = &bufs[j];
+            b->Hdr.NextBufPtr      = (j + 1u < n) ? &bufs[j + 1u] : NULL;
+            b->Hdr.ProtocolHdrType = NET_PROTOCOL_TYPE_TCP_V4;
+            b->Hdr.TransportHdrIx  = 0u;
+            b->Hdr.TransportHdrLen = 0u;
+            b->Hdr.DataLen         = piece_len[p0 + j];
+            b->DataPtr             = (CPU_INT08U *)(base + piece_off[p0 + j]);
+        }
+        if (op == 0) {
+            ((uint16_t *)out)[i] = Oracle_DataCalc(bufs, ph, pseudo_len, &err, 0);
+        } else {
+            ((uint8_t *)out)[i] = Oracle_DataVerify(bufs, ph, pseudo_len, &err, 0);
+        }
+        free(bufs);
     }
 }
 

@@ -59,6 +59,9 @@ void Oracle_BatchVarLen (const uint8_t *base, const uint64_t *seg_off, const uin
 
 /* splitmix64-based synthetic bytes, identical to NetUtil_MI355X_Fill (pattern 0..3), for
  * regenerating any byte range on the host. */
+void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const uint16_t *piece_len,
+                        const uint32_t *chain_first, const uint8_t *pseudo, uint32_t pseudo_stride,
+                        uint16_t pseudo_len, uint32_t n_chains, void *out, int op, int n_threads);
 void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern);
 
 /* Number of OpenMP threads the batch drivers would use with n_threads = 0. */

@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
         L.Oracle_BatchStrided.restype = None
         L.Oracle_BatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
         L.Oracle_BatchVarLen.restype = None
+        L.Oracle_BatchChains.argtypes = [vp, vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
+        L.Oracle_BatchChains.restype = None
         L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
         L.Oracle_Fill.restype = None
         L.Oracle_MaxThreads.argtypes = []
@@ -123,6 +125,20 @@ def batch_varlen(base: np.ndarray, seg_off: np.ndarray, seg_len: np.ndarray, pse
     out = _out_array(n, op)
     lib().Oracle_BatchVarLen(base.ctypes.data, seg_off.ctypes.data, seg_len.ctypes.data, _ptr(pseudo),
                              pseudo_stride, pseudo_len, n, out.ctypes.data, op, n_threads)
+    return out
+
+
+def batch_chains(base: np.ndarray, piece_off: np.ndarray, piece_len: np.ndarray, chain_first: np.ndarray,
+                 pseudo, pseudo_stride: int, pseudo_len: int, n_chains: int, op: int = 0,
+                 n_threads: int = 0) -> np.ndarray:
+    """Reference per-chain DataCalc/DataVerify over NET_BUF chains built from the piece spans."""
+    piece_off = np.ascontiguousarray(piece_off, np.uint64)
+    piece_len = np.ascontiguousarray(piece_len, np.uint16)
+    chain_first = np.ascontiguousarray(chain_first, np.uint32)
+    assert len(chain_first) >= n_chains + 1 and int(chain_first[n_chains]) <= len(piece_off)
+    out = _out_array(n_chains, op)
+    lib().Oracle_BatchChains(base.ctypes.data, piece_off.ctypes.data, piece_len.ctypes.data, chain_first.ctypes.data,
+                             _ptr(pseudo), pseudo_stride, pseudo_len, n_chains, out.ctypes.data, op, n_threads)
     return out
 
 

@@ -446,6 +446,40 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     return NET_UTIL_ERR_NONE;
 }
 
+NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_piece_off,
+                                        const uint16_t* d_piece_len, const uint32_t* d_chain_first,
+                                        const void* d_pseudo, uint32_t pseudo_stride, CPU_INT16U pseudo_len,
+                                        uint32_t n_chains, void* d_out, NETCSUM_OP op, void* hip_stream) {
+    if (op != NETCSUM_OP_DATA_CALC && op != NETCSUM_OP_DATA_VERIFY) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (n_chains == 0) return NET_UTIL_ERR_NONE;
+    if (n_chains > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (d_out == nullptr || d_chain_first == nullptr || d_piece_off == nullptr || d_piece_len == nullptr ||
+        (d_pseudo == nullptr && pseudo_len != 0)) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    netcsum::ChainBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.off = d_piece_off;
+    a.len = d_piece_len;
+    a.first = d_chain_first;
+    a.pseudo = (pseudo_len != 0) ? static_cast<const uint8_t*>(d_pseudo) : nullptr;
+    a.pseudo_stride = pseudo_stride;
+    a.pseudo_len = pseudo_len;
+    a.n = n_chains;
+    a.verify = (op == NETCSUM_OP_DATA_VERIFY) ? 1u : 0u;
+    a.out = d_out;
+    int g = g_tune_group.load();
+    g = (g == 16 || g == 32 || g == 64) ? g : 64;
+    const uint32_t gpb = 256u / (uint32_t)g;
+    const uint64_t need = ((uint64_t)n_chains + gpb - 1u) / gpb;
+    int grid = g_tune_grid.load();
+    if (grid <= 0) grid = (int)std::min<uint64_t>(need, (uint64_t)cu_count(dev) * 16u);
+    NC_HIP(netcsum::launch_chain_batch(a, g, grid, static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
 NET_ERR NetUtil_MI355X_RxValidateIPv4(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
                                       uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags,
                                       void* hip_stream) {

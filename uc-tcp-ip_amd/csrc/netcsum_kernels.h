@@ -48,6 +48,21 @@ struct PktBatchArgs {
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
 };
 
+struct ChainBatchArgs {
+    const uint8_t*  base;          // piece j starts at base + off[j]
+    const uint64_t* off;
+    const uint16_t* len;
+    const uint32_t* first;         // chain i = pieces [first[i], first[i+1])
+    const uint8_t*  pseudo;        // nullptr => no pseudo-header
+    uint32_t        pseudo_stride;
+    uint32_t        pseudo_len;
+    uint32_t        n;
+    uint32_t        verify;
+    void*           out;
+};
+
+hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
+
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s);
 
 bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation

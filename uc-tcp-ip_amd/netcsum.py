@@ -176,6 +176,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ChkSumBatchStrided.restype = i32
     L.NetUtil_MI355X_ChkSumBatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, vp]
     L.NetUtil_MI355X_ChkSumBatchVarLen.restype = i32
+    L.NetUtil_MI355X_ChkSumBatchChains.argtypes = [vp, vp, vp, vp, vp, u32, u16, u32, vp, i32, vp]
+    L.NetUtil_MI355X_ChkSumBatchChains.restype = i32
     L.NetUtil_MI355X_ChkSumBatchStridedHost.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, u32]
     L.NetUtil_MI355X_ChkSumBatchStridedHost.restype = i32
     L.NetUtil_MI355X_StreamSum32.argtypes = [ctypes.POINTER(Span), u32, ctypes.POINTER(ctypes.c_uint32)]
@@ -330,6 +332,25 @@ def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_l
                                                       pseudo_len, n_seg, _p(out), op, n_chunks)
     if check:
         _check(err, "NetUtil_MI355X_ChkSumBatchStridedHost")
+    return err
+
+
+def batch_chains(base, piece_off, piece_len, chain_first, pseudo, pseudo_stride, pseudo_len, n_chains, out,
+                 op=OP_DATA_CALC, stream=None, check=True, n_pieces=None):
+    """Checksum n_chains NET_BUF chains (pieces [chain_first[i], chain_first[i+1]) after pseudo-header i).
+    n_pieces (= chain_first[n_chains], if the caller knows it) bounds-checks the piece arrays."""
+    if n_chains:
+        _require(chain_first, 4 * (n_chains + 1), "chain index")
+        if n_pieces is not None and n_pieces:
+            _require(piece_off, 8 * n_pieces, "piece offsets")
+            _require(piece_len, 2 * n_pieces, "piece lengths")
+        if pseudo is not None and pseudo_len:
+            _require(pseudo, (n_chains - 1) * pseudo_stride + pseudo_len, "pseudo-headers")
+        _require(out, n_chains * (2 if op == OP_DATA_CALC else 1), "out")
+    err = lib().NetUtil_MI355X_ChkSumBatchChains(_p(base), _p(piece_off), _p(piece_len), _p(chain_first), _p(pseudo),
+                                                 pseudo_stride, pseudo_len, n_chains, _p(out), op, _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_ChkSumBatchChains")
     return err
 
 
