@@ -58,6 +58,23 @@ __device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi) {
     return v;
 }
 
+// Makes a loaded chunk opaque to the optimiser, so its use cannot be sunk into a branch: every
+// CFG path then waits for the load, and no load stays "pending" across a loop back-edge (the
+// waitcnt pass would drain vmcnt(0) before the register is re-used, serialising the pipeline).
+__device__ __forceinline__ u32x4 opaque(u32x4 v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return v;
+}
+
+// Iterations of a group walking first, first + step, ... < end, and the wave-uniform trip count
+// (the wave's lane 0 has the smallest `first` of its groups, hence the most iterations). A loop
+// over the uniform count with per-group validity keeps exits scalar: a divergent `break` in the
+// middle of a software-pipelined loop leaves a CFG path that skips the consume of the in-flight
+// stage, which again makes the compiler drain vmcnt(0) at the loop head.
+__device__ __forceinline__ uint32_t group_iters(uint32_t first, uint32_t step, uint32_t end) {
+    return first < end ? (uint32_t)(((uint64_t)end - first + step - 1u) / step) : 0u;
+}
+
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
 #pragma unroll

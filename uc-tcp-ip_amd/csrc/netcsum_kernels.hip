@@ -200,12 +200,13 @@ __device__ __forceinline__ uint32_t stage_consume(const SegStage<K>& st, uintptr
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = (uint32_t)(k * G + lane);
-        u32x4 v = st.v[k];
+        u32x4 v = opaque(st.v[k]);
         if (c < nch) {
             v = edge_mask_rel(v, c, lead, rend);
         }
         acc = sum4(v, acc);
     }
+    const u32x4 pv = opaque(st.pv);
     if (nch > (uint32_t)(G * K)) {                   // segments longer than one pass
         const uintptr_t q0 = a & ~(uintptr_t)15;
         for (uint32_t c0 = (uint32_t)(G * K); c0 < nch; c0 += (uint32_t)(G * K)) {
@@ -235,7 +236,7 @@ __device__ __forceinline__ uint32_t stage_consume(const SegStage<K>& st, uintptr
         const uint32_t plead = st.plead;
         const uint32_t prend = plead + plen;
         const uint32_t pnch = (prend + 15u) >> 4;
-        u32x4 v = st.pv;
+        u32x4 v = pv;
         if ((uint32_t)lane < pnch) {
             v = edge_mask_rel(v, (uint32_t)lane, plead, prend);
         }
@@ -300,42 +301,52 @@ __global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
 
     const SegRange R = seg_range(P, gpb, threadIdx.x / G);
     const uint32_t step = R.step;
-    uint32_t seg = R.first;
-    if (seg >= R.end) {
+    const uint32_t cnt = group_iters(R.first, step, R.end);
+    const uint32_t iters = __builtin_amdgcn_readfirstlane(cnt);
+    if (iters == 0u) {
         return;
     }
+    uint32_t seg = R.first;
     SegStage<K> A, B;
     SegDesc<VARLEN> dn = seg_desc<VARLEN>(P, seg);
     SegDesc<VARLEN> dnn = seg_desc<VARLEN>(P, seg + step);      // two ahead
-    uintptr_t aA = base + dn.off, paA = pbase + (uint64_t)seg * P.pseudo_stride;
+    bool vA = cnt != 0u, vB = false;
+    uintptr_t aA = vA ? base + dn.off : z, paA = vA ? pbase + (uint64_t)seg * P.pseudo_stride : z;
     uintptr_t aB = z, paB = z;
-    stage_issue<G, K, NT>(A, aA, dn.len, paA, plen, lane);
+    stage_issue<G, K, NT>(A, aA, vA ? dn.len : 0u, paA, vA ? plen : 0u, lane);
     dn = dnn;
-    for (;;) {
-        // ---- consume A (segment `seg`) with B (seg + step) in flight. Past the end, B reads the
-        //      zero chunk: branch-free issue keeps the compiler's vmcnt counting exact.
+    // Wave-uniform trip count (group_iters): the only exits are scalar; a group past its own end
+    // runs dummy stages (zero-chunk loads) and stores nothing.
+    for (uint32_t j = 0u;; j += 2u) {
+        // ---- consume A (iteration j) with B (j + 1) in flight
         uint32_t nxt = seg + step;
-        bool has_next = nxt < R.end;
+        vB = j + 1u < cnt;
         dnn = seg_desc<VARLEN>(P, nxt + step);
-        aB = has_next ? base + dn.off : z;
-        paB = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
-        stage_issue<G, K, NT>(B, aB, has_next ? dn.len : 0u, paB, has_next ? plen : 0u, lane);
+        aB = vB ? base + dn.off : z;
+        paB = vB ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        stage_issue<G, K, NT>(B, aB, vB ? dn.len : 0u, paB, vB ? plen : 0u, lane);
         dn = dnn;
-        group_store<G>(P, seg, stage_consume<G, K, NT>(A, aA, paA, ph_odd, lane), lane);
-        if (!has_next) {
+        uint32_t r = stage_consume<G, K, NT>(A, aA, paA, ph_odd, lane);
+        if (vA) {                                             // uniform within the group
+            group_store<G>(P, seg, r, lane);
+        }
+        if (j + 1u >= iters) {
             break;
         }
         seg = nxt;
-        // ---- consume B with A in flight
+        // ---- consume B (j + 1) with A (j + 2) in flight
         nxt = seg + step;
-        has_next = nxt < R.end;
+        vA = j + 2u < cnt;
         dnn = seg_desc<VARLEN>(P, nxt + step);
-        aA = has_next ? base + dn.off : z;
-        paA = has_next ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
-        stage_issue<G, K, NT>(A, aA, has_next ? dn.len : 0u, paA, has_next ? plen : 0u, lane);
+        aA = vA ? base + dn.off : z;
+        paA = vA ? pbase + (uint64_t)nxt * P.pseudo_stride : z;
+        stage_issue<G, K, NT>(A, aA, vA ? dn.len : 0u, paA, vA ? plen : 0u, lane);
         dn = dnn;
-        group_store<G>(P, seg, stage_consume<G, K, NT>(B, aB, paB, ph_odd, lane), lane);
-        if (!has_next) {
+        r = stage_consume<G, K, NT>(B, aB, paB, ph_odd, lane);
+        if (vB) {
+            group_store<G>(P, seg, r, lane);
+        }
+        if (j + 2u >= iters) {
             break;
         }
         seg = nxt;

@@ -88,28 +88,14 @@ __device__ __forceinline__ uint32_t be16_at(uint32_t dw, int byte) {   // bytes 
     return (((dw >> (8 * byte)) & 0xFFu) << 8) | ((dw >> (8 * byte + 8)) & 0xFFu);
 }
 
-// Bytes of chunk c (span-relative: the packet occupies frame bytes [lead, ...)) that fall in the
-// packet-offset range [r0, r1), minus the 2-byte hole at packet offset h (h = ~0u: no hole).
-__device__ __forceinline__ u32x4 region_chunk(u32x4 v, uint32_t c, uint32_t lead, uint32_t r0, uint32_t r1,
-                                              uint32_t h) {
-    const int q = (int)(16u * c) - (int)lead;                  // packet offset of the chunk's byte 0
-    int lo = (int)r0 - q, hi = (int)r1 - q;
-    lo = lo < 0 ? 0 : (lo > 16 ? 16 : lo);
-    hi = hi < 0 ? 0 : (hi > 16 ? 16 : hi);
-    if (hi <= lo) {
-        return u32x4{0u, 0u, 0u, 0u};
-    }
-    if (lo != 0 || hi != 16) {
-        v = mask_chunk(v, lo, hi);
-    }
-    const int hh = (int)h - q;
-    if (h != ~0u && hh > -2 && hh < 16) {                       // punch the checksum-field hole
-        const int h0 = hh < 0 ? 0 : hh, h1 = hh + 2 > 16 ? 16 : hh + 2;
-        const u32x4 keep_lo = mask_chunk(v, 0, h0);
-        const u32x4 keep_hi = mask_chunk(v, h1, 16);
-        v = keep_lo | keep_hi;
-    }
-    return v;
+// What the little-endian word w at even packet offset h adds to this lane's unfolded v_sad_u16
+// accumulator (the lane whose k = 0 chunk holds the byte; byte at frame position f weighs 2^(8(f&1))).
+__device__ __forceinline__ uint32_t hole_share(uint32_t w, uint32_t lead, uint32_t h, int lane) {
+    const uint32_t f0 = lead + h, f1 = f0 + 1u;
+    uint32_t r = 0u;
+    r += ((uint32_t)lane == (f0 >> 4)) ? ((w & 0xFFu) << (8u * (f0 & 1u))) : 0u;
+    r += ((uint32_t)lane == (f1 >> 4)) ? ((w >> 8) << (8u * (f1 & 1u))) : 0u;
+    return r;
 }
 
 struct PktInfo {
@@ -119,6 +105,8 @@ struct PktInfo {
     uint32_t l4_csum_off;  // packet offset of the transport checksum field (~0u: none)
     uint32_t pseudo_le;    // little-endian word sum of the pseudo-header (0: none)
     uint32_t proto;
+    uint32_t hole_ip;      // TX: little-endian word of the IP checksum field (bytes 10, 11)
+    uint32_t hole_l4;      // TX: little-endian word of the transport checksum field
     bool     check_l4;
 };
 
@@ -136,6 +124,7 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
     const uint32_t tot = be16_at(d0, 2);
     const uint32_t frag = be16_at(d1, 2) & 0x3FFFu;              // MF | fragment offset
     p.proto = (d2 >> 8) & 0xFFu;
+    p.hole_ip = d2 >> 16;
     if (avail < 20u || ver != 4u || p.hlen < 20u || tot < p.hlen || tot > avail) {
         p.flags = F_MALFORMED;
         p.l4_end = 0u;
@@ -157,6 +146,9 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
         }
         p.check_l4 = true;
         p.l4_csum_off = p.hlen + 16u;
+        if (TX) {
+            p.hole_l4 = pkt_dword(v0, lead, p.hlen + 16u, gbase) & 0xFFFFu;
+        }
         p.pseudo_le = src_dst + (6u << 8) + (((l4len & 0xFFu) << 8) | (l4len >> 8));
         break;
     case 17u: {                                                  // UDP
@@ -181,6 +173,7 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
             return p;
         }
         p.check_l4 = true;
+        p.hole_l4 = du >> 16;
         p.pseudo_le = src_dst + (17u << 8) + (((udp_len & 0xFFu) << 8) | (udp_len >> 8));
         break;
     }
@@ -192,6 +185,9 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
         }
         p.check_l4 = true;
         p.l4_csum_off = p.hlen + 2u;
+        if (TX) {
+            p.hole_l4 = pkt_dword(v0, lead, p.hlen, gbase) >> 16;
+        }
         break;
     default:
         break;
@@ -207,22 +203,39 @@ __device__ __forceinline__ void store_csum(uintptr_t a, uint32_t off, uint32_t h
 }
 
 template <int G, int K, bool NT, bool TX>
-__device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, int lane,
-                                            int gbase) {
+__device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
+                                            int lane, int gbase) {
+    // One masked sum over [0, end) per chunk (end = transport end, or the IP header end when the
+    // transport part is not checked), plus the IP header alone from the k = 0 chunks (hlen <= 60 <
+    // 16*G - 15). Both are exact integer sums of the same frame half-words, so the transport part
+    // is their difference — exact, hence still zero iff all its bytes are zero (the reference's
+    // all-zero -> 0 / 0xFFFF distinction). TX checksum fields count as zero: their bytes are
+    // subtracted from the owning lane's sums.
     const uint32_t lead = st.lead;
     PktInfo p = pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
-    const uint32_t hole_ip = TX ? 10u : ~0u;
-    const uint32_t hole_l4 = TX ? p.l4_csum_off : ~0u;
-    const uint32_t l4_begin = p.check_l4 ? p.hlen : p.l4_end;     // empty transport region if unchecked
-    uint32_t acc_ip = 0u, acc_l4 = 0u;
-    const uint32_t nch = (p.l4_end + lead + 15u) >> 4;
+    const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
+    const uint32_t rend = lead + end;
+    const uint32_t nch = (rend + 15u) >> 4;
+    uint32_t acc = 0u;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
+        // Every loaded register is consumed on every path (chunks past the range are zeroed by a
+        // select, not skipped by a branch; the empty asm keeps the optimiser from sinking the use
+        // into one): a load left unconsumed on some path stays "pending" across the loop back-edge
+        // and the compiler drains vmcnt(0) before re-issuing the stage.
         const uint32_t c = (uint32_t)(k * G + lane);
+        const uint32_t keep = (c < nch) ? 0xFFFFFFFFu : 0u;
+        u32x4 v = st.v[k];
+        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));   // opaque: no branch can skip it
+        v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
         if (c < nch) {
-            acc_ip = sum4(region_chunk(st.v[k], c, lead, 0u, p.hlen, hole_ip), acc_ip);
-            acc_l4 = sum4(region_chunk(st.v[k], c, lead, l4_begin, p.l4_end, hole_l4), acc_l4);
+            v = edge_mask_rel(v, c, lead, rend);
         }
+        acc = sum4(v, acc);
+    }
+    uint32_t ip_raw = 0u;
+    if ((uint32_t)lane * 16u < lead + p.hlen) {
+        ip_raw = sum4(edge_mask_rel(st.v[0], (uint32_t)lane, lead, lead + p.hlen), 0u);
     }
     if (nch > (uint32_t)(G * K)) {                               // packets longer than one pass
         const uintptr_t q0 = st.a & ~(uintptr_t)15;
@@ -236,10 +249,21 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint32_t c = c0 + (uint32_t)(k * G + lane);
+                u32x4 v = w[k];                                  // zero chunk past the range
                 if (c < nch) {
-                    acc_l4 = sum4(region_chunk(w[k], c, lead, l4_begin, p.l4_end, hole_l4), acc_l4);
+                    v = edge_mask_rel(v, c, lead, rend);
                 }
+                acc = sum4(v, acc);
             }
+        }
+    }
+    uint32_t acc_ip = ip_raw, acc_l4 = acc - ip_raw;
+    if (TX) {
+        if (!(p.flags & F_MALFORMED)) {
+            acc_ip -= hole_share(p.hole_ip, lead, 10u, lane);
+        }
+        if (p.check_l4) {
+            acc_l4 -= hole_share(p.hole_l4, lead, p.l4_csum_off, lane);
         }
     }
     uint32_t sip = fold16(acc_ip), sl4 = fold16(acc_l4);
@@ -249,7 +273,7 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
     }
     sip = fold16(group_sum<G>(sip));
     sl4 = fold16(group_sum<G>(sl4) + p.pseudo_le);
-    if (lane != 0) {
+    if (lane != 0 || !valid) {                                   // a dummy stage stores nothing
         return;
     }
     uint32_t f = p.flags;
@@ -309,7 +333,9 @@ __global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
         step = gridDim.x * gpb;
         end = A.n;
     }
-    if (first >= end) {
+    const uint32_t cnt = group_iters(first, step, end);
+    const uint32_t iters = __builtin_amdgcn_readfirstlane(cnt);   // wave-uniform trip count
+    if (iters == 0u) {
         return;
     }
     const uintptr_t base = (uintptr_t)A.base;
@@ -318,24 +344,25 @@ __global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
     uint64_t off;
     uint32_t avail;
     uint32_t i = first;
+    bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
-    pkt_issue<G, K, NT>(S0, base + off, avail, lane);
-    for (;;) {
+    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+    for (uint32_t j = 0u;; j += 2u) {                            // scalar exits only (group_iters)
         uint32_t nx = i + step;
-        bool more = nx < end;
+        v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S1, more ? base + off : z, more ? avail : 0u, lane);
-        pkt_consume<G, K, NT, TX>(S0, A, i, lane, gbase);
-        if (!more) {
+        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
+        pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
+        if (j + 1u >= iters) {
             break;
         }
         i = nx;
         nx = i + step;
-        more = nx < end;
+        v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S0, more ? base + off : z, more ? avail : 0u, lane);
-        pkt_consume<G, K, NT, TX>(S1, A, i, lane, gbase);
-        if (!more) {
+        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+        pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
+        if (j + 2u >= iters) {
             break;
         }
         i = nx;
