@@ -48,6 +48,7 @@ def main():
                  "GiB_per_s_checksummed": round(nh * 20 / ms / 1e6 / 1.073741824, 1),
                  "GB_per_s_algorithmic": round(nh * 22 / ms / 1e6, 1), "parity_sample_ok": ok}
     del hdr, o3
+    torch.cuda.empty_cache()
     # ---- C4: 1 M packed UDP datagrams, 40..9000 B (seed 7), 12-B pseudo each
     rng = np.random.default_rng(7)
     nv = 1 << 20
@@ -75,6 +76,7 @@ def main():
                  "GB_per_s_algorithmic": round((tot + 14 * nv) / ms / 1e6, 1),
                  "descriptor_bytes_per_launch": 10 * nv, "kernel": netcsum.last_launch(), "parity_sample_ok": bool(np.array_equal(got, want))}
     del base, o4, bh
+    torch.cuda.empty_cache()
     # ---- fused Rx validation of 1 M x 1500-B IPv4/TCP datagrams vs the two-pass form
     n, L = 1 << 20, 1500
     pk = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
@@ -110,6 +112,7 @@ def main():
     ms_tx = events_ms(lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st), st)
     out["tx_finalize_1500B_tcp"] = {"ms": round(ms_tx, 4), "GiB_per_s": round(n * L / ms_tx / 1e6 / 1.073741824, 1)}
     del pk, v, tcp_ph, flags, o_ip, o_l4
+    torch.cuda.empty_cache()
     # ---- batched NET_BUF chains: 16 Ki reassembled 64 KiB UDP datagrams, 45 fragments each, every
     #      fragment's payload in its own 2 KiB buffer at ix 42 (Ethernet + IPv4 + 8 B), 12-B pseudo each
     nc, per, B = 1 << 14, 45, 2048
@@ -147,6 +150,7 @@ def main():
         "GB_per_s_algorithmic": round((payload + 10 * nc * per + 18 * nc) / ms / 1e6, 1),
         "parity_sample_ok": bool(np.array_equal(oc[:k].cpu().numpy().view(np.uint16), want))}
     del base, off_d, len_d, first_d, oc, hb
+    torch.cuda.empty_cache()
     # ---- host-memory (PCIe-inclusive) C2 rate: pinned NIC/socket buffers -> GPU -> pinned results
     n, L = 1 << 20, 1500
     seg_h = torch.empty(n * L, dtype=torch.uint8).pin_memory()

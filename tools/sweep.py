@@ -67,11 +67,14 @@ def main():
     variants = []
     for probe in (0, 1):
         variants.append(("read", dict(grid=8192, nt=1, probe=probe)))
-    variants.append(("c2", dict(kernel=2, group=16, k=6, nt=1, grid=16384)))
-    for group in (16, 32, 64):
-        for nt in (0, 1):
-            for grid, mult, tile in ((0, 1, 0), (0, 2, 0), (0, 4, 0), (16384, 0, 0), (0, 0, 2), (0, 0, 8)):
-                variants.append(("c2", dict(kernel=4, group=group, nt=nt, grid=grid, mult=mult, tile=tile)))
+    for group in (8, 16, 32):
+        for tile, grid in ((1, 0), (2, 0), (4, 0), (8, 0), (0, 8192), (0, 16384), (0, 32768)):
+            variants.append(("c2", dict(kernel=2, group=group, nt=1, grid=grid, tile=tile)))
+    for block in (128, 64):
+        variants.append(("c2", dict(kernel=2, group=16, nt=1, block=block, tile=4)))
+    variants.append(("c2", dict(kernel=2, group=16, nt=0, tile=4)))
+    variants.append(("c2", dict(kernel=3, group=16, nt=1, tile=4)))
+    variants.append(("c2", dict(kernel=4, group=16, nt=1, tile=4)))
     res = {}
     for r in range(args.rounds):
         for kind, kw in variants:
@@ -98,8 +101,8 @@ def main():
         hdr = torch.empty(nh * 20 + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(hdr, nh * 20, SEED, 0)
         o3 = torch.empty(nh, dtype=torch.int16, device=dev)
-        for kernel, group, k, nt in ((2, 1, 2, 0), (4, 1, 0, 0), (4, 1, 0, 1), (4, 4, 0, 1)):
-            for grid, tile in ((8192, 0), (0, 0), (16384, 0), (0, 2), (0, 8)):
+        for kernel, group, k, nt in ((2, 1, 2, 0), (2, 1, 2, 1), (2, 4, 0, 0), (4, 1, 0, 1)):
+            for grid, tile in ((8192, 0), (16384, 0), (65536, 0), (0, 1), (0, 2), (0, 4), (0, 8), (0, 16)):
                 set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=nt, tile=tile)
                 med, mn = timeit(lambda: netcsum.batch_strided(hdr, 20, 20, None, 0, 0, nh, o3, 2, stream=st), st)
                 b = nh * (20 + 2)
@@ -120,7 +123,7 @@ def main():
         len_d = torch.from_numpy(lens.view(np.int16)).to(dev)
         ph4 = torch.zeros(nv * 12, dtype=torch.uint8, device=dev)
         o4 = torch.empty(nv, dtype=torch.int16, device=dev)
-        for kernel, group, k in ((2, 32, 6), (3, 32, 4), (2, 64, 4), (3, 64, 4)):
+        for kernel, group, k in ((2, 32, 8), (2, 32, 6), (2, 64, 4), (2, 16, 8)):
             for grid, tile in ((16384, 0), (0, 1), (0, 2), (0, 4)):
                 set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=1, tile=tile)
                 med, mn = timeit(lambda: netcsum.batch_varlen(base, off_d, len_d, ph4, 12, 12, nv, o4, 0, stream=st), st)

@@ -315,9 +315,11 @@ __global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
     uintptr_t aB = z, paB = z;
     stage_issue<G, K, NT>(A, aA, vA ? dn.len : 0u, paA, vA ? plen : 0u, lane);
     dn = dnn;
-    // Wave-uniform trip count (group_iters): the only exits are scalar; a group past its own end
-    // runs dummy stages (zero-chunk loads) and stores nothing.
-    for (uint32_t j = 0u;; j += 2u) {
+    // Wave-uniform trip count (group_iters) and ONE exit, at the latch: a group past its own end
+    // runs dummy stages (zero-chunk loads) and stores nothing. (A mid-body `break`, even a
+    // uniform one, leaves the structurizer's never-taken edge from the first half back to the
+    // header, on which stage B is still pending — and the waitcnt pass drains vmcnt(0) for it.)
+    for (uint32_t j = 0u; j < iters; j += 2u) {
         // ---- consume A (iteration j) with B (j + 1) in flight
         uint32_t nxt = seg + step;
         vB = j + 1u < cnt;
@@ -329,9 +331,6 @@ __global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
         uint32_t r = stage_consume<G, K, NT>(A, aA, paA, ph_odd, lane);
         if (vA) {                                             // uniform within the group
             group_store<G>(P, seg, r, lane);
-        }
-        if (j + 1u >= iters) {
-            break;
         }
         seg = nxt;
         // ---- consume B (j + 1) with A (j + 2) in flight
@@ -345,9 +344,6 @@ __global__ void __launch_bounds__(256) seg_pipe_kernel(SegBatchArgs P) {
         r = stage_consume<G, K, NT>(B, aB, paB, ph_odd, lane);
         if (vB) {
             group_store<G>(P, seg, r, lane);
-        }
-        if (j + 2u >= iters) {
-            break;
         }
         seg = nxt;
     }

@@ -197,7 +197,9 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
 
 template <int G>
 __device__ __forceinline__ void store_csum(uintptr_t a, uint32_t off, uint32_t host_val) {
-    uint8_t* p = reinterpret_cast<uint8_t*>(a + off);          // memcpy of the host-order value
+    // global (not flat) stores: a flat store counts in lgkmcnt too and makes the waitcnt pass
+    // drain vmcnt(0) in the next stage's issue. memcpy of the host-order value.
+    __attribute__((address_space(1))) uint8_t* p = (__attribute__((address_space(1))) uint8_t*)(a + off);
     p[0] = (uint8_t)(host_val & 0xFFu);
     p[1] = (uint8_t)(host_val >> 8);
 }
@@ -347,24 +349,18 @@ __global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
     bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
     pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
-    for (uint32_t j = 0u;; j += 2u) {                            // scalar exits only (group_iters)
+    for (uint32_t j = 0u; j < iters; j += 2u) {                  // one scalar exit (see seg_pipe_kernel)
         uint32_t nx = i + step;
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
         pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
         pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
-        if (j + 1u >= iters) {
-            break;
-        }
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
         pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
         pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
-        if (j + 2u >= iters) {
-            break;
-        }
         i = nx;
     }
 }
