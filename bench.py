@@ -40,13 +40,13 @@ SEED = 0x5EED0001
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--segments", type=int, default=1 << 20, help="segments per GPU (C2: 1 M)")
     ap.add_argument("--seg-len", type=int, default=1500)
     ap.add_argument("--pseudo-len", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall seconds of the CPU sample")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of the CPU sample")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default: newest profiles/*pmc*.json)")
     ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block)")
     return ap.parse_args()
@@ -92,7 +92,7 @@ def host_c2_shard(oracle, start, n, L, plen):
 def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
     """Oracle (reference C path restatement, gcc -O2) on a bounded sample of the C2 workload."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    n = 1 << 16                                                   # 64 Ki segments = 99 MB sample
+    n = 1 << 18                                      # 256 Ki segments = 396 MB: larger than the host LLC
     seg, ph = host_c2_shard(oracle, 0, n, L, plen)
     oracle.batch_strided(seg, L, L, ph, plen, plen, n, 0, n_threads=threads)   # warm
     reps, t0 = 0, time.perf_counter()
@@ -105,7 +105,8 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
     gib = reps * n * (L + plen) / el / 2 ** 30
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{reps} passes x {n} segments x ({L}+{plen}) B (C2 shape, {n * (L + plen) / 1e6:.0f} MB), "
-                      f"oracle/net_util_oracle.c -O2 OpenMP static, {el:.2f} s wall"}
+                      f"oracle/net_util_oracle.c -O2 OpenMP static, {el:.2f} s wall x {threads} threads "
+                      f"= {el * threads:.0f} core-s"}
 
 
 def load_traffic(path, n_seg):
@@ -156,20 +157,28 @@ def main():
     torch.cuda.synchronize()
     kernel_desc = "netcsum::" + netcsum.last_launch()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # timed region: exactly K steps, barrier + synchronize on both sides, nothing else enqueued
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
+    for _ in range(args.steps):
         step()
-        evs[i][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    # roofline pass (untimed for `value`): HIP events on the launch stream around each of K launches
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kern = sorted(a.elapsed_time(b) for a, b in evs)
+    kern_ms = sum(kern) / len(kern)
+    kern_med_ms = kern[len(kern) // 2]
 
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -231,7 +240,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
                          "kernel": kernel_desc,
-                         "kernel_ms": round(kern_ms, 5),
+                         "kernel_ms": round(kern_ms, 5), "kernel_ms_median": round(kern_med_ms, 5),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "traffic_source": traffic_src,
                          "read_stream_probe_GBps": round(n16 / (rs_ms * 1e-3) / 1e9, 1),
