@@ -41,7 +41,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--segments", type=int, default=1 << 20, help="segments per GPU (C2: 1 M)")
     ap.add_argument("--seg-len", type=int, default=1500)
     ap.add_argument("--pseudo-len", type=int, default=12)

@@ -19,9 +19,17 @@ import oracle  # noqa: E402
 from bench import SEED, c2_pseudo_headers  # noqa: E402
 
 
-def events_ms(fn, st, reps=20, warm=3):
-    for _ in range(warm):
+def events_ms(fn, st, reps=20, warm=3, warm_s=0.1):
+    # warm by time, not count: the first few ms of launches after an idle gap run at lower clocks
+    # (profiles/r1_rx_order.jsonl: 0.316 ms cold vs 0.254 ms warm for the same fused-Rx launch)
+    t0 = time.perf_counter()
+    k = 0
+    while k < warm or time.perf_counter() - t0 < warm_s:
         fn()
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
         a.record(st)

@@ -10,6 +10,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "uc-tcp-ip_amd"))
@@ -22,9 +23,15 @@ import netcsum  # noqa: E402
 from bench import SEED, c2_pseudo_headers  # noqa: E402
 
 
-def timeit(fn, stream, reps=20, warm=3):
-    for _ in range(warm):
+def timeit(fn, stream, reps=20, warm=3, warm_s=0.1):
+    t0 = time.perf_counter()                     # warm by time (clock ramp after idle gaps)
+    k = 0
+    while k < warm or time.perf_counter() - t0 < warm_s:
         fn()
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
         a.record(stream)
