@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--c3", action="store_true")
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--no-c2", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
@@ -83,6 +84,8 @@ def main():
     variants.append(("c2", dict(kernel=3, group=16, nt=1, tile=4)))
     variants.append(("c2", dict(kernel=4, group=16, nt=1, tile=4)))
     res = {}
+    if args.no_c2:
+        variants = []
     for r in range(args.rounds):
         for kind, kw in variants:
             set_tune(**kw)
@@ -108,8 +111,14 @@ def main():
         hdr = torch.empty(nh * 20 + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(hdr, nh * 20, SEED, 0)
         o3 = torch.empty(nh, dtype=torch.int16, device=dev)
-        for kernel, group, k, nt in ((2, 1, 2, 0), (2, 1, 2, 1), (2, 4, 0, 0), (4, 1, 0, 1)):
-            for grid, tile in ((8192, 0), (16384, 0), (65536, 0), (0, 1), (0, 2), (0, 4), (0, 8), (0, 16)):
+        for probe in (0, 1):
+            set_tune(grid=8192, nt=1, probe=probe)
+            nb = nh * 20 // 16 * 16
+            med, mn = timeit(lambda: netcsum.read_stream(hdr, nb, sink, stream=st), st)
+            print(json.dumps({"variant": ["c3-read", dict(probe=probe)], "ms_med": round(med, 4),
+                              "GBps_med": round(nb / med / 1e6, 1)}), flush=True)
+        for kernel, group, k, nt in ((2, 1, 2, 0), (5, 0, 0, 0)):
+            for grid, tile in ((8192, 0), (16384, 0), (0, 1), (0, 2), (0, 4), (0, 8), (0, 16)):
                 set_tune(grid=grid, group=group, kernel=kernel, k=k, nt=nt, tile=tile)
                 med, mn = timeit(lambda: netcsum.batch_strided(hdr, 20, 20, None, 0, 0, nh, o3, 2, stream=st), st)
                 b = nh * (20 + 2)

@@ -25,7 +25,7 @@ std::atomic<int> g_tune_grid{0};
 std::atomic<int> g_tune_group{0};
 std::atomic<int> g_tune_nt{-1};                   // -1: auto (nt when groups share no chunks)
 std::atomic<int> g_tune_block{256};
-std::atomic<int> g_tune_kernel{2};
+std::atomic<int> g_tune_kernel{0};                 // 0 = auto (5 when small_supported, else 2)
 std::atomic<int> g_tune_chunks{0};
 std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
@@ -140,6 +140,20 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
     c.tile = tile >= 0 ? tile : (c.grid > 0 ? 0 : 4);
     const int nt = g_tune_nt.load();
 
+    if (c.kernel == 0) {
+        c.kernel = netcsum::small_supported(a) ? 5 : 2;
+    }
+    if (c.kernel == 5) {
+        if (netcsum::small_supported(a)) {
+            c.group_lanes = 1;
+            c.chunks_per_pass = (int)((a.seg_len + 3u) >> 2);   // dwords per segment
+            c.tile = tile >= 0 ? tile : (c.grid > 0 ? 0 : 1);   // one pass: r1u sweep (C3)
+            c.nt = false;
+            c.blocks_needed = 0;
+            return c;
+        }
+        c.kernel = 2;                                  // not small / aligned: general form
+    }
     if (c.kernel == 4) {
         int g = 0, p = 0, k = 0;
         if (choose_tile(a, g_tune_group.load(), g_tune_chunks.load(), &g, &p, &k)) {
@@ -537,8 +551,8 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_nt.store(value < 0 ? -1 : (value != 0));
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
-        if (value < 0 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
-        g_tune_kernel.store(value == 0 ? 2 : value);
+        if (value < 0 || value > 5) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_kernel.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CHUNKS:
         if (!(value == 0 || value == 1 || value == 2 || value == 3 || value == 4 || value == 6 || value == 8)) {

@@ -31,7 +31,8 @@ struct LaunchCfg {
     int  chunks_per_pass;  // 16-B chunks per lane per pass: 1..4
     bool nt;               // non-temporal segment loads
     int  kernel;           // 1: seg_batch_kernel (one segment in flight per group), 2: seg_pipe_kernel,
-                           // 3: seg_lds_kernel, 4: seg_tile_kernel (strided only)
+                           // 3: seg_lds_kernel, 4: seg_tile_kernel (strided only),
+                           // 5: seg_small_kernel (small 4-B-aligned strided segments, no pseudo)
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
 };
@@ -69,6 +70,8 @@ bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instan
 const char* last_launch();                  // description of this thread's last batch launch
 
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
+bool small_supported(const SegBatchArgs& a);  // strided, no pseudo, 1..64 B, base/stride 4-B aligned
+hipError_t launch_small_batch(const SegBatchArgs& a, int grid, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s);
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,

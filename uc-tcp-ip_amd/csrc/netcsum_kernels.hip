@@ -817,14 +817,29 @@ static int pick_grid(Kern kern, const LaunchCfg& c) {
         return (int)((nseg + per - 1u) / per);
     }
     if (c.grid > 0) return c.grid;
-    static int occ_cache[3] = {0, 0, 0};                 // block 64 / 128 / 256
-    const int slot = c.block == 64 ? 0 : (c.block == 128 ? 1 : 2);
-    int occ = occ_cache[slot];
+    // residency per (kernel instantiation, block size), queried once
+    struct OccEntry {
+        const void* fn;
+        int block;
+        int occ;
+    };
+    static thread_local OccEntry cache[64];
+    static thread_local int n_cache = 0;
+    const void* fn = reinterpret_cast<const void*>(kern);
+    int occ = 0;
+    for (int i = 0; i < n_cache; ++i) {
+        if (cache[i].fn == fn && cache[i].block == c.block) {
+            occ = cache[i].occ;
+            break;
+        }
+    }
     if (occ <= 0) {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, c.block, 0) != hipSuccess || occ <= 0) {
             occ = 1;
         }
-        occ_cache[slot] = occ;
+        if (n_cache < 64) {
+            cache[n_cache++] = OccEntry{fn, c.block, occ};
+        }
     }
     uint64_t g = (uint64_t)occ * (uint64_t)c.cus * (uint64_t)(c.grid_mult > 0 ? c.grid_mult : 1);
     if (g > c.blocks_needed) g = c.blocks_needed;
@@ -976,8 +991,9 @@ const char* last_launch() {
 }
 
 static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
-    static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel"};
-    const int kid = (c.kernel >= 1 && c.kernel <= 4) ? c.kernel : 0;
+    static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel",
+                                  "seg_small_kernel"};
+    const int kid = (c.kernel >= 1 && c.kernel <= 5) ? c.kernel : 0;
     snprintf(g_last_launch, sizeof(g_last_launch), "%s<G=%d,K=%d%s%s%s> block=%d tile=%d grid=%d P=%d",
              names[kid], c.group_lanes, c.chunks_per_pass, a.seg_off ? ",varlen" : ",strided",
              c.nt ? ",nt" : "", "", c.block, c.tile, c.grid, c.tile_pieces);
@@ -987,6 +1003,9 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
     note_launch(c, args);
     SegBatchArgs a = args;
     a.tile = c.tile > 0 ? (uint32_t)c.tile : 0u;
+    if (c.kernel == 5) {
+        return launch_small_batch(a, c.grid, s);              // K = dwords per segment
+    }
     if (c.kernel == 4) {
         return launch_tile_dispatch(a, c, s);
     }
