@@ -9,8 +9,8 @@ bytes per rank) with no collective on the data path; the only communication is t
 the max-over-ranks of the timed region.
 
 value     = Σ_ranks n_seg*(1500+12) bytes * steps / max_rank(wall time of the K timed steps) / 2^30
-roofline  = dominant kernel (seg_batch_kernel<32,3,strided>) algorithmic bytes per launch
-            n_seg*(1500+12+2) / mean HIP-event duration of that launch on its own stream, vs the
+roofline  = dominant kernel (the form the library picks for C2: seg_stream_kernel) algorithmic bytes
+            per launch n_seg*(1500+12+2) / mean HIP-event duration of that launch on its stream, vs the
             8.0 TB/s HBM3E spec peak; `traffic` = HBM bytes per launch from rocprofv3 PMC
             (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) or null.
 cpu_baseline = the oracle's restatement of the reference C path (gcc -O2, same per-segment
@@ -109,14 +109,17 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
                       f"= {el * threads:.0f} core-s"}
 
 
-def load_traffic(path, n_seg):
-    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+def load_traffic(path, n_seg, kernel_fn):
+    """HBM bytes per launch of THIS kernel form at this size, from the newest matching PMC summary."""
+    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")),
+                                       key=os.path.getmtime)
     for p in reversed(cands):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("n_seg") == n_seg and "hbm_bytes_per_launch" in d:
+        if (d.get("n_seg") == n_seg and "hbm_bytes_per_launch" in d
+                and kernel_fn in d.get("dominant_kernel", "")):
             return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, REPO)
     return None, None
 
@@ -138,7 +141,8 @@ def main():
     torch.cuda.set_device(dev)
 
     keymap = {"grid": netcsum.TUNE_GRID_BLOCKS, "group": netcsum.TUNE_GROUP_LANES,
-              "nt": netcsum.TUNE_NT_LOADS, "block": netcsum.TUNE_BLOCK_THREADS}
+              "nt": netcsum.TUNE_NT_LOADS, "block": netcsum.TUNE_BLOCK_THREADS, "kernel": netcsum.TUNE_KERNEL,
+              "chunks": netcsum.TUNE_CHUNKS, "tile": netcsum.TUNE_TILE, "mult": netcsum.TUNE_GRID_MULT}
     for kv in args.tune:
         k, v = kv.split("=")
         netcsum.tune(keymap[k], int(v))
@@ -213,16 +217,24 @@ def main():
     torch.cuda.synchronize()
     rs_ms = sum(a.elapsed_time(b) for a, b in rs) / len(rs)
 
+    parity_all = parity_ok
+    if world > 1:                                  # every rank's sample must match its oracle
+        t = torch.tensor([1 if parity_ok is True else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        parity_all = bool(t.item()) if not isinstance(parity_ok, str) else parity_ok
+
     if rank == 0:
         total_bytes = world * n * (L + plen) * args.steps
         value = total_bytes / wall / 2 ** 30
         algo_bytes = n * (L + plen + 2)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.traffic_json, n)
+        kernel_fn = kernel_desc.split("::")[-1].split("<")[0]
+        traffic, traffic_src = load_traffic(args.traffic_json, n, kernel_fn)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
+            "value_per_gpu": round(value / world, 2),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -245,7 +257,7 @@ def main():
                          "traffic_source": traffic_src,
                          "read_stream_probe_GBps": round(n16 / (rs_ms * 1e-3) / 1e9, 1),
                          "frac_of_read_stream_probe": round(achieved / (n16 / (rs_ms * 1e-3) / 1e9), 4)},
-            "parity_sample_ok": parity_ok,
+            "parity_sample_ok": parity_all,
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -66,11 +66,12 @@ LENGTHS = [0, 1, 2, 3, 4, 5, 7, 15, 16, 17, 19, 20, 21, 31, 33, 40, 63, 64, 65, 
            1023, 1499, 1500, 1501, 4520, 8999, 9000, 16385, 65535]
 
 
-@pytest.mark.parametrize("kernel", [0, 2, 4])
+@pytest.mark.parametrize("kernel", [0, 2, 4, 6])
 @pytest.mark.parametrize("L", LENGTHS)
 def test_strided_matrix_vs_oracle(L, kernel):
     """Every length class x stride x base misalignment x pseudo-header shape x op, per kernel form
-    (0 = library default; 4 = wave-tile LDS image where it fits, else its fallback)."""
+    (0 = library default; 4 = wave-tile LDS image where it fits, 6 = segmented stream where it
+    fits, else their fallback)."""
     netcsum.tune(netcsum.TUNE_KERNEL, kernel)
     rng = np.random.default_rng(L + 11)
     n = 37 if L < 20000 else 5
@@ -345,3 +346,69 @@ def test_small_aligned_kernel_vs_oracle(L):
     got = _gpu_strided(data_d, 1, 64, L, None, 0, 0, 300, 0)
     assert np.array_equal(got, oracle.batch_strided(data, 64, L, None, 0, 0, 300, 0, seg_offset=1))
     assert netcsum.last_launch().startswith("seg_pipe_kernel")
+
+
+STREAM_LENGTHS = [256, 257, 300, 1023, 1024, 1025, 1499, 1500, 1501, 2048, 4520, 9000, 65535]
+
+
+@pytest.mark.parametrize("L", STREAM_LENGTHS)
+def test_stream_kernel_runs_vs_oracle(L):
+    """seg_stream_kernel (kernel 6): a wave walks a contiguous RUN of segments (forced small grids
+    make runs of 1..hundreds of segments), so segment boundaries fall at every piece / chunk / byte
+    position, next to pseudo-headers of every shape and alignment, with gaps of 0..64 B."""
+    rng = np.random.default_rng(L * 7 + 1)
+    n = 300 if L <= 9000 else 9
+    for pattern in ("random", "zero", "ff", "carry"):
+        for stride in (L, L + 1, L + 3, L + 13, L + 64):
+            data = _host_bytes(rng, n * stride + L + 64, pattern)
+            data_d = torch.from_numpy(data).to(DEV)
+            for base_off in ((0, 1, 2, 3, 5, 127) if pattern == "random" else (0, 1)):
+                for plen, pstride in ((0, 0), (12, 12), (11, 13), (40, 41), (1, 1), (64, 64), (12, 0)):
+                    ph = _host_bytes(rng, n * max(pstride, 1) + 128, pattern)
+                    ph_d = torch.from_numpy(ph).to(DEV)
+                    pofs = int(rng.integers(0, 5)) if plen else 0
+                    for grid, chunks, run in ((1, 4, -1), (2, 6, -1), (3, 8, -1), (0, 0, -1), (0, 4, 1), (0, 6, 7),
+                                              (0, 8, 128)):
+                        netcsum.tune(netcsum.TUNE_KERNEL, 6)
+                        netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+                        netcsum.tune(netcsum.TUNE_CHUNKS, chunks)
+                        netcsum.tune(netcsum.TUNE_TILE, run)
+                        for op in (0, 1) if plen else (0, 1, 2, 3):
+                            got = _gpu_strided(data_d, base_off, stride, L, ph_d.data_ptr() + pofs if plen else None,
+                                               pstride, plen, n, op)
+                            assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
+                            want = oracle.batch_strided(data, stride, L, ph[pofs:] if plen else None, pstride, plen,
+                                                        n, op, seg_offset=base_off)
+                            assert np.array_equal(got, want), (L, pattern, stride, base_off, plen, pstride, grid, chunks, run, op)
+    # outside its domain kernel 6 falls back to the general form
+    netcsum.tune(netcsum.TUNE_KERNEL, 6)
+    netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
+    netcsum.tune(netcsum.TUNE_TILE, -1)
+    data = _host_bytes(rng, 40 * 200, "random")
+    got = _gpu_strided(torch.from_numpy(data).to(DEV), 0, 200, 100, None, 0, 0, 40, 0)
+    assert np.array_equal(got, oracle.batch_strided(data, 200, 100, None, 0, 0, 40, 0))
+    assert netcsum.last_launch().startswith("seg_pipe_kernel")
+
+
+def test_stream_kernel_full_c2_equals_pipe_kernel():
+    """C2 at full size: the stream kernel's 1 M checksums equal the pipelined kernel's, and every
+    segment verifies after write-back (size-independent round trip)."""
+    n = 1 << 20
+    seg, ph, L = _c2_batch(n)
+    outs = []
+    for kernel in (2, 0):                      # 0: the library default for C2 is the stream kernel
+        netcsum.tune(netcsum.TUNE_KERNEL, kernel)
+        o = _out(n, 0)
+        netcsum.batch_strided(seg, L, L, ph, 12, 12, n, o, 0)
+        torch.cuda.synchronize()
+        outs.append(o)
+    assert netcsum.last_launch().startswith("seg_stream_kernel")
+    assert torch.equal(outs[0], outs[1])
+    s2 = seg.view(n, L)
+    s2[:, 16:18] = 0
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, outs[1], 0)
+    s2[:, 16:18] = outs[1].view(torch.uint8).view(n, 2)
+    ok = _out(n, 1)
+    netcsum.batch_strided(seg, L, L, ph, 12, 12, n, ok, 1)
+    torch.cuda.synchronize()
+    assert bool(ok.all())

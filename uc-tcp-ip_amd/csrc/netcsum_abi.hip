@@ -141,7 +141,34 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
     const int nt = g_tune_nt.load();
 
     if (c.kernel == 0) {
-        c.kernel = netcsum::small_supported(a) ? 5 : 2;
+        c.kernel = netcsum::small_supported(a) ? 5 : (netcsum::stream_dense(a) ? 6 : 2);
+    }
+    if (c.kernel == 6) {
+        if (netcsum::stream_supported(a)) {
+            int d = g_tune_chunks.load();
+            if (!(d == 4 || d == 6 || d == 8)) d = 4;
+            c.chunks_per_pass = d;
+            c.nt = nt != 0;                                // default non-temporal: the run is read once
+            // Run length (segments per wave): TILE > 0 sets it; GRID_BLOCKS > 0 forces 4 x grid runs;
+            // GRID_MULT > 1 sizes runs for that many rounds of resident waves; default 16 segments
+            // (r1w5 sweep, C2: runs of 16 read 6.8 TB/s, single-round runs of 128 6.6 TB/s — short
+            // runs keep the waves in flight on nearby bytes).
+            uint64_t waves;
+            if (tile > 0) {
+                waves = ((uint64_t)a.n_seg + (uint64_t)tile - 1u) / (uint64_t)tile;
+            } else if (c.grid > 0) {
+                waves = 4ull * (uint64_t)c.grid;
+            } else if (c.grid_mult > 1) {
+                waves = (uint64_t)netcsum::stream_occupancy(d, a, c.nt) * 4u * (uint64_t)c.cus * (uint64_t)c.grid_mult;
+            } else {
+                waves = ((uint64_t)a.n_seg + 15u) / 16u;
+            }
+            c.stream_spw = netcsum::stream_spw(a, waves);
+            c.group_lanes = 64;
+            c.blocks_needed = 0;
+            return c;
+        }
+        c.kernel = 2;                                  // varlen, sparse or short segments: general form
     }
     if (c.kernel == 5) {
         if (netcsum::small_supported(a)) {
@@ -551,7 +578,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_nt.store(value < 0 ? -1 : (value != 0));
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
-        if (value < 0 || value > 5) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 6) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_kernel.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CHUNKS:

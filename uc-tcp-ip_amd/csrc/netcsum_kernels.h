@@ -32,9 +32,11 @@ struct LaunchCfg {
     bool nt;               // non-temporal segment loads
     int  kernel;           // 1: seg_batch_kernel (one segment in flight per group), 2: seg_pipe_kernel,
                            // 3: seg_lds_kernel, 4: seg_tile_kernel (strided only),
-                           // 5: seg_small_kernel (small 4-B-aligned strided segments, no pseudo)
+                           // 5: seg_small_kernel (small 4-B-aligned strided segments, no pseudo),
+                           // 6: seg_stream_kernel (dense strided runs, one wave per run)
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
+    uint32_t stream_spw;   // kernel 6: segments per wave (one contiguous run each)
 };
 
 struct PktBatchArgs {
@@ -72,6 +74,11 @@ const char* last_launch();                  // description of this thread's last
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
 bool small_supported(const SegBatchArgs& a);  // strided, no pseudo, 1..64 B, base/stride 4-B aligned
 hipError_t launch_small_batch(const SegBatchArgs& a, int grid, hipStream_t s);
+bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256
+bool stream_dense(const SegBatchArgs& a);      // strided, stride == len >= 1024: the default for kernel 6
+uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves);
+int stream_occupancy(int depth, const SegBatchArgs& a, bool nt);   // resident 256-thread blocks per CU
+hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s);
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,

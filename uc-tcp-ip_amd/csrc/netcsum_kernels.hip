@@ -992,8 +992,13 @@ const char* last_launch() {
 
 static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel",
-                                  "seg_small_kernel"};
-    const int kid = (c.kernel >= 1 && c.kernel <= 5) ? c.kernel : 0;
+                                  "seg_small_kernel", "seg_stream_kernel"};
+    const int kid = (c.kernel >= 1 && c.kernel <= 6) ? c.kernel : 0;
+    if (kid == 6) {
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_stream_kernel<D=%d%s%s> block=256 segs_per_wave=%u",
+                 c.chunks_per_pass, (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "", c.stream_spw);
+        return;
+    }
     snprintf(g_last_launch, sizeof(g_last_launch), "%s<G=%d,K=%d%s%s%s> block=%d tile=%d grid=%d P=%d",
              names[kid], c.group_lanes, c.chunks_per_pass, a.seg_off ? ",varlen" : ",strided",
              c.nt ? ",nt" : "", "", c.block, c.tile, c.grid, c.tile_pieces);
@@ -1005,6 +1010,9 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
     a.tile = c.tile > 0 ? (uint32_t)c.tile : 0u;
     if (c.kernel == 5) {
         return launch_small_batch(a, c.grid, s);              // K = dwords per segment
+    }
+    if (c.kernel == 6) {
+        return launch_stream_batch(a, c.chunks_per_pass, c.stream_spw, c.nt, s);   // K = pieces in flight
     }
     if (c.kernel == 4) {
         return launch_tile_dispatch(a, c, s);

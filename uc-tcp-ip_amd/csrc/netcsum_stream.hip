@@ -1,0 +1,370 @@
+// netcsum_stream.hip — gfx950 "segmented stream" kernel for dense strided segment batches
+// (configs C2 / C5: 1500 B TCP segments + 12 B IPv4 pseudo-headers, one
+// NetUtil_16BitOnesCplChkSumDataCalc / ...DataVerify per segment, net_util.c:344-363, :428-449;
+// the sum itself is NetUtil_16BitSumDataCalc, net_util.c:1321-1475, plus the pseudo-header partial
+// of NetUtil_16BitOnesCplSumDataCalc, net_util.c:1591-1609).
+//
+// Why a third form. The lane-group kernels (netcsum_kernels.hip) give every segment its own G
+// lanes, so a wave-instruction reads G-lane pieces at 16-B alignment and the 16-B chunks that
+// straddle two segments are fetched twice. Here a WAVE owns a contiguous run of segments and reads
+// their bytes exactly like a pure read stream: piece q of the wave is the 1 KiB at O + 1024*q
+// (O = 128-B line below the first segment), lane l holds its 16 B at O + 1024*q + 16*l — every
+// wave-instruction is 8 whole, aligned cache lines and every byte of the run is fetched once.
+// Segment boundaries are wave-uniform scalar events: while consuming piece q the wave walks (on
+// the SALU) the segments that END inside it; for each, every lane adds the bytes of that segment
+// in its chunk to its running partial, the 64 partials are reduced with four DPP row shifts and
+// four v_readlane, and lane 0 writes the folded result to a per-wave LDS result array, flushed to
+// HBM with coalesced stores when the run is done.
+//
+// Pseudo-headers (12 B for IPv4 TCP/UDP, net_tcp.h:1545-1551) ride in the same pipeline: when
+// piece q is issued, the scalar issue cursor finds the segments that end in piece q and their
+// pseudo-headers (contiguous in the pseudo array) are fetched as 16-B chunks by the first lanes,
+// so they are in registers when the events of piece q are consumed.
+//
+// Loads are raw buffer loads (V# over the wave's byte run, voffset = 1024*q + 16*lane): the
+// hardware range check returns zeros past the run, so the pipeline's dummy pieces and unused pseudo
+// lanes need no zero-chunk address select. D pieces are in flight per wave (register ring,
+// counted vmcnt, `opaque` keeps every stage's wait in straight-line code — netcsum_device.h).
+//
+// Arithmetic (bit-exact; see netcsum_kernels.hip): absolute 16-B frame, v_sad_u16 little-endian
+// half-word sums, per-lane exact partials (< 2^26 for a 64 KiB segment), per-lane fold16 + the
+// segment's parity rotation, DPP sum of 64 folded values (< 2^23), fold16, complement.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "netcsum_device.h"
+#include "netcsum_kernels.h"
+
+namespace netcsum {
+
+namespace {
+
+constexpr int kRsrcWord3 = 0x00020000;     // gfx9-family raw buffer V# word 3 (32-bit data format)
+constexpr uint32_t kOOB = 0x80000000u;     // voffset past every run's num_records: reads zeros
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t run_rsrc(uintptr_t base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, NT ? 2 : 0);
+}
+
+// `opaque` over the whole 128-bit register tuple (one "+v" operand): the value stays in the tuple the
+// load wrote, so the refill of the same ring slot needs no copy (a copy would force a vmcnt wait).
+__device__ __forceinline__ u32x4 opaque_tuple(u32x4 v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// Sum of bytes [0, m) of this lane's chunk, m per lane in [0, 16] (VALU only: no scalar mask work).
+__device__ __forceinline__ uint32_t low_bytes(u32x4 v, int m) {
+    uint32_t acc = 0u;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = min(max(m - 4 * i, 0), 4);
+        const uint32_t mask = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+        acc = __builtin_amdgcn_sad_u16(d[i] & mask, 0u, acc);
+    }
+    return acc;
+}
+
+// This lane's share of the bytes of a 1-KiB piece that lie below piece offset x (wave-uniform,
+// 0..1024): its whole chunk if the chunk ends at or below x, the low (x - 16*lane) bytes if x falls
+// inside it, nothing above. A span [xs, xe) of the piece is prefix(xe) - prefix(xs), exactly.
+__device__ __forceinline__ uint32_t piece_prefix(u32x4 v, uint32_t lane16, uint32_t x) {
+    return low_bytes(v, min(max((int)x - (int)lane16, 0), 16));
+}
+
+// Sum over the 64 lanes (every lane active): inclusive row scans by DPP row_shr 1/2/4/8 (lanes with
+// no source add the 0 `old` operand), then the four row totals from lanes 15/31/47/63 (scalar).
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) + (uint32_t)__builtin_amdgcn_readlane((int)v, 31) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+constexpr uint32_t kMaxRun = 128u;     // segments per wave run: results live in two VGPRs (lane = k % 64)
+
+// One wave = segments [s_begin, s_end) of a strided batch (stride >= len >= 1, run <= 128 segments).
+// ONE: stride == len >= 1024, so at most one segment ends inside any 1-KiB piece and the next one
+// starts at that same byte — the per-piece work is one uniform branch, and an event is one prefix
+// mask, one DPP reduction and a scalar epilogue. Otherwise the general walk (any number of events
+// per piece, gaps between segments).
+// PH: 0 no pseudo-header, 1 pseudo-headers touching <= 2 aligned chunks (<= 17 B), 2 up to 64 B.
+template <int D, int PH, bool NT, bool ONE>
+__global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_t spw) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    if (sb64 >= A.n_seg) {
+        return;
+    }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(A.n_seg - s_begin, spw);
+    const uint32_t s_end = s_begin + nres;
+
+    const uint32_t L = A.seg_len;
+    const uint32_t st = (uint32_t)A.seg_stride;
+    const uintptr_t a_first = (uintptr_t)A.base + (uint64_t)s_begin * A.seg_stride;
+    const uintptr_t O = a_first & ~(uintptr_t)127;
+    const uint32_t span = (uint32_t)(a_first - O) + (nres - 1u) * st + L;
+    const uint32_t npieces = (span + 1023u) >> 10;
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
+    const uint32_t lane16 = 16u * lane;
+    const bool ph_odd = PH != 0 && (A.pseudo_len & 1u) != 0u;
+
+    u32x4 dv[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {                              // first D pieces in flight ...
+        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+    }
+
+    // ... while the run's pseudo-header sums are computed: lane k % 64 of slot k / 64 holds segment
+    // k's pseudo-header sum (folded, in its own stream frame) from its 16-B-aligned chunks.
+    uint32_t ps0 = 0u, ps1 = 0u;
+    if constexpr (PH != 0) {
+        const uint32_t plen = A.pseudo_len;
+        const uint32_t pst = A.pseudo_stride;
+        const uintptr_t pfirst = (uintptr_t)A.pseudo + (uint64_t)s_begin * pst;
+        const uintptr_t PB = pfirst & ~(uintptr_t)15;
+        const uint32_t plead = (uint32_t)(pfirst - PB);
+        const uint32_t pspan = plead + (nres - 1u) * pst + plen;
+        const __amdgpu_buffer_rsrc_t rp = run_rsrc(PB, (pspan + 15u) & ~15u);
+        const uint32_t nchmax = (plen + 30u) >> 4;             // chunks one pseudo-header can touch (<= 5)
+        constexpr int kPch = PH == 1 ? 2 : 5;
+        u32x4 pv[2][kPch];                                     // all loads issued before any is used
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            const uint32_t k = lane + 64u * (uint32_t)sl;
+            const uint32_t a = plead + k * pst;
+            const uint32_t hi = (a & 15u) + plen;
+#pragma unroll
+            for (int i = 0; i < kPch; ++i) {
+                if ((uint32_t)i < nchmax) {                    // wave-uniform
+                    const uint32_t off = (k < nres && 16u * (uint32_t)i < hi) ? (a & ~15u) + 16u * (uint32_t)i : kOOB;
+                    pv[sl][i] = buf_load16<false>(rp, off);
+                } else {
+                    pv[sl][i] = u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            const uint32_t k = lane + 64u * (uint32_t)sl;
+            const uint32_t a = plead + k * pst;
+            const int lo = (int)(a & 15u);
+            const int hi = lo + (int)plen;
+            uint32_t acc = 0u;
+#pragma unroll
+            for (int i = 0; i < kPch; ++i) {
+                const int b = 16 * i;
+                acc += low_bytes(pv[sl][i], min(max(hi - b, 0), 16)) - low_bytes(pv[sl][i], min(max(lo - b, 0), 16));
+            }
+            uint32_t s = fold16(acc);
+            if (a & 1u) {
+                s = rot8(s);
+            }
+            if (sl == 0) {
+                ps0 = s;
+            } else {
+                ps1 = s;
+            }
+        }
+    }
+
+    uint32_t res0 = 0u, res1 = 0u;                             // result of run segment k: lane k % 64
+    // Scalar epilogue of segment `cur` from the wave total T of its bytes (absolute LE frame).
+    auto finish = [&](uint32_t cur, uint32_t T, bool odd) {
+        uint32_t t = fold16(T);
+        if (odd) {
+            t = rot8(t);
+        }
+        const uint32_t k = cur - s_begin;
+        if constexpr (PH != 0) {
+            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)ps0, (int)(k & 63u));
+            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)ps1, (int)(k & 63u));
+            const uint32_t p = k < 64u ? p0 : p1;
+            t = fold16(t + p);
+        }
+        const uint32_t val = A.verify ? (t == 0xFFFFu ? 1u : 0u) : (~t & 0xFFFFu);
+        res0 = (lane == k) ? val : res0;
+        res1 = (lane + 64u == k) ? val : res1;
+    };
+
+    uint32_t cur = s_begin;                                    // next segment to finish
+    uint32_t cs = (uint32_t)(a_first - O);                     // its start / end, run-relative
+    uint32_t ce = cs + L;
+    uint32_t acc = 0u;                                         // this lane's share so far (mod 2^32)
+    if constexpr (ONE) {
+        acc = 0u - piece_prefix(opaque_tuple(dv[0]), lane16, cs);    // bytes of piece 0 before the run
+    }
+
+    // State lives in locals inside consume and is written back unconditionally at the end: a branch
+    // that updates `ce` on one side and `acc` on the other must not be merged by the optimiser into
+    // one store through a phi of two addresses (that pins the state in scratch memory).
+    auto consume = [&](uint32_t q, u32x4 v) {
+        const uint32_t qb = q << 10;
+        const uint32_t pend = qb + 1024u;
+        const uint32_t full = sum4(v, 0u);
+        uint32_t u = cur, c = cs, e = ce, a = acc;
+        if constexpr (ONE) {
+            if (u < s_end && e <= pend) {                      // segment `u` ends in this piece
+                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                finish(u, wave_total(a + Pe), (((e - L) & 1u) != 0u) != ph_odd);
+                a = full - Pe;                                 // the next segment starts at e
+                ++u;
+                e += st;
+            } else {
+                a += full;
+            }
+        } else {
+            if (!(u < s_end && e <= pend)) {                   // no segment ends in this piece
+                if (u < s_end) {
+                    a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+                }
+            } else {
+                uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+#pragma clang loop vectorize(disable) unroll(disable)
+                do {
+                    const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                    finish(u, wave_total(a + (Pe - Ps)), ((c & 1u) != 0u) != ph_odd);
+                    a = 0u;
+                    ++u;
+                    c += st;
+                    e += st;
+                    Ps = (st == L) ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+                } while (u < s_end && e <= pend);
+                if (u < s_end) {
+                    a = full - Ps;
+                }
+            }
+        }
+        cur = u;
+        cs = c;
+        ce = e;
+        acc = a;
+    };
+
+    const uint32_t rounds = (npieces + (uint32_t)D - 1u) / (uint32_t)D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const uint32_t q = r * (uint32_t)D + (uint32_t)j;
+            consume(q, opaque_tuple(dv[j]));
+            dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
+            asm volatile("" ::: "memory");                     // keep the refill here, not sunk to the latch
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
+
+    if (A.verify) {
+        uint8_t* o = static_cast<uint8_t*>(A.out) + s_begin;
+        if (lane < nres) o[lane] = (uint8_t)res0;
+        if (lane + 64u < nres) o[lane + 64u] = (uint8_t)res1;
+    } else {
+        uint16_t* o = static_cast<uint16_t*>(A.out) + s_begin;
+        if (lane < nres) o[lane] = (uint16_t)res0;
+        if (lane + 64u < nres) o[lane + 64u] = (uint16_t)res1;
+    }
+}
+
+template <int D, int PH, bool NT, bool ONE>
+hipError_t launch_stream_t(const SegBatchArgs& a, uint32_t spw, hipStream_t s) {
+    const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
+    const int grid = (int)((waves + 3u) / 4u);
+    hipLaunchKernelGGL((seg_stream_kernel<D, PH, NT, ONE>), dim3(grid), dim3(256), 0, s, a, spw);
+    return hipGetLastError();
+}
+
+int stream_ph(const SegBatchArgs& a) {
+    if (a.pseudo == nullptr || a.pseudo_len == 0u) return 0;
+    return a.pseudo_len <= 17u ? 1 : 2;
+}
+
+bool stream_one(const SegBatchArgs& a) {
+    return a.seg_stride == a.seg_len && a.seg_len >= 1024u;
+}
+
+}  // namespace
+
+// Packed segments of >= 1 KiB (stride == len): the form the library picks by default (C2, C5).
+bool stream_dense(const SegBatchArgs& a) {
+    return a.seg_off == nullptr && stream_one(a) && (a.pseudo == nullptr || a.pseudo_len <= 64u);
+}
+
+namespace {
+
+template <int D>
+hipError_t launch_stream_d(const SegBatchArgs& a, uint32_t spw, bool nt, hipStream_t s) {
+    const int ph = stream_ph(a);
+    const bool one = stream_one(a);
+#define NETCSUM_L(PH_, NT_, ONE_) \
+    if (ph == PH_ && nt == NT_ && one == ONE_) return launch_stream_t<D, PH_, NT_, ONE_>(a, spw, s);
+#define NETCSUM_L2(PH_) NETCSUM_L(PH_, true, true) NETCSUM_L(PH_, true, false) NETCSUM_L(PH_, false, true) \
+    NETCSUM_L(PH_, false, false)
+    NETCSUM_L2(0) NETCSUM_L2(1) NETCSUM_L2(2)
+#undef NETCSUM_L2
+#undef NETCSUM_L
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// Dense strided batches only: the wave reads every byte of its run, gaps included, and walks one
+// scalar event per segment, so segments must be long (>= 256 B) with little or no gap between them.
+bool stream_supported(const SegBatchArgs& a) {
+    if (a.seg_off != nullptr || a.seg_len < 256u || a.seg_stride < a.seg_len || a.seg_stride > a.seg_len + 64u) {
+        return false;
+    }
+    if (a.pseudo != nullptr && a.pseudo_len != 0u && a.pseudo_len > 64u) {
+        return false;
+    }
+    return true;
+}
+
+// Segments per wave for a given number of waves: one contiguous run per wave, <= kMaxRun segments
+// (results are held in two VGPRs), run byte span < 2^31.
+uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves) {
+    uint64_t spw = ((uint64_t)a.n_seg + waves - 1u) / (waves ? waves : 1u);
+    spw = std::min<uint64_t>(spw, kMaxRun);
+    return (uint32_t)(spw ? spw : 1u);
+}
+
+int stream_occupancy(int depth, const SegBatchArgs& a, bool nt) {
+    int occ = 0;
+    hipError_t e = hipErrorInvalidValue;
+    const int ph = stream_ph(a);
+    const bool one = stream_one(a);
+#define NETCSUM_OCC(D_, PH_, NT_, ONE_)                                                                   \
+    if (depth == D_ && ph == PH_ && nt == NT_ && one == ONE_) {                                           \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, seg_stream_kernel<D_, PH_, NT_, ONE_>, 256, 0); \
+    }
+#define NETCSUM_OCC2(D_, PH_) NETCSUM_OCC(D_, PH_, true, true) NETCSUM_OCC(D_, PH_, true, false) \
+    NETCSUM_OCC(D_, PH_, false, true) NETCSUM_OCC(D_, PH_, false, false)
+#define NETCSUM_OCC3(D_) NETCSUM_OCC2(D_, 0) NETCSUM_OCC2(D_, 1) NETCSUM_OCC2(D_, 2)
+    NETCSUM_OCC3(4) NETCSUM_OCC3(6) NETCSUM_OCC3(8)
+#undef NETCSUM_OCC3
+#undef NETCSUM_OCC2
+#undef NETCSUM_OCC
+    return (e == hipSuccess && occ > 0) ? occ : 1;
+}
+
+hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s) {
+    if (spw == 0u || spw > kMaxRun) return hipErrorInvalidValue;
+    switch (depth) {
+    case 4: return launch_stream_d<4>(a, spw, nt, s);
+    case 6: return launch_stream_d<6>(a, spw, nt, s);
+    case 8: return launch_stream_d<8>(a, spw, nt, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace netcsum
