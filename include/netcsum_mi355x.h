@@ -263,15 +263,19 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */
     NETCSUM_TUNE_NT_LOADS      = 3,   /* -1 auto (default), 0 plain, 1 non-temporal segment loads */
     NETCSUM_TUNE_BLOCK_THREADS = 4,   /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
-    NETCSUM_TUNE_KERNEL        = 5,   /* 0 auto (default: 5 where it applies, 6 for packed segments
-                                         of >= 1 KiB, else 2), 1 simple,
+    NETCSUM_TUNE_KERNEL        = 5,   /* 0 auto (default: 7 where it applies, else 5 where it
+                                         applies, 6 for packed strided segments of >= 1 KiB and for
+                                         offset/length batches, else 2), 1 simple,
                                          2 pipelined register loads, 3 pipelined LDS-DMA, 4 wave-tile
                                          LDS image (strided; else falls back to 2), 5 small aligned
                                          segments (strided, no pseudo-header, 1-64 B, base and stride
                                          multiples of 4; else falls back to 2), 6 segmented stream
-                                         (strided, stride in [len, len+64], len >= 256, pseudo-header
-                                         <= 64 B; one wave per contiguous run; else falls back to 2;
-                                         CHUNKS = pieces in flight per wave: 4, 6 or 8)             */
+                                         (strided, stride in [len, len+64], len >= 256, or any
+                                         offset/length batch; pseudo-header <= 64 B; one wave per run
+                                         of segments, streamed when packed; else falls back to 2;
+                                         CHUNKS = pieces in flight per wave: 4, 6 or 8), 7 header
+                                         tiles through LDS (kernel 5's domain with stride <= 64 B;
+                                         CHUNKS = tiles in flight per wave: 2, 3 or 4)              */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */

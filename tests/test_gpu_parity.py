@@ -310,7 +310,8 @@ def test_full_size_c2_round_trip_and_sample():
 
 @pytest.mark.parametrize("L", list(range(1, 65)))
 def test_small_aligned_kernel_vs_oracle(L):
-    """seg_small_kernel (kernel 5, auto-selected for strided, pseudo-less, 4-B-aligned segments of
+    """seg_small_kernel (kernel 5) and seg_hdr_kernel (kernel 7, LDS-image tiles; strides <= 64 B)
+    for strided, pseudo-less, 4-B-aligned segments of
     1..64 B — the C3 header shape): every length, several 4-B-aligned strides and base offsets,
     tile / grid-stride geometry, all four ops, half of the segments carrying a valid checksum
     (HdrCalc written at bytes 10-11 as in an IPv4 header) so Verify sees both verdicts."""
@@ -327,16 +328,20 @@ def test_small_aligned_kernel_vs_oracle(L):
                     data[4 + i * stride + 10: 4 + i * stride + 12] = np.frombuffer(np.uint16(c).tobytes(), np.uint8)
             data_d = torch.from_numpy(data).to(DEV)
             for base_off in (0, 4):
-                for kernel, tile, grid in ((0, -1, 0), (5, 0, 1), (5, 0, 3), (5, 1, 0), (5, 7, 0), (5, 2, 3)):
+                for kernel, tile, grid, chunks in ((0, -1, 0, 0), (5, 0, 1, 0), (5, 0, 3, 0), (5, 1, 0, 0),
+                                                   (5, 7, 0, 0), (5, 2, 3, 0), (7, -1, 0, 0), (7, -1, 1, 2),
+                                                   (7, -1, 3, 3), (7, -1, 2, 4)):
                     netcsum.tune(netcsum.TUNE_KERNEL, kernel)
                     netcsum.tune(netcsum.TUNE_TILE, tile)
                     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+                    netcsum.tune(netcsum.TUNE_CHUNKS, chunks)
                     for op in (0, 1, 2, 3):
                         got = _gpu_strided(data_d, base_off, stride, L, None, 0, 0, n, op)
                         want = oracle.batch_strided(data, stride, L, None, 0, 0, n, op, seg_offset=base_off)
-                        assert np.array_equal(got, want), (L, stride, pattern, base_off, kernel, tile, grid, op)
-                        if kernel == 5 and op == 2:
-                            assert netcsum.last_launch().startswith("seg_small_kernel"), netcsum.last_launch()
+                        assert np.array_equal(got, want), (L, stride, pattern, base_off, kernel, tile, grid, chunks, op)
+                        if kernel in (5, 7) and op == 2:
+                            name = "seg_small_kernel" if kernel == 5 or stride > 64 else "seg_hdr_kernel"
+                            assert netcsum.last_launch().startswith(name), netcsum.last_launch()
                     if L >= 12 and pattern == "random" and base_off == 4:
                         assert int(want.sum()) > 0                 # op 3: some headers verify
     # outside its domain kernel 5 falls back to the general form (pseudo-header, odd base)
@@ -412,3 +417,55 @@ def test_stream_kernel_full_c2_equals_pipe_kernel():
     netcsum.batch_strided(seg, L, L, ph, 12, 12, n, ok, 1)
     torch.cuda.synchronize()
     assert bool(ok.all())
+
+
+@pytest.mark.parametrize("layout", ["packed", "packed_zero_len", "gaps", "reversed", "overlap", "mixed", "nic_ring",
+                                    "gap_65"])
+def test_stream_varlen_layouts_vs_oracle(layout):
+    """Kernel 6 on offset/length descriptors: packed runs stream (segment ends from the run's
+    descriptors), every other layout takes the per-segment path of the same kernel; runs of 1..128
+    segments, pseudo-headers of 0/12/40 B, all four ops, against the oracle."""
+    rng = np.random.default_rng(["packed", "packed_zero_len", "gaps", "reversed", "overlap", "mixed", "nic_ring",
+                                 "gap_65"].index(layout))
+    n = 700
+    lens = rng.integers(0, 9001, size=n).astype(np.uint16)
+    small = rng.random(n) < 0.3                                   # many short segments: several ends per piece
+    lens[small] = rng.integers(1, 300, size=int(small.sum())).astype(np.uint16)
+    if layout == "packed_zero_len":
+        lens[::5] = 0
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    off += 3                                                      # odd base for every other segment
+    if layout == "gaps":
+        off += np.arange(n, dtype=np.uint64) * 7
+    elif layout == "reversed":
+        off = off[::-1].copy()
+        lens = lens[::-1].copy()
+        off[1:] = off[:-1]                                         # descending offsets, lengths shuffled
+    elif layout == "overlap":
+        off = (off // 2).astype(np.uint64)
+    elif layout == "mixed":
+        off[n // 2:] += 1                                          # second half shifted by one byte
+    elif layout == "nic_ring":                                     # one 16 KiB ring buffer per datagram
+        off = np.arange(n, dtype=np.uint64) * 16384 + 42
+    elif layout == "gap_65":                                       # just past the streamed-gap limit
+        off += np.arange(n, dtype=np.uint64) * 65
+    tot = int((off + lens).max()) + 64
+    base = _host_bytes(rng, tot, "random")
+    base_d = torch.from_numpy(base).to(DEV)
+    off_d = torch.from_numpy(off.view(np.int64)).to(DEV)
+    len_d = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    for plen, pstride in ((0, 0), (12, 12), (40, 41)):
+        ph = _host_bytes(rng, n * max(pstride, 1) + 64, "random")
+        ph_d = torch.from_numpy(ph).to(DEV)
+        for run, chunks in ((-1, 0), (1, 4), (7, 8), (64, 4), (128, 8), (65, 4)):
+            netcsum.tune(netcsum.TUNE_KERNEL, 6)
+            netcsum.tune(netcsum.TUNE_TILE, run)
+            netcsum.tune(netcsum.TUNE_CHUNKS, chunks)
+            for op in ((0, 1) if plen else (0, 1, 2, 3)):
+                out = _out(n, op)
+                netcsum.batch_varlen(base_d, off_d, len_d, ph_d if plen else None, pstride, plen, n, out, op)
+                torch.cuda.synchronize()
+                assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
+                want = oracle.batch_varlen(base, off, lens, ph if plen else None, pstride, plen, op)
+                assert np.array_equal(_np_out(out), want), (layout, plen, run, chunks, op)

@@ -141,7 +141,28 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
     const int nt = g_tune_nt.load();
 
     if (c.kernel == 0) {
-        c.kernel = netcsum::small_supported(a) ? 5 : (netcsum::stream_dense(a) ? 6 : 2);
+        c.kernel = netcsum::hdr_supported(a) ? 7
+                 : netcsum::small_supported(a) ? 5
+                 : (netcsum::stream_dense(a) || (varlen && netcsum::stream_supported(a))) ? 6 : 2;
+    }
+    if (c.kernel == 7) {
+        if (netcsum::hdr_supported(a)) {
+            // Defaults from the r1y sweeps (C3, 16 M x 20 B): 2 tiles in flight per wave, 4 tiles
+            // per wave (grid = tiles / 16): 5.77 TB/s vs 5.46 for kernel 5; GRID_MULT > 1 instead
+            // sizes the grid as resident blocks x CUs x mult.
+            int st = g_tune_chunks.load();
+            if (!(st == 2 || st == 3 || st == 4)) st = 2;
+            c.chunks_per_pass = st;
+            c.group_lanes = 1;
+            c.nt = true;
+            c.blocks_needed = 0;
+            if (c.grid <= 0) {
+                c.grid = c.grid_mult > 1 ? netcsum::hdr_occupancy(a, st) * c.cus * c.grid_mult
+                                         : (int)std::max<uint64_t>(1u, ((uint64_t)a.n_seg + 1023u) / 1024u);
+            }
+            return c;
+        }
+        c.kernel = 5;                                  // outside its domain: the register form
     }
     if (c.kernel == 6) {
         if (netcsum::stream_supported(a)) {
@@ -578,7 +599,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_nt.store(value < 0 ? -1 : (value != 0));
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
-        if (value < 0 || value > 6) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 7) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_kernel.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CHUNKS:

@@ -123,6 +123,39 @@ __device__ __forceinline__ void wait_vmcnt() {
     else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
 }
 
+// Sum (in the absolute LE frame) of the byte span [a, a+len) by the G lanes of a group; K chunks
+// per lane per pass. Returns the lane's 32-bit partial (exact for
+// spans < 64 KiB).
+template <int G, int K, bool NT>
+__device__ __forceinline__ uint32_t span_partial(uintptr_t a, uint32_t len, int lane) {
+    const uintptr_t q0  = a & ~(uintptr_t)15;
+    const uintptr_t end = a + len;
+    const uint32_t  nch = len ? (uint32_t)((end - q0 + 15) >> 4) : 0u;
+    const int       lead = (int)(a - q0);
+    uint32_t acc = 0u;
+    for (uint32_t c0 = 0; c0 < nch; c0 += (uint32_t)(G * K)) {
+        u32x4 v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = c0 + (uint32_t)(k * G + lane);
+            v[k] = (c < nch) ? load16<NT>(reinterpret_cast<gu32x4*>(q0 + 16u * (uintptr_t)c))
+                             : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t c = c0 + (uint32_t)(k * G + lane);
+            const uintptr_t q = q0 + 16u * (uintptr_t)c;
+            const int lo = (c == 0u) ? lead : 0;
+            const int hi = (c < nch && q + 16u > end) ? (int)(end - q) : 16;
+            if (lo != 0 || hi != 16) {
+                v[k] = mask_chunk(v[k], lo, hi);
+            }
+            acc = sum4(v[k], acc);
+        }
+    }
+    return acc;
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 
 

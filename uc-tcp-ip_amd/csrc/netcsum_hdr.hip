@@ -1,0 +1,180 @@
+// netcsum_hdr.hip — gfx950 kernel for batches of SMALL strided headers through an LDS image
+// (config C3: 16 M x 20 B IPv4 headers; NetUtil_16BitOnesCplChkSumHdrCalc / ...HdrVerify,
+// net_util.c:159-195 / :245-284, whose sum is NetUtil_16BitSumHdrCalc, net_util.c:1160-1208).
+//
+// One lane per header, as in seg_small_kernel (netcsum_small.hip), but the bytes do not reach the
+// lanes through per-lane 20-B-strided loads: a wave's TILE of 64 consecutive headers is one
+// contiguous byte range, fetched as whole 1-KiB LDS-DMA pieces (raw buffer loads with the `lds`
+// modifier: 64 lanes x 16 B, 8 aligned cache lines per wave-instruction, the hardware range check
+// drops the lanes past the tile), and each lane then reads its header's ND dwords back from the LDS
+// image (ds_read_b32 at a 4-B-aligned offset; an odd dword stride such as 5 is bank-conflict free).
+//
+// Pipeline: each wave keeps S tiles in flight in an LDS ring (S x P KiB per wave). Nothing orders a
+// ds_read behind an LDS-DMA except the wave's own vmcnt, so the waits are counted by hand: every
+// iteration issues exactly P DMA and ONE store (a raw buffer store whose inactive lanes carry an
+// out-of-range offset, so the instruction always issues; the prologue pairs each of its S-1 tiles
+// with a dropped store), hence consuming tile i while tiles i+1 .. i+S-1 are in flight waits
+// vmcnt((S-1)(P+1)).
+//
+// Tiles are dealt round-robin over the grid's waves (wave g: tiles g, g+W, g+2W, ...), so at any
+// time the waves in flight read one dense, advancing window of HBM (the read-probe pattern).
+//
+// Arithmetic: headers start at even addresses (base and stride multiples of 4), so the
+// little-endian half-word sum v_sad_u16 needs no rotation; the last dword is masked to the header's
+// length; ~fold16 is the reference's host-order return value (netcsum_kernels.hip header).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "netcsum_device.h"
+#include "netcsum_kernels.h"
+
+namespace netcsum {
+
+namespace {
+
+constexpr int kRsrcWord3 = 0x00020000;     // gfx9-family raw buffer V# word 3
+constexpr uint32_t kOOB = 0x80000000u;     // offset past every num_records: dropped by the range check
+
+typedef __attribute__((address_space(3))) void lds_t;
+
+// Built from readfirstlane'd inputs so the compiler can prove the V# wave-uniform (else it wraps
+// every buffer op in a waterfall loop — cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+    const uint64_t b = reinterpret_cast<uintptr_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), kRsrcWord3);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx9");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// P KiB pieces per tile, S tiles in flight per wave.
+template <int P, int S>
+__global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t nd) {
+    __shared__ uint32_t img[4][S][P * 256];                    // per wave: S stages x P KiB
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = A.n_seg;
+    const uint32_t ntiles = (n + 63u) >> 6;
+    const uint32_t W = gridDim.x * 4u;
+    const uint32_t t0 = blockIdx.x * 4u + w;
+    if (t0 >= ntiles) {
+        return;
+    }
+    const uint32_t cnt = (ntiles - t0 + W - 1u) / W;          // tiles of this wave
+    const uint32_t st = (uint32_t)A.seg_stride;
+    const uint32_t len = A.seg_len;
+    const uint32_t last_mask = (len & 3u) ? ((1u << (8u * (len & 3u))) - 1u) : 0xFFFFFFFFu;
+    const uintptr_t base = (uintptr_t)A.base;
+    const bool verify = A.verify != 0u;
+    const __amdgpu_buffer_rsrc_t ro = rsrc(A.out, verify ? n : 2u * n);
+
+    // Issue tile i (i >= cnt: a dummy whose lanes are all out of range) into ring slot i % S.
+    auto issue = [&](uint32_t i) {
+        const uint32_t slot = i % (uint32_t)S;
+        const uint32_t t = t0 + i * W;
+        const bool live = i < cnt;
+        const uint32_t h0 = live ? t * 64u : 0u;
+        const uint32_t nh = live ? min(64u, n - h0) : 0u;
+        const uintptr_t a0 = base + (uint64_t)h0 * st;
+        const uintptr_t i0 = a0 & ~(uintptr_t)15;
+        const uint32_t bytes = nh ? (uint32_t)(a0 - i0) + (nh - 1u) * st + len : 0u;
+        const __amdgpu_buffer_rsrc_t r = rsrc(reinterpret_cast<const void*>(i0), (bytes + 15u) & ~15u);
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)&img[w][slot][p * 256], 16,
+                                                     (int)(1024u * (uint32_t)p + 16u * lane), 0, 0, 2);
+        }
+    };
+
+    // Prologue: S-1 tiles, each followed by a dropped store (out-of-range offset), so that from the
+    // first iteration on exactly (S-1)(P+1) VMEM ops are younger than the tile being consumed.
+#pragma unroll
+    for (int j = 0; j < S - 1; ++j) {
+        issue((uint32_t)j);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, ro, (int)kOOB, 0, 0);
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+        issue(i + (uint32_t)S - 1u);
+        wait_vm<(S - 1) * (P + 1)>();                         // tile i landed in LDS
+        const uint32_t slot = i % (uint32_t)S;
+        const uint32_t h0 = (t0 + i * W) * 64u;
+        const uint32_t nh = min(64u, n - h0);
+        const uintptr_t a0 = base + (uint64_t)h0 * st;
+        const uint32_t dw0 = ((uint32_t)(a0 & 15u) + lane * st) >> 2;   // header's first dword in the image
+        const uint32_t* im = &img[w][slot][0];
+        uint32_t acc = 0u;
+        for (uint32_t d = 0; d + 1u < nd; ++d) {
+            acc = __builtin_amdgcn_sad_u16(im[dw0 + d], 0u, acc);
+        }
+        acc = __builtin_amdgcn_sad_u16(im[dw0 + nd - 1u] & last_mask, 0u, acc);
+        const uint32_t s = fold16(acc);
+        const uint32_t h = h0 + lane;
+        if (verify) {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(s == 0xFFFFu ? 1u : 0u), ro,
+                                                 (int)(lane < nh ? h : kOOB), 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(~s), ro, (int)(lane < nh ? 2u * h : kOOB), 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // image reads done before the slot refills
+    }
+    wait_vm<0>();                                              // trailing dummy DMA
+}
+
+template <int P, int S>
+hipError_t launch_hdr_t(const SegBatchArgs& a, int grid, hipStream_t s) {
+    const uint32_t tiles = (a.n_seg + 63u) / 64u;
+    const uint32_t g = grid > 0 ? (uint32_t)grid : (tiles + 3u) / 4u;
+    hipLaunchKernelGGL((seg_hdr_kernel<P, S>), dim3(std::max<uint32_t>(1u, std::min<uint32_t>(g, (tiles + 3u) / 4u))),
+                       dim3(256), 0, s, a, (a.seg_len + 3u) >> 2);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Pieces per 64-header tile: the image starts at the 16-B boundary below the tile (lead <= 12).
+uint32_t hdr_pieces(const SegBatchArgs& a) {
+    return (uint32_t)((12u + 63u * a.seg_stride + a.seg_len + 1023u) / 1024u);
+}
+
+bool hdr_supported(const SegBatchArgs& a) {
+    return small_supported(a) && a.seg_stride <= 64u && hdr_pieces(a) <= 5u && a.n_seg < 0x3FFFFFFFu;
+}
+
+// grid <= 0: one wave per tile (4 tiles per block). grid > 0: that many blocks, tiles dealt
+// round-robin over their waves.
+int hdr_occupancy(const SegBatchArgs& a, int stages) {
+    const uint32_t p = hdr_pieces(a);
+    const int S = stages == 2 ? 2 : (stages == 3 ? 3 : 4);
+    int occ = 0;
+    hipError_t e = hipErrorInvalidValue;
+#define NETCSUM_H(P_, S_) \
+    if (p == P_ && S == S_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, seg_hdr_kernel<P_, S_>, 256, 0);
+    NETCSUM_H(1, 2) NETCSUM_H(1, 3) NETCSUM_H(1, 4) NETCSUM_H(2, 2) NETCSUM_H(2, 3) NETCSUM_H(2, 4)
+    NETCSUM_H(3, 2) NETCSUM_H(3, 3) NETCSUM_H(3, 4) NETCSUM_H(4, 2) NETCSUM_H(4, 3) NETCSUM_H(4, 4) \
+    NETCSUM_H(5, 2) NETCSUM_H(5, 3) NETCSUM_H(5, 4)
+#undef NETCSUM_H
+    return (e == hipSuccess && occ > 0) ? occ : 1;
+}
+
+hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int grid, hipStream_t s) {
+    if (!hdr_supported(a)) return hipErrorInvalidValue;
+    const uint32_t p = hdr_pieces(a);
+    const int S = stages == 2 ? 2 : (stages == 3 ? 3 : 4);
+#define NETCSUM_H(P_, S_) \
+    if (p == P_ && S == S_) return launch_hdr_t<P_, S_>(a, grid, s);
+    NETCSUM_H(1, 2) NETCSUM_H(1, 3) NETCSUM_H(1, 4) NETCSUM_H(2, 2) NETCSUM_H(2, 3) NETCSUM_H(2, 4)
+    NETCSUM_H(3, 2) NETCSUM_H(3, 3) NETCSUM_H(3, 4) NETCSUM_H(4, 2) NETCSUM_H(4, 3) NETCSUM_H(4, 4) \
+    NETCSUM_H(5, 2) NETCSUM_H(5, 3) NETCSUM_H(5, 4)
+#undef NETCSUM_H
+    return hipErrorInvalidValue;
+}
+
+}  // namespace netcsum

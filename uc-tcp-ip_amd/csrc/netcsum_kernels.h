@@ -33,7 +33,8 @@ struct LaunchCfg {
     int  kernel;           // 1: seg_batch_kernel (one segment in flight per group), 2: seg_pipe_kernel,
                            // 3: seg_lds_kernel, 4: seg_tile_kernel (strided only),
                            // 5: seg_small_kernel (small 4-B-aligned strided segments, no pseudo),
-                           // 6: seg_stream_kernel (dense strided runs, one wave per run)
+                           // 6: seg_stream_kernel (dense strided runs, one wave per run),
+                           // 7: seg_hdr_kernel (small headers through LDS-image tiles)
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
     uint32_t stream_spw;   // kernel 6: segments per wave (one contiguous run each)
@@ -74,6 +75,9 @@ const char* last_launch();                  // description of this thread's last
 hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream_t s);
 bool small_supported(const SegBatchArgs& a);  // strided, no pseudo, 1..64 B, base/stride 4-B aligned
 hipError_t launch_small_batch(const SegBatchArgs& a, int grid, hipStream_t s);
+bool hdr_supported(const SegBatchArgs& a);     // small_supported and stride <= 64: LDS-image header tiles
+int hdr_occupancy(const SegBatchArgs& a, int stages);
+hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256
 bool stream_dense(const SegBatchArgs& a);      // strided, stride == len >= 1024: the default for kernel 6
 uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves);

@@ -38,38 +38,6 @@
 
 namespace netcsum {
 
-// Sum (in the absolute LE frame) of the byte span [a, a+len) by the G lanes of a group; K chunks
-// per lane per pass. Returns the lane's 32-bit partial.
-template <int G, int K, bool NT>
-__device__ __forceinline__ uint32_t span_partial(uintptr_t a, uint32_t len, int lane) {
-    const uintptr_t q0  = a & ~(uintptr_t)15;
-    const uintptr_t end = a + len;
-    const uint32_t  nch = len ? (uint32_t)((end - q0 + 15) >> 4) : 0u;
-    const int       lead = (int)(a - q0);
-    uint32_t acc = 0u;
-    for (uint32_t c0 = 0; c0 < nch; c0 += (uint32_t)(G * K)) {
-        u32x4 v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t c = c0 + (uint32_t)(k * G + lane);
-            v[k] = (c < nch) ? load16<NT>(reinterpret_cast<gu32x4*>(q0 + 16u * (uintptr_t)c))
-                             : u32x4{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t c = c0 + (uint32_t)(k * G + lane);
-            const uintptr_t q = q0 + 16u * (uintptr_t)c;
-            const int lo = (c == 0u) ? lead : 0;
-            const int hi = (c < nch && q + 16u > end) ? (int)(end - q) : 16;
-            if (lo != 0 || hi != 16) {
-                v[k] = mask_chunk(v[k], lo, hi);
-            }
-            acc = sum4(v[k], acc);
-        }
-    }
-    return acc;
-}
-
 // Segment -> group mapping. Tile mode (P.tile = J > 0): block b owns the contiguous tile
 // [b*gpb*J, (b+1)*gpb*J) and its gpb groups step through it gpb segments at a time, so the blocks
 // in flight (dispatched in order) read one contiguous, advancing window of HBM. Grid-stride mode
@@ -992,8 +960,13 @@ const char* last_launch() {
 
 static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel",
-                                  "seg_small_kernel", "seg_stream_kernel"};
-    const int kid = (c.kernel >= 1 && c.kernel <= 6) ? c.kernel : 0;
+                                  "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel"};
+    const int kid = (c.kernel >= 1 && c.kernel <= 7) ? c.kernel : 0;
+    if (kid == 7) {
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<S=%d> block=256 grid=%d", c.chunks_per_pass,
+                 c.grid);
+        return;
+    }
     if (kid == 6) {
         snprintf(g_last_launch, sizeof(g_last_launch), "seg_stream_kernel<D=%d%s%s> block=256 segs_per_wave=%u",
                  c.chunks_per_pass, (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "", c.stream_spw);
@@ -1013,6 +986,9 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
     }
     if (c.kernel == 6) {
         return launch_stream_batch(a, c.chunks_per_pass, c.stream_spw, c.nt, s);   // K = pieces in flight
+    }
+    if (c.kernel == 7) {
+        return launch_hdr_batch(a, c.chunks_per_pass, c.grid, s);                 // K = tiles in flight
     }
     if (c.kernel == 4) {
         return launch_tile_dispatch(a, c, s);

@@ -91,7 +91,96 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-constexpr uint32_t kMaxRun = 128u;     // segments per wave run: results live in two VGPRs (lane = k % 64)
+constexpr uint32_t kMaxRun = 128u;
+constexpr uint64_t kMaxGap = 64u;      // varlen runs stream across gaps of up to this many bytes     // segments per wave run: results live in two VGPRs (lane = k % 64)
+
+// Pseudo-header sums of run segments [s_begin, s_begin + nres): lane k % 64 of ps0 (k < 64) / ps1
+// holds segment k's pseudo-header sum, folded, in its own stream frame, from the 16-B-aligned chunks
+// that cover it (all loads issued before any is used). PH 1: <= 2 chunks per header, 2: <= 5.
+template <int PH>
+__device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t s_begin, uint32_t nres, uint32_t lane,
+                                                uint32_t& ps0, uint32_t& ps1) {
+    const uint32_t plen = A.pseudo_len;
+    const uint32_t pst = A.pseudo_stride;
+    const uintptr_t pfirst = (uintptr_t)A.pseudo + (uint64_t)s_begin * pst;
+    const uintptr_t PB = pfirst & ~(uintptr_t)15;
+    const uint32_t plead = (uint32_t)(pfirst - PB);
+    const uint32_t pspan = plead + (nres - 1u) * pst + plen;
+    const __amdgpu_buffer_rsrc_t rp = run_rsrc(PB, (pspan + 15u) & ~15u);
+    const uint32_t nchmax = (plen + 30u) >> 4;                 // chunks one pseudo-header can touch
+    constexpr int kPch = PH == 1 ? 2 : 5;
+    u32x4 pv[2][kPch];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        const uint32_t k = lane + 64u * (uint32_t)sl;
+        const uint32_t a = plead + k * pst;
+        const uint32_t hi = (a & 15u) + plen;
+#pragma unroll
+        for (int i = 0; i < kPch; ++i) {
+            if ((uint32_t)i < nchmax) {                        // wave-uniform
+                const uint32_t off = (k < nres && 16u * (uint32_t)i < hi) ? (a & ~15u) + 16u * (uint32_t)i : kOOB;
+                pv[sl][i] = buf_load16<false>(rp, off);
+            } else {
+                pv[sl][i] = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        const uint32_t k = lane + 64u * (uint32_t)sl;
+        const uint32_t a = plead + k * pst;
+        const int lo = (int)(a & 15u);
+        const int hi = lo + (int)plen;
+        uint32_t acc = 0u;
+#pragma unroll
+        for (int i = 0; i < kPch; ++i) {
+            const int b = 16 * i;
+            acc += low_bytes(pv[sl][i], min(max(hi - b, 0), 16)) - low_bytes(pv[sl][i], min(max(lo - b, 0), 16));
+        }
+        uint32_t s = fold16(acc);
+        if (a & 1u) {
+            s = rot8(s);
+        }
+        if (sl == 0) {
+            ps0 = s;
+        } else {
+            ps1 = s;
+        }
+    }
+}
+
+// Scalar epilogue shared by the stream kernels: the folded result of run segment k from the wave
+// total T of its bytes (absolute LE frame; `odd`: the segment starts at an odd stream position),
+// plus its pseudo-header sum, complemented (Calc) or compared (Verify), into lane k % 64 of r0/r1.
+template <int PH>
+__device__ __forceinline__ void finish_segment(uint32_t k, uint32_t T, bool odd, bool verify, uint32_t lane,
+                                               uint32_t ps0, uint32_t ps1, uint32_t& r0, uint32_t& r1) {
+    uint32_t t = fold16(T);
+    if (odd) {
+        t = rot8(t);
+    }
+    if constexpr (PH != 0) {
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)ps0, (int)(k & 63u));
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)ps1, (int)(k & 63u));
+        t = fold16(t + (k < 64u ? p0 : p1));
+    }
+    const uint32_t val = verify ? (t == 0xFFFFu ? 1u : 0u) : (~t & 0xFFFFu);
+    r0 = (lane == k) ? val : r0;
+    r1 = (lane + 64u == k) ? val : r1;
+}
+
+__device__ __forceinline__ void store_run_results(const SegBatchArgs& A, uint32_t s_begin, uint32_t nres,
+                                                  uint32_t lane, uint32_t r0, uint32_t r1) {
+    if (A.verify) {
+        uint8_t* o = static_cast<uint8_t*>(A.out) + s_begin;
+        if (lane < nres) o[lane] = (uint8_t)r0;
+        if (lane + 64u < nres) o[lane + 64u] = (uint8_t)r1;
+    } else {
+        uint16_t* o = static_cast<uint16_t*>(A.out) + s_begin;
+        if (lane < nres) o[lane] = (uint16_t)r0;
+        if (lane + 64u < nres) o[lane + 64u] = (uint16_t)r1;
+    }
+}
 
 // One wave = segments [s_begin, s_end) of a strided batch (stride >= len >= 1, run <= 128 segments).
 // ONE: stride == len >= 1024, so at most one segment ends inside any 1-KiB piece and the next one
@@ -127,76 +216,15 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
 
-    // ... while the run's pseudo-header sums are computed: lane k % 64 of slot k / 64 holds segment
-    // k's pseudo-header sum (folded, in its own stream frame) from its 16-B-aligned chunks.
+    // ... while the run's pseudo-header sums are computed.
     uint32_t ps0 = 0u, ps1 = 0u;
     if constexpr (PH != 0) {
-        const uint32_t plen = A.pseudo_len;
-        const uint32_t pst = A.pseudo_stride;
-        const uintptr_t pfirst = (uintptr_t)A.pseudo + (uint64_t)s_begin * pst;
-        const uintptr_t PB = pfirst & ~(uintptr_t)15;
-        const uint32_t plead = (uint32_t)(pfirst - PB);
-        const uint32_t pspan = plead + (nres - 1u) * pst + plen;
-        const __amdgpu_buffer_rsrc_t rp = run_rsrc(PB, (pspan + 15u) & ~15u);
-        const uint32_t nchmax = (plen + 30u) >> 4;             // chunks one pseudo-header can touch (<= 5)
-        constexpr int kPch = PH == 1 ? 2 : 5;
-        u32x4 pv[2][kPch];                                     // all loads issued before any is used
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-            const uint32_t k = lane + 64u * (uint32_t)sl;
-            const uint32_t a = plead + k * pst;
-            const uint32_t hi = (a & 15u) + plen;
-#pragma unroll
-            for (int i = 0; i < kPch; ++i) {
-                if ((uint32_t)i < nchmax) {                    // wave-uniform
-                    const uint32_t off = (k < nres && 16u * (uint32_t)i < hi) ? (a & ~15u) + 16u * (uint32_t)i : kOOB;
-                    pv[sl][i] = buf_load16<false>(rp, off);
-                } else {
-                    pv[sl][i] = u32x4{0u, 0u, 0u, 0u};
-                }
-            }
-        }
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-            const uint32_t k = lane + 64u * (uint32_t)sl;
-            const uint32_t a = plead + k * pst;
-            const int lo = (int)(a & 15u);
-            const int hi = lo + (int)plen;
-            uint32_t acc = 0u;
-#pragma unroll
-            for (int i = 0; i < kPch; ++i) {
-                const int b = 16 * i;
-                acc += low_bytes(pv[sl][i], min(max(hi - b, 0), 16)) - low_bytes(pv[sl][i], min(max(lo - b, 0), 16));
-            }
-            uint32_t s = fold16(acc);
-            if (a & 1u) {
-                s = rot8(s);
-            }
-            if (sl == 0) {
-                ps0 = s;
-            } else {
-                ps1 = s;
-            }
-        }
+        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
     }
 
     uint32_t res0 = 0u, res1 = 0u;                             // result of run segment k: lane k % 64
-    // Scalar epilogue of segment `cur` from the wave total T of its bytes (absolute LE frame).
     auto finish = [&](uint32_t cur, uint32_t T, bool odd) {
-        uint32_t t = fold16(T);
-        if (odd) {
-            t = rot8(t);
-        }
-        const uint32_t k = cur - s_begin;
-        if constexpr (PH != 0) {
-            const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)ps0, (int)(k & 63u));
-            const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)ps1, (int)(k & 63u));
-            const uint32_t p = k < 64u ? p0 : p1;
-            t = fold16(t + p);
-        }
-        const uint32_t val = A.verify ? (t == 0xFFFFu ? 1u : 0u) : (~t & 0xFFFFu);
-        res0 = (lane == k) ? val : res0;
-        res1 = (lane + 64u == k) ? val : res1;
+        finish_segment<PH>(cur - s_begin, T, odd, A.verify != 0u, lane, ps0, ps1, res0, res1);
     };
 
     uint32_t cur = s_begin;                                    // next segment to finish
@@ -265,15 +293,168 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
 
-    if (A.verify) {
-        uint8_t* o = static_cast<uint8_t*>(A.out) + s_begin;
-        if (lane < nres) o[lane] = (uint8_t)res0;
-        if (lane + 64u < nres) o[lane + 64u] = (uint8_t)res1;
-    } else {
-        uint16_t* o = static_cast<uint16_t*>(A.out) + s_begin;
-        if (lane < nres) o[lane] = (uint16_t)res0;
-        if (lane + 64u < nres) o[lane + 64u] = (uint16_t)res1;
+    store_run_results(A, s_begin, nres, lane, res0, res1);
+}
+
+// Variable-length batches (offset/length descriptors, config C4). A wave takes a run of segments;
+// when they are PACKED (each starts where the previous one ends — the layout of back-to-back
+// datagrams) the run is one byte stream and the wave reads it exactly like seg_stream_kernel, with
+// the segment bounds taken from the run's descriptors (held in VGPRs: lane k % 64 of slot k / 64) by
+// v_readlane; gaps of up to kMaxGap bytes between segments are read and skipped. Any other run
+// (larger gaps, reordering, overlap, a span >= 2^31) is summed four segments at a time by 16-lane
+// groups — always correct; the packed layout is the fast path.
+template <int D, int PH, bool NT>
+__global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, uint32_t spw) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    if (sb64 >= A.n_seg) {
+        return;
     }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(A.n_seg - s_begin, spw);
+    const uint32_t s_end = s_begin + nres;
+    const uint32_t lane16 = 16u * lane;
+    const bool ph_odd = PH != 0 && (A.pseudo_len & 1u) != 0u;
+    const uintptr_t base = (uintptr_t)A.base;
+
+    // The run's descriptors: slot 0 = segments lane, slot 1 = segments 64 + lane.
+    const bool v0 = lane < nres, v1 = lane + 64u < nres;
+    const uint64_t off0 = v0 ? A.seg_off[s_begin + lane] : 0ull;
+    const uint64_t off1 = v1 ? A.seg_off[s_begin + 64u + lane] : 0ull;
+    const uint32_t len0 = v0 ? A.seg_len_v[s_begin + lane] : 0u;
+    const uint32_t len1 = v1 ? A.seg_len_v[s_begin + 64u + lane] : 0u;
+
+    uint32_t ps0 = 0u, ps1 = 0u;
+    if constexpr (PH != 0) {
+        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
+    }
+    uint32_t res0 = 0u, res1 = 0u;
+
+    // Packed? Segment k starts where k - 1 ends, and the run spans < 2^31 bytes.
+    const uint64_t end0 = off0 + len0, end1 = off1 + len1;
+    const uint64_t prev0 = __shfl_up(end0, 1, 64);
+    const uint64_t prev1_up = __shfl_up(end1, 1, 64);
+    const uint64_t last0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end0 >> 32), 63) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end0, 63);
+    const uint64_t prev1 = lane == 0u ? last0 : prev1_up;
+    const bool ok0 = !v0 || lane == 0u || (off0 >= prev0 && off0 - prev0 <= kMaxGap);
+    const bool ok1 = !v1 || (off1 >= prev1 && off1 - prev1 <= kMaxGap);
+    const uint64_t first = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(off0 >> 32), 0) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off0, 0);
+    const uint32_t kl = nres - 1u;                             // last segment of the run
+    const uint64_t eA = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end0 >> 32), (int)(kl & 63u)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end0, (int)(kl & 63u));
+    const uint64_t eB = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end1 >> 32), (int)(kl & 63u)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end1, (int)(kl & 63u));
+    const uint64_t run_end = kl < 64u ? eA : eB;
+    const bool packed = __all(ok0 && ok1) && run_end >= first && run_end - first < (1ull << 31) - 256u;
+
+    if (!packed) {
+        // Scattered run: four segments at a time, a 16-lane group each (the lane-group form of
+        // seg_pipe_kernel: 4 chunks per lane in flight per pass), group totals to the scalar epilogue.
+        const uint32_t g = lane >> 4;
+        for (uint32_t k0 = 0; k0 < nres; k0 += 4u) {          // wave-uniform loop
+            const uint32_t k = k0 + g;
+            const int src = (int)(k & 63u);
+            const uint64_t o0 = __shfl(off0, src, 64), o1 = __shfl(off1, src, 64);
+            const uint32_t l0 = (uint32_t)__shfl((int)len0, src, 64), l1 = (uint32_t)__shfl((int)len1, src, 64);
+            const uintptr_t a = base + (k < 64u ? o0 : o1);
+            const uint32_t len = k < nres ? (k < 64u ? l0 : l1) : 0u;
+            const uint32_t tot = group_sum<16>(span_partial<16, 4, NT>(a, len, (int)(lane & 15u)));
+            const uint32_t odd = (uint32_t)(((a & 1u) != 0u) != ph_odd);
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+                if (k0 + i < nres) {
+                    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)(16u * i));
+                    const bool o = __builtin_amdgcn_readlane((int)odd, (int)(16u * i)) != 0;
+                    finish_segment<PH>(k0 + i, T, o, A.verify != 0u, lane, ps0, ps1, res0, res1);
+                }
+            }
+        }
+        store_run_results(A, s_begin, nres, lane, res0, res1);
+        return;
+    }
+
+    const uintptr_t a_first = base + first;
+    const uintptr_t O = a_first & ~(uintptr_t)127;
+    const uint32_t lead = (uint32_t)(a_first - O);
+    const uint32_t span = lead + (uint32_t)(run_end - first);
+    const uint32_t npieces = max(1u, (span + 1023u) >> 10);   // >= 1: a run of empty segments still ends
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
+    u32x4 dv[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+    }
+    // run-relative segment starts and ends (a packed run may have gaps of <= kMaxGap bytes)
+    const uint32_t rs0 = lead + (uint32_t)(off0 - first), re0 = rs0 + len0;
+    const uint32_t rs1 = lead + (uint32_t)(off1 - first), re1 = rs1 + len1;
+    auto pick = [&](uint32_t x0, uint32_t x1, uint32_t k) -> uint32_t {   // lane k % 64 of slot k / 64
+        const uint32_t y0 = (uint32_t)__builtin_amdgcn_readlane((int)x0, (int)(k & 63u));
+        const uint32_t y1 = (uint32_t)__builtin_amdgcn_readlane((int)x1, (int)(k & 63u));
+        return k < 64u ? y0 : y1;
+    };
+
+    uint32_t cur = s_begin;
+    uint32_t cs = lead;
+    uint32_t ce = pick(re0, re1, 0u);
+    uint32_t acc = 0u;
+    auto consume = [&](uint32_t q, u32x4 v) {
+        const uint32_t qb = q << 10;
+        const uint32_t pend = qb + 1024u;
+        const uint32_t full = sum4(v, 0u);
+        uint32_t u = cur, c = cs, e = ce, a = acc;
+        if (!(u < s_end && e <= pend)) {
+            if (u < s_end) {
+                a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+            }
+        } else {
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+#pragma clang loop vectorize(disable) unroll(disable)
+            do {
+                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                finish_segment<PH>(u - s_begin, wave_total(a + (Pe - Ps)), ((c & 1u) != 0u) != ph_odd,
+                                   A.verify != 0u, lane, ps0, ps1, res0, res1);
+                a = 0u;
+                ++u;
+                const uint32_t pe = e;
+                if (u < s_end) {
+                    c = pick(rs0, rs1, u - s_begin);
+                    e = pick(re0, re1, u - s_begin);
+                }
+                Ps = (c == pe) ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+            } while (u < s_end && e <= pend);
+            if (u < s_end) {
+                a = full - Ps;
+            }
+        }
+        cur = u;
+        cs = c;
+        ce = e;
+        acc = a;
+    };
+
+    const uint32_t rounds = (npieces + (uint32_t)D - 1u) / (uint32_t)D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const uint32_t q = r * (uint32_t)D + (uint32_t)j;
+            consume(q, opaque_tuple(dv[j]));
+            dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);
+            asm volatile("" ::: "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_run_results(A, s_begin, nres, lane, res0, res1);
+}
+
+template <int D, int PH, bool NT>
+hipError_t launch_stream_varlen_t(const SegBatchArgs& a, uint32_t spw, hipStream_t s) {
+    const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
+    const int grid = (int)((waves + 3u) / 4u);
+    hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256), 0, s, a, spw);
+    return hipGetLastError();
 }
 
 template <int D, int PH, bool NT, bool ONE>
@@ -321,7 +502,10 @@ hipError_t launch_stream_d(const SegBatchArgs& a, uint32_t spw, bool nt, hipStre
 // Dense strided batches only: the wave reads every byte of its run, gaps included, and walks one
 // scalar event per segment, so segments must be long (>= 256 B) with little or no gap between them.
 bool stream_supported(const SegBatchArgs& a) {
-    if (a.seg_off != nullptr || a.seg_len < 256u || a.seg_stride < a.seg_len || a.seg_stride > a.seg_len + 64u) {
+    if (a.seg_off != nullptr) {                       // varlen: any layout (packed runs stream)
+        return a.pseudo == nullptr || a.pseudo_len == 0u || a.pseudo_len <= 64u;
+    }
+    if (a.seg_len < 256u || a.seg_stride < a.seg_len || a.seg_stride > a.seg_len + 64u) {
         return false;
     }
     if (a.pseudo != nullptr && a.pseudo_len != 0u && a.pseudo_len > 64u) {
@@ -359,6 +543,16 @@ int stream_occupancy(int depth, const SegBatchArgs& a, bool nt) {
 
 hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s) {
     if (spw == 0u || spw > kMaxRun) return hipErrorInvalidValue;
+    if (a.seg_off != nullptr) {                       // varlen: depth 4 or 8
+        const int ph = stream_ph(a);
+#define NETCSUM_V(D_, PH_, NT_) \
+        if ((depth == 8) == (D_ == 8) && ph == PH_ && nt == NT_) return launch_stream_varlen_t<D_, PH_, NT_>(a, spw, s);
+        NETCSUM_V(4, 0, true) NETCSUM_V(4, 0, false) NETCSUM_V(4, 1, true) NETCSUM_V(4, 1, false)
+        NETCSUM_V(4, 2, true) NETCSUM_V(4, 2, false) NETCSUM_V(8, 0, true) NETCSUM_V(8, 0, false)
+        NETCSUM_V(8, 1, true) NETCSUM_V(8, 1, false) NETCSUM_V(8, 2, true) NETCSUM_V(8, 2, false)
+#undef NETCSUM_V
+        return hipErrorInvalidValue;
+    }
     switch (depth) {
     case 4: return launch_stream_d<4>(a, spw, nt, s);
     case 6: return launch_stream_d<6>(a, spw, nt, s);
