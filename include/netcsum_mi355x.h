@@ -67,6 +67,15 @@ CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumDataVerify(void        *pdata_buf,
                                                   CPU_INT16U   pseudo_hdr_size,
                                                   NET_ERR     *p_err);
 
+/* The reference's optional native-loop seam (net_util.h:486-490; NET_CFG_OPTIMIZE_ASM_EN): unfolded
+ * sum of the network-order 16-bit words of [pdata_32, pdata_32 + size), size a multiple of 4, as
+ * NetUtil_16BitSumDataCalc adds it (net_util.c:1407-1415). A stack that keeps its own net_util.c with
+ * the ASM option enabled links this instead of a Ports/<cpu>/net_util_a.* file. Per-buffer and
+ * synchronous (one GPU round trip per call); a device failure returns 0 with a message on stderr
+ * (the signature has no error channel). */
+CPU_INT32U   NetUtil_16BitSumDataCalcAlign_32    (void        *pdata_32,
+                                                  CPU_INT32U   size);
+
 /* ============================================================================================
  * (2) Batch ABI — device-resident segments.
  *
@@ -279,9 +288,14 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
-    NETCSUM_TUNE_TILE          = 9    /* J > 0: each block owns a contiguous tile of J segments per
+    NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).
                                          Kernel 6: J > 0 = segments per wave run (<= 128; auto 16) */
+    NETCSUM_TUNE_TX_WRITEBACK  = 10   /* TxFinalizeIPv4 checksum stores: -1 auto (default), 0 two-
+                                         byte stores, 1 / 2 rewrite the whole aligned 32 / 64-B
+                                         sectors holding the fields (strided batches with stride
+                                         >= 192 B, sector-aligned d_base, >= 16 lanes per packet;
+                                         elsewhere two-byte stores)                                 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

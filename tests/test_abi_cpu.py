@@ -98,6 +98,7 @@ def test_no_gpu_fails_loudly_without_fallback():
     ch = netcsum.Chain([{"data": b"abcdef", "proto": 71}])
     assert netcsum.DataVerify(ch.ptr, None, 0) == (0, netcsum.NET_UTIL_ERR_MI355X_DEV)
     assert netcsum.stream_sum32([(hb.ptr, 20)])[1] == netcsum.NET_UTIL_ERR_MI355X_DEV
+    assert netcsum.SumDataCalcAlign_32(hb.ptr, 20) == 0         # no error channel: 0 + stderr
 
 
 def test_header_is_plain_c():

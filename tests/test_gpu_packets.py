@@ -20,11 +20,13 @@ def _defaults():
         netcsum.tune(k, 0)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_TILE, -1)
+    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, -1)
     yield
     for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES):
         netcsum.tune(k, 0)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_TILE, -1)
+    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, -1)
 
 
 def _rx_gpu(buf, offs, lens):
@@ -101,3 +103,40 @@ def test_tx_finalize_writes_reference_checksums_then_rx_accepts(udp_tx_csum):
     assert ((got[ok] & op.IP_OK) != 0).all()
     checked = ok & ((got & op.L4_CHECKED) != 0)
     assert ((got[checked] & op.L4_OK) != 0).all()
+
+
+@pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (2048, 1514), (200, 184), (192, 48)])
+@pytest.mark.parametrize("wb", [-1, 0, 1, 2])
+def test_tx_finalize_strided_writeback_modes(stride, pkt_len, wb):
+    """Strided Tx finalize under every write-back form (TUNE_TX_WRITEBACK: 0 two-byte stores, 1 / 2
+    whole 32 / 64-B sectors): packets finalized exactly as the packet oracle does, and every byte
+    between packets (stride > pkt_len) and past the last one left as it was. Strides that are not
+    multiples of 64 put packets at every sector offset; 48-B slots make the 64-B sectors overrun
+    the packet, which must fall back to two-byte stores."""
+    rng = random.Random(stride * 7 + pkt_len * 3 + wb)
+    n = 600
+    kinds = ["tcp", "tcp", "udp", "udp0", "icmp", "igmp", "other", "frag", "tcp_short", "bad_ver"]
+    buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
+    for i in range(n):
+        p = bytearray(make_packet(rng, rng.choice(kinds), payload=rng.randint(0, max(0, pkt_len - 100))))
+        p = p[:pkt_len]
+        if len(p) >= 12 and rng.random() < 0.5:
+            p[10:12] = rng.randbytes(2)                           # stale IP checksum field
+        buf[i * stride:i * stride + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, wb)
+    if pkt_len < 1000:
+        netcsum.tune(netcsum.TUNE_GROUP_LANES, 16)                # write-back needs >= 16 lanes per packet
+    b = torch.from_numpy(buf).to(DEV)
+    assert b.data_ptr() % 64 == 0
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b, n, f, stride=stride, pkt_len=pkt_len)
+    torch.cuda.synchronize()
+    out = b.cpu().numpy()
+    want = buf.copy()
+    want_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        pk, want_f[i] = op.tx_finalize(bytes(buf[i * stride:i * stride + pkt_len]), True)
+        want[i * stride:i * stride + pkt_len] = np.frombuffer(pk, np.uint8)
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, [(int(j), int(j) // stride, int(j) % stride, int(out[j]), int(want[j])) for j in bad[:8]]
+    assert np.array_equal(f.cpu().numpy(), want_f)

@@ -469,3 +469,16 @@ def test_stream_varlen_layouts_vs_oracle(layout):
                 assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
                 want = oracle.batch_varlen(base, off, lens, ph if plen else None, pstride, plen, op)
                 assert np.array_equal(_np_out(out), want), (layout, plen, run, chunks, op)
+
+
+def test_sum_align32_hook_matches_reference_inner_sum():
+    """NetUtil_16BitSumDataCalcAlign_32 (net_util.h:486-490): the unfolded network-order word sum the
+    reference's inner loop adds (net_util.c:1407-1415), for 4-byte-aligned regions of 0..65532 B."""
+    rng = random.Random(31)
+    for size in [0, 4, 8, 20, 1480, 1500, 9000, 65532]:
+        for pat in ("random", "ff", "carry"):
+            data = rand_bytes(rng, size, pat)
+            hb = netcsum.HostBytes(data)
+            assert hb.ptr % 4 == 0
+            want = sum(int.from_bytes(data[i:i + 2], "big") for i in range(0, size, 2)) & 0xFFFFFFFF
+            assert netcsum.SumDataCalcAlign_32(hb.ptr, size) == want, (size, pat)

@@ -30,6 +30,8 @@ std::atomic<int> g_tune_chunks{0};
 std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
 std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
+std::atomic<int> g_tune_tx_wb{-1};                // -1: auto Tx write-back form (kTxSectorAuto)
+constexpr uint32_t kTxSectorAuto = 0u;            // sector bytes auto mode uses where eligible (0: two-byte stores)
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -498,9 +500,25 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         g = d_off ? 32 : std::max(8, pow2_group((chunks + 5u) / 6u));
     }
     c.group_lanes = pow2_group((uint32_t)g);
-    c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks + c.group_lanes - 1u) / c.group_lanes));
+    if (tx) {
+        // Whole-sector write-back (PktBatchArgs::wb_sector): strided batches only, packets at least
+        // 192 B apart (no two packets' checksum fields share a sector: fields lie within the first
+        // 78 B), a sector-aligned base (no frame starts before the buffer), >= 16 lanes per packet
+        // (header fields within the frame's first 16*G bytes).
+        const int wb = g_tune_tx_wb.load();
+        const uint32_t sec = wb == 1 ? 32u : (wb == 2 ? 64u : (wb < 0 ? kTxSectorAuto : 0u));
+        if (sec != 0u && d_off == nullptr && stride >= 192u && ((uintptr_t)d_base % sec) == 0u &&
+            c.group_lanes >= 16) {
+            a.wb_sector = sec;
+        }
+    }
+    const uint32_t lead_max = a.wb_sector ? a.wb_sector - 1u : 15u;
+    const uint32_t chunks_f = d_off ? chunks : ((uint32_t)pkt_len + lead_max + 15u) / 16u;
+    c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks_f + c.group_lanes - 1u) / c.group_lanes));
+    // Rx streams with nt loads; Tx re-writes header lines it has just read and is faster with plain
+    // loads (profiles/r1tc_tx_sweep.jsonl: 0.323 vs 0.356 ms at tile 2).
     const int nt = g_tune_nt.load();
-    c.nt = nt >= 0 ? (nt != 0) : true;
+    c.nt = nt >= 0 ? (nt != 0) : !tx;
     c.grid = g_tune_grid.load();
     const int tile = g_tune_tile.load();
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
@@ -532,12 +550,14 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
     a.n = n_chains;
     a.verify = (op == NETCSUM_OP_DATA_VERIFY) ? 1u : 0u;
     a.out = d_out;
+    // GROUP_LANES 16/32/64: chain_batch_kernel with that many lanes per chain; otherwise (auto) the
+    // wave-per-chain kernel (4 chains per 256-thread block).
     int g = g_tune_group.load();
-    g = (g == 16 || g == 32 || g == 64) ? g : 32;                  // measured best on 45 x 1480 B chains
-    const uint32_t gpb = 256u / (uint32_t)g;
+    g = (g == 16 || g == 32 || g == 64) ? g : 0;
+    const uint32_t gpb = g ? 256u / (uint32_t)g : 4u;
     const uint64_t need = ((uint64_t)n_chains + gpb - 1u) / gpb;
     int grid = g_tune_grid.load();
-    if (grid <= 0) grid = (int)std::min<uint64_t>(need, (uint64_t)cu_count(dev) * 16u);
+    if (grid <= 0) grid = (int)std::min<uint64_t>(need, (uint64_t)cu_count(dev) * (g ? 16u : 64u));
     NC_HIP(netcsum::launch_chain_batch(a, g, grid, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
@@ -615,6 +635,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_TILE:
         if (value < -1 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tile.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_TX_WRITEBACK:
+        if (value < -1 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_tx_wb.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:
         if (value != 0 && value != 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

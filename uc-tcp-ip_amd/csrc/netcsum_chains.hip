@@ -14,10 +14,14 @@
 // whose stream position parity differs from its address parity swaps the two. The result is
 // wrapped to u32 exactly like the reference, then folded.
 //
-// One G-lane group per chain, pieces in order (their stream offsets are a running sum), chunks of a
-// piece spread over the group's lanes. Piece count 0 means pdata_buf == NULL: an odd-length
-// pseudo-header then loses its last octet (net_util.c:1601-1611); pass one zero-length piece for a
-// chain of empty buffers.
+// Two forms. chain_wave_kernel (default): one WAVE per chain, 16 lanes per piece, four pieces of the
+// chain per step, six 16-B chunks per lane per pass (one pass covers a 1480-B fragment at any
+// alignment), two steps in flight — step t+1's loads are issued before step t is reduced. The four
+// piece descriptors of a step are wave-uniform, so they are scalar loads issued a step ahead, and a
+// piece's stream parity (pseudo-header length plus the lengths before it, mod 2) is SALU arithmetic
+// on them. chain_batch_kernel<G> (tuning option): a G-lane group per chain, pieces in order, one load
+// per lane in flight. Piece count 0 means pdata_buf == NULL: an odd-length pseudo-header then loses
+// its last octet (net_util.c:1601-1611); pass one zero-length piece for a chain of empty buffers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -68,6 +72,19 @@ __device__ __forceinline__ uint64_t group_sum64(uint64_t v) {
     return v;
 }
 
+__device__ __forceinline__ void chain_out(const ChainBatchArgs& A, uint32_t ch, uint64_t E, uint64_t O) {
+    uint32_t sum = (uint32_t)((E << 8) + O);                      // the reference's u32 accumulator
+    while (sum >> 16) {
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+    }
+    const uint32_t host = ((sum & 0xFFu) << 8) | (sum >> 8);       // NET_UTIL_NET_TO_HOST_16
+    if (A.verify) {
+        static_cast<uint8_t*>(A.out)[ch] = (host == 0xFFFFu) ? 1u : 0u;
+    } else {
+        static_cast<uint16_t*>(A.out)[ch] = (uint16_t)(~host);
+    }
+}
+
 template <int G>
 __global__ void __launch_bounds__(256) chain_batch_kernel(ChainBatchArgs A) {
     const int lane = (int)(threadIdx.x & (G - 1));
@@ -96,16 +113,158 @@ __global__ void __launch_bounds__(256) chain_batch_kernel(ChainBatchArgs A) {
         E = group_sum64<G>(E);
         O = group_sum64<G>(O);
         if (lane == 0) {
-            uint32_t sum = (uint32_t)((E << 8) + O);              // the reference's u32 accumulator
-            while (sum >> 16) {
-                sum = (sum & 0xFFFFu) + (sum >> 16);
+            chain_out(A, ch, E, O);
+        }
+    }
+}
+
+// ---- chain_wave_kernel ------------------------------------------------------------------------
+constexpr int kWQ = 16;    // lanes per piece (quarter of the wave)
+constexpr int kWK = 6;     // 16-B chunks per lane per pass
+
+typedef const __attribute__((address_space(4))) uint64_t c_u64;    // constant address space:
+typedef const __attribute__((address_space(4))) uint32_t c_u32;    // scalar loads when uniform
+
+struct StepDesc {           // the four pieces of one step (len 0 past the chain's end)
+    uint64_t off[4];
+    uint32_t len[4];
+};
+
+__device__ __forceinline__ StepDesc step_desc(const ChainBatchArgs& A, uint32_t j0, uint32_t p1) {
+    StepDesc d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = j0 + (uint32_t)q;
+        d.off[q] = 0u;
+        d.len[q] = 0u;
+        if (j < p1) {
+            d.off[q] = *reinterpret_cast<c_u64*>(reinterpret_cast<uintptr_t>(A.off + j));
+            const uintptr_t la = reinterpret_cast<uintptr_t>(A.len + j);
+            const uint32_t w = *reinterpret_cast<c_u32*>(la & ~(uintptr_t)3);
+            d.len[q] = (w >> (8u * (uint32_t)(la & 2u))) & 0xFFFFu;
+        }
+    }
+    return d;
+}
+
+__device__ __forceinline__ uint32_t step_odd(const StepDesc& d) {
+    return (d.len[0] ^ d.len[1] ^ d.len[2] ^ d.len[3]) & 1u;
+}
+
+struct WStage {
+    u32x4     v[kWK];
+    uintptr_t a;           // piece start
+    uint32_t  len;
+    uint32_t  swap;        // 1: the piece's stream parity differs from its address parity
+};
+
+// Issue quarter qi's piece of the step described by d; par = stream parity at the step's first piece.
+__device__ __forceinline__ void wave_issue(WStage& st, const StepDesc& d, uint32_t par, uintptr_t base, int qi,
+                                           int ql) {
+    const uint32_t o0 = d.len[0] & 1u, o1 = d.len[1] & 1u, o2 = d.len[2] & 1u;
+    uint64_t off = d.off[0];
+    uint32_t len = d.len[0], pre = 0u;
+    if (qi == 1) { off = d.off[1]; len = d.len[1]; pre = o0; }
+    if (qi == 2) { off = d.off[2]; len = d.len[2]; pre = o0 ^ o1; }
+    if (qi == 3) { off = d.off[3]; len = d.len[3]; pre = o0 ^ o1 ^ o2; }
+    const uintptr_t a = base + off;
+    st.a = a;
+    st.len = len;
+    st.swap = ((uint32_t)(a & 1u)) ^ par ^ pre;
+    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uint32_t nch = len ? (uint32_t)(((a & 15u) + len + 15u) >> 4) : 0u;
+    const uintptr_t z = zero_addr();
+#pragma unroll
+    for (int k = 0; k < kWK; ++k) {
+        const uint32_t c = (uint32_t)(k * kWQ + ql);
+        st.v[k] = load16<true>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z));
+    }
+}
+
+__device__ __forceinline__ void wave_consume(const WStage& st, int ql, uint64_t& E, uint64_t& O) {
+    const uint32_t lead = (uint32_t)(st.a & 15u);
+    const uint32_t rend = lead + st.len;
+    const uint32_t nch = st.len ? (rend + 15u) >> 4 : 0u;
+    EO s{0u, 0u};
+#pragma unroll
+    for (int k = 0; k < kWK; ++k) {
+        // every loaded register consumed on every path (netcsum_device.h, opaque)
+        const uint32_t c = (uint32_t)(k * kWQ + ql);
+        const uint32_t keep = (c < nch) ? 0xFFFFFFFFu : 0u;
+        u32x4 v = opaque(st.v[k]);
+        v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
+        if (c < nch) {
+            v = edge_mask_rel(v, c, lead, rend);
+        }
+        eo_add(v, s);
+    }
+    if (nch > (uint32_t)(kWQ * kWK)) {                            // pieces longer than one pass
+        const uintptr_t q0 = st.a & ~(uintptr_t)15;
+        for (uint32_t c0 = (uint32_t)(kWQ * kWK); c0 < nch; c0 += (uint32_t)(kWQ * kWK)) {
+            u32x4 w[kWK];
+#pragma unroll
+            for (int k = 0; k < kWK; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * kWQ + ql);
+                w[k] = load16<true>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : zero_addr()));
             }
-            const uint32_t host = ((sum & 0xFFu) << 8) | (sum >> 8);   // NET_UTIL_NET_TO_HOST_16
-            if (A.verify) {
-                static_cast<uint8_t*>(A.out)[ch] = (host == 0xFFFFu) ? 1u : 0u;
-            } else {
-                static_cast<uint16_t*>(A.out)[ch] = (uint16_t)(~host);
+#pragma unroll
+            for (int k = 0; k < kWK; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * kWQ + ql);
+                u32x4 v = w[k];
+                if (c < nch) {
+                    v = edge_mask_rel(v, c, lead, rend);
+                }
+                eo_add(v, s);
             }
+        }
+    }
+    if (st.swap) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
+}
+
+__global__ void __launch_bounds__(256) chain_wave_kernel(ChainBatchArgs A) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int ql = lane & (kWQ - 1);
+    const int qi = lane >> 4;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * 4u;
+    const uintptr_t base = (uintptr_t)A.base;
+    for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += nw) {      // wave-uniform
+        const uint32_t p0 = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + ch));
+        const uint32_t p1 = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + ch + 1u));
+        uint64_t E = 0u, O = 0u;
+        uint32_t par = 0u;                                        // stream parity at the next piece
+        if (A.pseudo && A.pseudo_len) {
+            uint32_t plen = A.pseudo_len;
+            if (p0 == p1 && (plen & 1u)) {
+                plen -= 1u;                                       // NULL chain quirk
+            }
+            const uintptr_t pa = (uintptr_t)A.pseudo + (uint64_t)ch * A.pseudo_stride;
+            const EO s = span_eo<64>(pa, plen, lane);
+            if (pa & 1u) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
+            par = A.pseudo_len & 1u;                              // pieces follow ALL pseudo bytes
+        }
+        const uint32_t steps = (p1 - p0 + 3u) >> 2;
+        if (steps != 0u) {
+            WStage S0, S1;
+            StepDesc d = step_desc(A, p0, p1);
+            wave_issue(S0, d, par, base, qi, ql);
+            par ^= step_odd(d);
+            d = step_desc(A, p0 + 4u, p1);
+            for (uint32_t t = 0; t < steps; t += 2u) {
+                wave_issue(S1, d, par, base, qi, ql);             // step t + 1 (empty past the end)
+                par ^= step_odd(d);
+                d = step_desc(A, p0 + 4u * (t + 2u), p1);
+                wave_consume(S0, ql, E, O);                       // step t
+                wave_issue(S0, d, par, base, qi, ql);             // step t + 2
+                par ^= step_odd(d);
+                d = step_desc(A, p0 + 4u * (t + 3u), p1);
+                wave_consume(S1, ql, E, O);                       // step t + 1
+            }
+        }
+        E = group_sum64<64>(E);
+        O = group_sum64<64>(O);
+        if (lane == 0) {
+            chain_out(A, ch, E, O);
         }
     }
 }
@@ -120,8 +279,11 @@ hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipS
     case 32:
         hipLaunchKernelGGL(chain_batch_kernel<32>, dim3(grid), dim3(256), 0, s, a);
         break;
-    default:
+    case 64:
         hipLaunchKernelGGL(chain_batch_kernel<64>, dim3(grid), dim3(256), 0, s, a);
+        break;
+    default:
+        hipLaunchKernelGGL(chain_wave_kernel, dim3(grid), dim3(256), 0, s, a);
         break;
     }
     return hipGetLastError();

@@ -86,7 +86,9 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
 
 // A 16-byte zero chunk inside the code object (one per translation unit): chunk slots past the
 // end of a span load from here, so every load is unconditional and always hits mapped memory.
-static __device__ u32x4 g_zero_chunk[4];
+// 64-B aligned: a frame that starts at the sector below its span (Tx sector write-back) maps the
+// zero chunk to lead 0.
+static __device__ __attribute__((aligned(64))) u32x4 g_zero_chunk[4];
 
 __device__ __forceinline__ uintptr_t zero_addr() {
     return reinterpret_cast<uintptr_t>(&g_zero_chunk[0]);
@@ -101,6 +103,18 @@ __device__ __forceinline__ uint32_t span_chunks(uintptr_t a, uint32_t len) {
 __device__ __forceinline__ u32x4 edge_mask_rel(u32x4 v, uint32_t c, uint32_t lead, uint32_t rend) {
     const uint32_t q = 16u * c;
     const int lo = (c == 0u) ? (int)lead : 0;
+    const int hi = (rend - q < 16u) ? (int)(rend - q) : 16;
+    if (lo != 0 || hi != 16) {
+        v = mask_chunk(v, lo, hi);
+    }
+    return v;
+}
+
+// edge_mask_rel for frames that may start more than 16 B before the span (lead up to 63, Tx sector
+// write-back): chunks wholly before `lead` are zeroed too.
+__device__ __forceinline__ u32x4 frame_mask(u32x4 v, uint32_t c, uint32_t lead, uint32_t rend) {
+    const uint32_t q = 16u * c;
+    const int lo = (lead > q) ? (int)min(lead - q, 16u) : 0;
     const int hi = (rend - q < 16u) ? (int)(rend - q) : 16;
     if (lo != 0 || hi != 16) {
         v = mask_chunk(v, lo, hi);

@@ -50,6 +50,8 @@ struct PktBatchArgs {
     uint8_t*        flags_out;     // NETCSUM_PKT_* per packet (optional for Tx)
     uint32_t        tile;          // segments (packets) per group per block tile (0 = grid-stride)
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
+    uint32_t        wb_sector;     // Tx: 0 = two-byte checksum stores; 32 / 64 = whole aligned sectors
+                                   // (each packet's frame then starts at the sector below it)
 };
 
 struct ChainBatchArgs {

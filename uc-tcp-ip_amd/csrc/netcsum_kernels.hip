@@ -968,8 +968,9 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
         return;
     }
     if (kid == 6) {
-        snprintf(g_last_launch, sizeof(g_last_launch), "seg_stream_kernel<D=%d%s%s> block=256 segs_per_wave=%u",
-                 c.chunks_per_pass, (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "", c.stream_spw);
+        snprintf(g_last_launch, sizeof(g_last_launch), "%s<D=%d%s%s> block=256 segs_per_wave=%u",
+                 a.seg_off ? "seg_stream_varlen_kernel" : "seg_stream_kernel", c.chunks_per_pass,
+                 (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "", c.stream_spw);
         return;
     }
     snprintf(g_last_launch, sizeof(g_last_launch), "%s<G=%d,K=%d%s%s%s> block=%d tile=%d grid=%d P=%d",

@@ -50,12 +50,14 @@ struct PktStage {
     uintptr_t a;         // packet start address
 };
 
+// The packet's frame starts at the 16-B boundary below it (fmask 15), or for Tx sector write-back at
+// the sector boundary below it (fmask 31 / 63); chunk c of the frame is [q0 + 16c, q0 + 16c + 16).
 template <int G, int K, bool NT>
-__device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane) {
+__device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane, uint32_t fmask) {
     st.a = a;
-    st.lead = (uint32_t)(a & 15u);
+    st.lead = (uint32_t)(a & fmask);
     st.avail = avail;
-    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uintptr_t q0 = a - st.lead;
     const uint32_t nch = (avail + st.lead + 15u) >> 4;
     const uintptr_t z = zero_addr();
 #pragma unroll
@@ -204,6 +206,56 @@ __device__ __forceinline__ void store_csum(uintptr_t a, uint32_t off, uint32_t h
     p[1] = (uint8_t)(host_val >> 8);
 }
 
+__device__ __forceinline__ u32x4 patch_byte(u32x4 v, uint32_t pos, uint32_t b) {   // byte pos of a chunk
+    const uint32_t sh = 8u * (pos & 3u);
+    const uint32_t m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
+    const uint32_t d = pos >> 2;
+    v.x = (d == 0u) ? ((v.x & m) | x) : v.x;
+    v.y = (d == 1u) ? ((v.y & m) | x) : v.y;
+    v.z = (d == 2u) ? ((v.z & m) | x) : v.z;
+    v.w = (d == 3u) ? ((v.w & m) | x) : v.w;
+    return v;
+}
+
+// The host-order value `val` memcpy'd to frame bytes f, f+1, where they fall in chunk c.
+__device__ __forceinline__ u32x4 patch_field(u32x4 v, uint32_t c, uint32_t f, uint32_t val) {
+    if ((f >> 4) == c) v = patch_byte(v, f & 15u, val & 0xFFu);
+    if (((f + 1u) >> 4) == c) v = patch_byte(v, (f + 1u) & 15u, val >> 8);
+    return v;
+}
+
+// Whole-sector write-back: the aligned `sec`-byte sectors that hold a checksum byte are rewritten
+// whole from the chunks already in registers (slot k = 0: lane c holds frame chunk c, and the frame
+// starts at the sector boundary below the packet), so HBM sees full-sector writes instead of 2-byte
+// partial ones. The rewritten bytes outside the fields are the values just read (callers own the
+// batch buffer; the host enables this only where no other packet's fields share a sector). Returns
+// false — nothing stored — when a sector would reach past the packet's bytes or past slot 0; the
+// caller then stores the fields two bytes at a time. The decision is uniform over the group.
+template <int G, int K>
+__device__ __forceinline__ bool tx_sector_writeback(const PktStage<K>& st, uint32_t cip, uint32_t cl4, uint32_t l4off,
+                                                    uint32_t sec, int lane) {
+    const uint32_t lead = st.lead;
+    const uint32_t lim = min(lead + st.avail, 16u * (uint32_t)G);
+    const uint32_t sh = (sec == 64u) ? 6u : 5u;
+    const uint32_t fi = lead + 10u;                              // IPv4 header checksum
+    const uint32_t ci0 = (fi >> sh) << (sh - 4u), ci1 = (((fi + 1u) >> sh) + 1u) << (sh - 4u);
+    const bool l4 = cl4 != ~0u;
+    const uint32_t fl = lead + (l4 ? l4off : 10u);
+    const uint32_t cl0 = (fl >> sh) << (sh - 4u), cl1 = (((fl + 1u) >> sh) + 1u) << (sh - 4u);
+    if (16u * max(ci1, cl1) > lim) {
+        return false;
+    }
+    const uint32_t c = (uint32_t)lane;
+    if ((c >= ci0 && c < ci1) || (c >= cl0 && c < cl1)) {
+        u32x4 w = patch_field(st.v[0], c, fi, cip);
+        if (l4) {
+            w = patch_field(w, c, fl, cl4);
+        }
+        *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(st.a - lead + 16u * c) = w;
+    }
+    return true;
+}
+
 template <int G, int K, bool NT, bool TX>
 __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
                                             int lane, int gbase) {
@@ -231,16 +283,17 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
         asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));   // opaque: no branch can skip it
         v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
         if (c < nch) {
-            v = edge_mask_rel(v, c, lead, rend);
+            v = TX ? frame_mask(v, c, lead, rend) : edge_mask_rel(v, c, lead, rend);
         }
         acc = sum4(v, acc);
     }
     uint32_t ip_raw = 0u;
     if ((uint32_t)lane * 16u < lead + p.hlen) {
-        ip_raw = sum4(edge_mask_rel(st.v[0], (uint32_t)lane, lead, lead + p.hlen), 0u);
+        ip_raw = sum4(TX ? frame_mask(st.v[0], (uint32_t)lane, lead, lead + p.hlen)
+                         : edge_mask_rel(st.v[0], (uint32_t)lane, lead, lead + p.hlen), 0u);
     }
     if (nch > (uint32_t)(G * K)) {                               // packets longer than one pass
-        const uintptr_t q0 = st.a & ~(uintptr_t)15;
+        const uintptr_t q0 = st.a - lead;
         for (uint32_t c0 = (uint32_t)(G * K); c0 < nch; c0 += (uint32_t)(G * K)) {
             u32x4 w[K];
 #pragma unroll
@@ -275,28 +328,46 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
     }
     sip = fold16(group_sum<G>(sip));
     sl4 = fold16(group_sum<G>(sl4) + p.pseudo_le);
-    if (lane != 0 || !valid) {                                   // a dummy stage stores nothing
+    if (!valid) {                                                // a dummy stage stores nothing
         return;
     }
     uint32_t f = p.flags;
-    if (!(f & F_MALFORMED)) {
-        if (!TX) {
+    if constexpr (TX) {
+        uint32_t cip = ~0u, cl4 = ~0u;                           // values to store; ~0u = none
+        if (!(f & F_MALFORMED)) {
+            cip = (~sip) & 0xFFFFu;                              // net_ipv4.c:9578-9586
+            f |= F_IP_OK;
+            if (p.check_l4) {
+                cl4 = (~sl4) & 0xFFFFu;
+                if (p.proto == 17u && cl4 == 0u) {
+                    cl4 = 0xFFFFu;                               // RFC 768 (net_udp.c:2929-2931)
+                }
+                f |= F_L4_CHECKED | F_L4_OK;
+            } else if ((f & F_UDP_NO_CSUM) && p.l4_csum_off != ~0u) {
+                cl4 = 0u;                                        // no UDP checksum (net_udp.c:2935)
+            }
+        }
+        bool two_byte = cip != ~0u;
+        if (two_byte && A.wb_sector != 0u) {
+            two_byte = !tx_sector_writeback<G, K>(st, cip, cl4, p.l4_csum_off, A.wb_sector, lane);
+        }
+        if (lane != 0) {
+            return;
+        }
+        if (two_byte) {
+            store_csum<G>(st.a, 10u, cip);
+            if (cl4 != ~0u) {
+                store_csum<G>(st.a, p.l4_csum_off, cl4);
+            }
+        }
+    } else {
+        if (lane != 0) {
+            return;
+        }
+        if (!(f & F_MALFORMED)) {
             f |= (sip == 0xFFFFu) ? F_IP_OK : 0u;
             if (p.check_l4) {
                 f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
-            }
-        } else {
-            store_csum<G>(st.a, 10u, (~sip) & 0xFFFFu);
-            f |= F_IP_OK;
-            if (p.check_l4) {
-                uint32_t c = (~sl4) & 0xFFFFu;
-                if (p.proto == 17u && c == 0u) {
-                    c = 0xFFFFu;                                 // RFC 768 (net_udp.c:2929-2931)
-                }
-                store_csum<G>(st.a, p.l4_csum_off, c);
-                f |= F_L4_CHECKED | F_L4_OK;
-            } else if ((f & F_UDP_NO_CSUM) && p.l4_csum_off != ~0u) {
-                store_csum<G>(st.a, p.l4_csum_off, 0u);
             }
         }
     }
@@ -317,8 +388,10 @@ __device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint
     }
 }
 
+// 4 waves per SIMD: the Tx instantiations otherwise take 131 VGPRs (3 waves), 25 % less memory
+// parallelism than Rx (122 VGPRs); capped at 128 they do not spill (profiles/r1txp_pmc.json).
 template <int G, int K, bool VARLEN, bool NT, bool TX>
-__global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pkt_batch_kernel(PktBatchArgs A) {
     static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
     const int lane = (int)(threadIdx.x & (G - 1));
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
@@ -342,24 +415,25 @@ __global__ void __launch_bounds__(256) pkt_batch_kernel(PktBatchArgs A) {
     }
     const uintptr_t base = (uintptr_t)A.base;
     const uintptr_t z = zero_addr();
+    const uint32_t fmask = (TX && A.wb_sector != 0u) ? A.wb_sector - 1u : 15u;
     PktStage<K> S0, S1;
     uint64_t off;
     uint32_t avail;
     uint32_t i = first;
     bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
-    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane, fmask);
     for (uint32_t j = 0u; j < iters; j += 2u) {                  // one scalar exit (see seg_pipe_kernel)
         uint32_t nx = i + step;
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
+        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane, fmask);
         pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane, fmask);
         pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
         i = nx;
     }

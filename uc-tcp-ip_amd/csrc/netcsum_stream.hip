@@ -11,15 +11,14 @@
 // (O = 128-B line below the first segment), lane l holds its 16 B at O + 1024*q + 16*l — every
 // wave-instruction is 8 whole, aligned cache lines and every byte of the run is fetched once.
 // Segment boundaries are wave-uniform scalar events: while consuming piece q the wave walks (on
-// the SALU) the segments that END inside it; for each, every lane adds the bytes of that segment
-// in its chunk to its running partial, the 64 partials are reduced with four DPP row shifts and
-// four v_readlane, and lane 0 writes the folded result to a per-wave LDS result array, flushed to
-// HBM with coalesced stores when the run is done.
+// the SALU) the segments that END inside it; for each, every lane takes the bytes of that segment
+// in its chunk (a VALU prefix mask), the 64 shares are reduced with four DPP row shifts and four
+// v_readlane, and the scalar epilogue (fold, parity rotation, + the pseudo-header sum, complement)
+// leaves the result in lane k % 64 of two VGPRs, stored with one coalesced store per run.
 //
-// Pseudo-headers (12 B for IPv4 TCP/UDP, net_tcp.h:1545-1551) ride in the same pipeline: when
-// piece q is issued, the scalar issue cursor finds the segments that end in piece q and their
-// pseudo-headers (contiguous in the pseudo array) are fetched as 16-B chunks by the first lanes,
-// so they are in registers when the events of piece q are consumed.
+// Pseudo-headers (12 B for IPv4 TCP/UDP, net_tcp.h:1545-1551) are summed in a per-run prologue
+// (lane k = segment k, 16-B-aligned chunks, all loads issued together) while the run's first
+// pieces are in flight.
 //
 // Loads are raw buffer loads (V# over the wave's byte run, voffset = 1024*q + 16*lane): the
 // hardware range check returns zeros past the run, so the pipeline's dummy pieces and unused pseudo
@@ -91,8 +90,8 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-constexpr uint32_t kMaxRun = 128u;
-constexpr uint64_t kMaxGap = 64u;      // varlen runs stream across gaps of up to this many bytes     // segments per wave run: results live in two VGPRs (lane = k % 64)
+constexpr uint32_t kMaxRun = 128u;     // segments per wave run: results live in two VGPRs (lane = k % 64)
+constexpr uint64_t kMaxGap = 64u;      // varlen runs stream across gaps of up to this many bytes
 
 // Pseudo-header sums of run segments [s_begin, s_begin + nres): lane k % 64 of ps0 (k < 64) / ps1
 // holds segment k's pseudo-header sum, folded, in its own stream frame, from the 16-B-aligned chunks

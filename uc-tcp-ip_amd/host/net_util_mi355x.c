@@ -39,6 +39,7 @@
 #endif
 
 #include <stddef.h>
+#include <stdio.h>
 
 #define NC_NEG_ZERO   0xFFFFu              /* NET_UTIL_16_BIT_ONES_CPL_NEG_ZERO (net_util.c:56) */
 #define NC_MAX_SPANS  64u                  /* pseudo-header + up to 63 chained buffers per call */
@@ -223,4 +224,30 @@ CPU_BOOLEAN NetUtil_16BitOnesCplChkSumDataVerify(void *pdata_buf, void *ppseudo_
     }
     *p_err = NET_UTIL_ERR_NONE;
     return (NC_NET_TO_HOST_16(nc_fold(sum32)) == NC_NEG_ZERO) ? DEF_OK : DEF_FAIL;
+}
+
+/* The reference's optional native-inner-loop seam (Source/net_util.h:486-490, declared when
+ * NET_CFG_OPTIMIZE_ASM_EN is enabled; ports Ports/<cpu>/<compiler>/net_util_a.*): the unfolded sum
+ * of the network-order 16-bit words of a 4-byte-aligned region of `size` bytes (a multiple of 4),
+ * which NetUtil_16BitSumDataCalc adds to its accumulator (net_util.c:1407-1415). Summed on the GPU
+ * (exact, mod 2^32 — sizes passed by the reference are < 2^16, so the sum is exact). The reference
+ * signature has no error channel: a device failure returns 0 and is reported on stderr (there is no
+ * CPU path). */
+CPU_INT32U NetUtil_16BitSumDataCalcAlign_32(void *pdata_32, CPU_INT32U size)
+{
+    NETCSUM_SPAN span;
+    uint32_t sum32 = 0u;
+    NET_ERR err;
+    if (size == 0u) {
+        return 0u;
+    }
+    span.p = pdata_32;
+    span.len = size;
+    span.rsvd = 0u;
+    err = NetUtil_MI355X_StreamSum32(&span, 1u, &sum32);
+    if (err != NET_UTIL_ERR_NONE) {
+        fprintf(stderr, "[netcsum-mi355x] NetUtil_16BitSumDataCalcAlign_32: NET_ERR %d, returning 0\n", (int)err);
+        return 0u;
+    }
+    return (CPU_INT32U)sum32;
 }

@@ -50,6 +50,7 @@ PKT_IP_OK, PKT_L4_OK, PKT_L4_CHECKED, PKT_UDP_NO_CSUM = 0x01, 0x02, 0x04, 0x08
 PKT_MALFORMED, PKT_FRAGMENT, PKT_L4_MALFORMED = 0x10, 0x20, 0x40
 TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
 TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
+TUNE_TX_WRITEBACK = 10
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
@@ -180,6 +181,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ChkSumBatchChains.restype = i32
     L.NetUtil_MI355X_ChkSumBatchStridedHost.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, u32]
     L.NetUtil_MI355X_ChkSumBatchStridedHost.restype = i32
+    L.NetUtil_16BitSumDataCalcAlign_32.argtypes = [vp, u32]
+    L.NetUtil_16BitSumDataCalcAlign_32.restype = u32
     L.NetUtil_MI355X_StreamSum32.argtypes = [ctypes.POINTER(Span), u32, ctypes.POINTER(ctypes.c_uint32)]
     L.NetUtil_MI355X_StreamSum32.restype = i32
     L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
@@ -270,6 +273,11 @@ def DataVerify(pdata_buf, ppseudo_hdr, pseudo_hdr_size):
     v = lib().NetUtil_16BitOnesCplChkSumDataVerify(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size,
                                                    ctypes.byref(err))
     return int(v), int(err.value)
+
+
+def SumDataCalcAlign_32(pdata_32, size):
+    """NetUtil_16BitSumDataCalcAlign_32 (net_util.h:486-490): unfolded network-order word sum."""
+    return int(lib().NetUtil_16BitSumDataCalcAlign_32(_p(pdata_32), size))
 
 
 def chain_to_spans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, dbg=False, max_spans=64):
