@@ -28,36 +28,58 @@ def build() -> str:
     return _LIB_PATH
 
 
+def build_native(out_dir: str, cc: str = "gcc") -> str:
+    """The same C restatement built for THIS host's CPU (-O3 -march=native): bench.py's "best CPU"
+    line. Built where it runs (the GPU box's host), never shipped."""
+    out = os.path.join(out_dir, "liboracle_netutil_native.so")
+    subprocess.run([cc, "-O3", "-march=native", "-std=gnu11", "-fPIC", "-fopenmp", "-shared", "-o", out,
+                    os.path.join(_HERE, "net_util_oracle.c")], check=True, timeout=120)
+    return out
+
+
+def batch_strided_with(path: str, seg: np.ndarray, seg_stride: int, seg_len: int, pseudo, pseudo_stride: int,
+                       pseudo_len: int, n_seg: int, op: int = OP_DATA_CALC, n_threads: int = 1) -> np.ndarray:
+    """batch_strided through another build of the restatement (build_native)."""
+    L = _bind(ctypes.CDLL(path))
+    out = _out_array(n_seg, op)
+    L.Oracle_BatchStrided(seg.ctypes.data, seg_stride, seg_len, _ptr(pseudo), pseudo_stride, pseudo_len,
+                          n_seg, out.ctypes.data, op, n_threads)
+    return out
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
-        vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
-        pu32 = ctypes.POINTER(ctypes.c_uint32)
-        L.Oracle_HdrCalc.argtypes = [vp, u16, pu32, i32]
-        L.Oracle_HdrCalc.restype = u16
-        L.Oracle_HdrVerify.argtypes = [vp, u16, pu32, i32]
-        L.Oracle_HdrVerify.restype = ctypes.c_uint8
-        L.Oracle_DataCalc.argtypes = [vp, vp, u16, pu32, i32]
-        L.Oracle_DataCalc.restype = u16
-        L.Oracle_DataVerify.argtypes = [vp, vp, u16, pu32, i32]
-        L.Oracle_DataVerify.restype = ctypes.c_uint8
-        L.Oracle_DataSum32.argtypes = [vp, vp, u16, pu32]
-        L.Oracle_DataSum32.restype = u32
-        L.Oracle_BatchStrided.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, i32]
-        L.Oracle_BatchStrided.restype = None
-        L.Oracle_BatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
-        L.Oracle_BatchVarLen.restype = None
-        L.Oracle_BatchChains.argtypes = [vp, vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
-        L.Oracle_BatchChains.restype = None
-        L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
-        L.Oracle_Fill.restype = None
-        L.Oracle_MaxThreads.argtypes = []
-        L.Oracle_MaxThreads.restype = i32
-        _lib = L
+        _lib = _bind(ctypes.CDLL(_LIB_PATH))
     return _lib
+
+
+def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
+    vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    pu32 = ctypes.POINTER(ctypes.c_uint32)
+    L.Oracle_HdrCalc.argtypes = [vp, u16, pu32, i32]
+    L.Oracle_HdrCalc.restype = u16
+    L.Oracle_HdrVerify.argtypes = [vp, u16, pu32, i32]
+    L.Oracle_HdrVerify.restype = ctypes.c_uint8
+    L.Oracle_DataCalc.argtypes = [vp, vp, u16, pu32, i32]
+    L.Oracle_DataCalc.restype = u16
+    L.Oracle_DataVerify.argtypes = [vp, vp, u16, pu32, i32]
+    L.Oracle_DataVerify.restype = ctypes.c_uint8
+    L.Oracle_DataSum32.argtypes = [vp, vp, u16, pu32]
+    L.Oracle_DataSum32.restype = u32
+    L.Oracle_BatchStrided.argtypes = [vp, u64, u16, vp, u32, u16, u32, vp, i32, i32]
+    L.Oracle_BatchStrided.restype = None
+    L.Oracle_BatchVarLen.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
+    L.Oracle_BatchVarLen.restype = None
+    L.Oracle_BatchChains.argtypes = [vp, vp, vp, vp, vp, u32, u16, u32, vp, i32, i32]
+    L.Oracle_BatchChains.restype = None
+    L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
+    L.Oracle_Fill.restype = None
+    L.Oracle_MaxThreads.argtypes = []
+    L.Oracle_MaxThreads.restype = i32
+    return L
 
 
 def _ptr(a):
