@@ -466,7 +466,7 @@ def test_stream_varlen_layouts_vs_oracle(layout):
                 out = _out(n, op)
                 netcsum.batch_varlen(base_d, off_d, len_d, ph_d if plen else None, pstride, plen, n, out, op)
                 torch.cuda.synchronize()
-                assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
+                assert netcsum.last_launch().startswith("seg_stream_varlen_kernel"), netcsum.last_launch()
                 want = oracle.batch_varlen(base, off, lens, ph if plen else None, pstride, plen, op)
                 assert np.array_equal(_np_out(out), want), (layout, plen, run, chunks, op)
 
