@@ -106,7 +106,7 @@ def test_tx_finalize_writes_reference_checksums_then_rx_accepts(udp_tx_csum):
 
 
 @pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (2048, 1514), (200, 184), (192, 48)])
-@pytest.mark.parametrize("wb", [-1, 0, 1, 2])
+@pytest.mark.parametrize("wb", [-1, 0, 1, 2, 3])
 def test_tx_finalize_strided_writeback_modes(stride, pkt_len, wb):
     """Strided Tx finalize under every write-back form (TUNE_TX_WRITEBACK: 0 two-byte stores, 1 / 2
     whole 32 / 64-B sectors): packets finalized exactly as the packet oracle does, and every byte

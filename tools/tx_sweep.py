@@ -45,9 +45,16 @@ def main():
     ms_rx = events_ms(lambda: netcsum.rx_validate_ipv4(want, n, flags, stride=L, pkt_len=L, stream=st), st, reps=40)
     print(json.dumps({"variant": "rx_fused", "ms_med": round(ms_rx, 4),
                       "GBps_med": round(n * L / ms_rx / 1e6, 1), "oracle_sample_ok": oracle_ok}), flush=True)
-    for wb in (0, 1, 2):
-        for nt in (1, 0):
-            for tile in (1, 2, 4):
+    groups = [int(g) for g in os.environ.get("TX_SWEEP_GROUPS", "0").split(",")]
+    wbs = [int(w) for w in os.environ.get("TX_SWEEP_WB", "0,1,2,3").split(",")]
+    for g in groups:
+        netcsum.tune(netcsum.TUNE_GROUP_LANES, g)
+        if g:
+            ms_g = events_ms(lambda: netcsum.rx_validate_ipv4(want, n, flags, stride=L, pkt_len=L, stream=st), st,
+                             reps=40)
+            print(json.dumps({"variant": {"rx_group": g}, "ms_med": round(ms_g, 4),
+                              "GBps_med": round(n * L / ms_g / 1e6, 1)}), flush=True)
+        for wb, nt, tile in [(w, t, j) for w in wbs for t in (1, 0) for j in (1, 2, 4)]:
                 netcsum.tune(netcsum.TUNE_TX_WRITEBACK, wb)
                 netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
                 netcsum.tune(netcsum.TUNE_TILE, tile)
@@ -57,10 +64,11 @@ def main():
                 same = bool(torch.equal(pk, want))
                 ms = events_ms(lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st), st,
                                reps=40)
-                print(json.dumps({"variant": {"wb": wb, "nt": nt, "tile": tile}, "ms_med": round(ms, 4),
+                print(json.dumps({"variant": {"group": g, "wb": wb, "nt": nt, "tile": tile}, "ms_med": round(ms, 4),
                                   "GBps_med": round(n * (L + 4) / ms / 1e6, 1), "same_as_two_byte": same}),
                       flush=True)
-    for k, val in ((netcsum.TUNE_TX_WRITEBACK, -1), (netcsum.TUNE_NT_LOADS, -1), (netcsum.TUNE_TILE, -1)):
+    for k, val in ((netcsum.TUNE_TX_WRITEBACK, -1), (netcsum.TUNE_NT_LOADS, -1), (netcsum.TUNE_TILE, -1),
+                   (netcsum.TUNE_GROUP_LANES, 0)):
         netcsum.tune(k, val)
 
 

@@ -500,12 +500,14 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         g = d_off ? 32 : std::max(8, pow2_group((chunks + 5u) / 6u));
     }
     c.group_lanes = pow2_group((uint32_t)g);
+    bool two_phase = false;
     if (tx) {
         // Whole-sector write-back (PktBatchArgs::wb_sector): strided batches only, packets at least
         // 192 B apart (no two packets' checksum fields share a sector: fields lie within the first
         // 78 B), a sector-aligned base (no frame starts before the buffer), >= 16 lanes per packet
         // (header fields within the frame's first 16*G bytes).
         const int wb = g_tune_tx_wb.load();
+        two_phase = wb == 3;
         const uint32_t sec = wb == 1 ? 32u : (wb == 2 ? 64u : (wb < 0 ? kTxSectorAuto : 0u));
         if (sec != 0u && d_off == nullptr && stride >= 192u && ((uintptr_t)d_base % sec) == 0u &&
             c.group_lanes >= 16) {
@@ -522,6 +524,18 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     c.grid = g_tune_grid.load();
     const int tile = g_tune_tile.load();
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
+    if (two_phase) {
+        // Two-phase Tx: the fused kernel records each packet's checksums densely (8 B), a second
+        // kernel scatters them into the headers; the record buffer is stream-ordered.
+        hipStream_t st = static_cast<hipStream_t>(hip_stream);
+        void* rec = nullptr;
+        NC_HIP(hipMallocAsync(&rec, (size_t)n_pkt * 8u, st));
+        a.tx_rec = static_cast<uint2*>(rec);
+        NC_HIP(netcsum::launch_pkt_batch(a, c, tx, st));
+        NC_HIP(netcsum::launch_tx_scatter(a, st));
+        NC_HIP(hipFreeAsync(rec, st));
+        return NET_UTIL_ERR_NONE;
+    }
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
@@ -637,7 +651,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_tile.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_TX_WRITEBACK:
-        if (value < -1 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tx_wb.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:

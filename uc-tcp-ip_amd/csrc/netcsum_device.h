@@ -110,16 +110,17 @@ __device__ __forceinline__ u32x4 edge_mask_rel(u32x4 v, uint32_t c, uint32_t lea
     return v;
 }
 
-// edge_mask_rel for frames that may start more than 16 B before the span (lead up to 63, Tx sector
-// write-back): chunks wholly before `lead` are zeroed too.
-__device__ __forceinline__ u32x4 frame_mask(u32x4 v, uint32_t c, uint32_t lead, uint32_t rend) {
-    const uint32_t q = 16u * c;
-    const int lo = (lead > q) ? (int)min(lead - q, 16u) : 0;
-    const int hi = (rend - q < 16u) ? (int)(rend - q) : 16;
-    if (lo != 0 || hi != 16) {
-        v = mask_chunk(v, lo, hi);
+// Sum of bytes [0, m) of this lane's chunk; m per lane, clamped to [0, 16] (VALU only, no scalar mask work).
+__device__ __forceinline__ uint32_t low_bytes(u32x4 v, int m) {
+    uint32_t acc = 0u;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = min(max(m - 4 * i, 0), 4);
+        const uint32_t mask = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+        acc = __builtin_amdgcn_sad_u16(d[i] & mask, 0u, acc);
     }
-    return v;
+    return acc;
 }
 
 template <int N>

@@ -90,14 +90,14 @@ __device__ __forceinline__ uint32_t be16_at(uint32_t dw, int byte) {   // bytes 
     return (((dw >> (8 * byte)) & 0xFFu) << 8) | ((dw >> (8 * byte + 8)) & 0xFFu);
 }
 
-// What the little-endian word w at even packet offset h adds to this lane's unfolded v_sad_u16
-// accumulator (the lane whose k = 0 chunk holds the byte; byte at frame position f weighs 2^(8(f&1))).
-__device__ __forceinline__ uint32_t hole_share(uint32_t w, uint32_t lead, uint32_t h, int lane) {
-    const uint32_t f0 = lead + h, f1 = f0 + 1u;
-    uint32_t r = 0u;
-    r += ((uint32_t)lane == (f0 >> 4)) ? ((w & 0xFFu) << (8u * (f0 & 1u))) : 0u;
-    r += ((uint32_t)lane == (f1 >> 4)) ? ((w >> 8) << (8u * (f1 & 1u))) : 0u;
-    return r;
+// What frame byte f adds to this lane's unfolded v_sad_u16 accumulator, read from the lane's OWN
+// k = 0 chunk (0 unless the lane holds the byte; weight 2^(8(f&1)) in the absolute LE frame). Tx
+// checksum fields count as zero: their bytes are subtracted where they were summed, with no
+// cross-lane traffic (the transport field's offset depends on the IP header length, so a shuffle
+// would add a dependent LDS round trip per packet).
+__device__ __forceinline__ uint32_t own_byte(u32x4 v0, uint32_t f, int lane) {
+    const uint32_t b = (pick4(v0, (f >> 2) & 3u) >> (8u * (f & 3u))) & 0xFFu;
+    return ((uint32_t)lane == (f >> 4)) ? (b << (8u * (f & 1u))) : 0u;
 }
 
 struct PktInfo {
@@ -107,8 +107,6 @@ struct PktInfo {
     uint32_t l4_csum_off;  // packet offset of the transport checksum field (~0u: none)
     uint32_t pseudo_le;    // little-endian word sum of the pseudo-header (0: none)
     uint32_t proto;
-    uint32_t hole_ip;      // TX: little-endian word of the IP checksum field (bytes 10, 11)
-    uint32_t hole_l4;      // TX: little-endian word of the transport checksum field
     bool     check_l4;
 };
 
@@ -126,7 +124,6 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
     const uint32_t tot = be16_at(d0, 2);
     const uint32_t frag = be16_at(d1, 2) & 0x3FFFu;              // MF | fragment offset
     p.proto = (d2 >> 8) & 0xFFu;
-    p.hole_ip = d2 >> 16;
     if (avail < 20u || ver != 4u || p.hlen < 20u || tot < p.hlen || tot > avail) {
         p.flags = F_MALFORMED;
         p.l4_end = 0u;
@@ -148,9 +145,6 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
         }
         p.check_l4 = true;
         p.l4_csum_off = p.hlen + 16u;
-        if (TX) {
-            p.hole_l4 = pkt_dword(v0, lead, p.hlen + 16u, gbase) & 0xFFFFu;
-        }
         p.pseudo_le = src_dst + (6u << 8) + (((l4len & 0xFFu) << 8) | (l4len >> 8));
         break;
     case 17u: {                                                  // UDP
@@ -175,7 +169,6 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
             return p;
         }
         p.check_l4 = true;
-        p.hole_l4 = du >> 16;
         p.pseudo_le = src_dst + (17u << 8) + (((udp_len & 0xFFu) << 8) | (udp_len >> 8));
         break;
     }
@@ -187,9 +180,6 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
         }
         p.check_l4 = true;
         p.l4_csum_off = p.hlen + 2u;
-        if (TX) {
-            p.hole_l4 = pkt_dword(v0, lead, p.hlen, gbase) >> 16;
-        }
         break;
     default:
         break;
@@ -259,39 +249,42 @@ __device__ __forceinline__ bool tx_sector_writeback(const PktStage<K>& st, uint3
 template <int G, int K, bool NT, bool TX>
 __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
                                             int lane, int gbase) {
-    // One masked sum over [0, end) per chunk (end = transport end, or the IP header end when the
-    // transport part is not checked), plus the IP header alone from the k = 0 chunks (hlen <= 60 <
-    // 16*G - 15). Both are exact integer sums of the same frame half-words, so the transport part
-    // is their difference — exact, hence still zero iff all its bytes are zero (the reference's
-    // all-zero -> 0 / 0xFFFF distinction). TX checksum fields count as zero: their bytes are
-    // subtracted from the owning lane's sums.
+    // One sum over [lead, lead + end) (end = transport end, or the IP header end when the transport
+    // part is not checked), plus the IP header alone from the k = 0 chunks (lead + hlen < 16*G).
+    // Both are exact integer sums of the same frame half-words, so the transport part is their
+    // difference — exact, hence still zero iff all its bytes are zero (the reference's all-zero ->
+    // 0 / 0xFFFF distinction). TX checksum fields count as zero: their bytes are subtracted from
+    // the owning lane's sums.
+    //
+    // The chunks are summed UNMASKED (chunks past `end` dropped by a select on their sum); the bytes
+    // of the frame before the packet and those past `end` in the last chunk are subtracted once per
+    // lane afterwards (low_bytes), instead of masking every chunk: the packet kernels are VALU-issue
+    // bound (profiles/r1txp_pmc.json), and per-chunk edge masks executed on every k slot dominated.
     const uint32_t lead = st.lead;
     PktInfo p = pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
     const uint32_t nch = (rend + 15u) >> 4;
+    const uint32_t cl = nch - 1u;                                // chunk holding byte rend - 1 (~0u: none)
     uint32_t acc = 0u;
+    u32x4 vl = u32x4{0u, 0u, 0u, 0u};                            // that chunk, on the lane holding it
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        // Every loaded register is consumed on every path (chunks past the range are zeroed by a
-        // select, not skipped by a branch; the empty asm keeps the optimiser from sinking the use
-        // into one): a load left unconsumed on some path stays "pending" across the loop back-edge
-        // and the compiler drains vmcnt(0) before re-issuing the stage.
+        // Every loaded register is consumed on every path (no branch: a load left unconsumed on some
+        // path stays "pending" across the loop back-edge and the compiler drains vmcnt(0) there).
         const uint32_t c = (uint32_t)(k * G + lane);
-        const uint32_t keep = (c < nch) ? 0xFFFFFFFFu : 0u;
-        u32x4 v = st.v[k];
-        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));   // opaque: no branch can skip it
-        v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
-        if (c < nch) {
-            v = TX ? frame_mask(v, c, lead, rend) : edge_mask_rel(v, c, lead, rend);
-        }
-        acc = sum4(v, acc);
+        const u32x4 v = st.v[k];
+        const uint32_t sv = sum4(v, 0u);
+        acc += (c < nch) ? sv : 0u;
+        vl.x = (c == cl) ? v.x : vl.x;
+        vl.y = (c == cl) ? v.y : vl.y;
+        vl.z = (c == cl) ? v.z : vl.z;
+        vl.w = (c == cl) ? v.w : vl.w;
     }
-    uint32_t ip_raw = 0u;
-    if ((uint32_t)lane * 16u < lead + p.hlen) {
-        ip_raw = sum4(TX ? frame_mask(st.v[0], (uint32_t)lane, lead, lead + p.hlen)
-                         : edge_mask_rel(st.v[0], (uint32_t)lane, lead, lead + p.hlen), 0u);
-    }
+    const int l16 = 16 * lane;
+    const uint32_t pre = low_bytes(st.v[0], (int)lead - l16);   // frame bytes before the packet
+    acc -= pre + (sum4(vl, 0u) - low_bytes(vl, (int)(rend - 16u * cl)));
+    const uint32_t ip_raw = low_bytes(st.v[0], (int)(lead + p.hlen) - l16) - pre;
     if (nch > (uint32_t)(G * K)) {                               // packets longer than one pass
         const uintptr_t q0 = st.a - lead;
         for (uint32_t c0 = (uint32_t)(G * K); c0 < nch; c0 += (uint32_t)(G * K)) {
@@ -315,10 +308,11 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
     uint32_t acc_ip = ip_raw, acc_l4 = acc - ip_raw;
     if (TX) {
         if (!(p.flags & F_MALFORMED)) {
-            acc_ip -= hole_share(p.hole_ip, lead, 10u, lane);
+            acc_ip -= own_byte(st.v[0], lead + 10u, lane) + own_byte(st.v[0], lead + 11u, lane);
         }
         if (p.check_l4) {
-            acc_l4 -= hole_share(p.hole_l4, lead, p.l4_csum_off, lane);
+            const uint32_t f = lead + p.l4_csum_off;
+            acc_l4 -= own_byte(st.v[0], f, lane) + own_byte(st.v[0], f + 1u, lane);
         }
     }
     uint32_t sip = fold16(acc_ip), sl4 = fold16(acc_l4);
@@ -348,7 +342,14 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
             }
         }
         bool two_byte = cip != ~0u;
-        if (two_byte && A.wb_sector != 0u) {
+        if (A.tx_rec != nullptr) {                               // two-phase: record, scatter later
+            if (lane == 0) {
+                A.tx_rec[idx] = make_uint2((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16),
+                                           (p.l4_csum_off & 0xFFFFu) | (cip != ~0u ? 0x10000u : 0u) |
+                                               (cl4 != ~0u ? 0x20000u : 0u));
+            }
+            two_byte = false;
+        } else if (two_byte && A.wb_sector != 0u) {
             two_byte = !tx_sector_writeback<G, K>(st, cip, cl4, p.l4_csum_off, A.wb_sector, lane);
         }
         if (lane != 0) {
@@ -470,7 +471,29 @@ hipError_t launch_pkt_v(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s
     }
 }
 
+// Phase 2 of the two-phase Tx finalize: one thread per packet stores the checksums recorded by
+// phase 1 (x: IP | transport << 16; y: transport field offset | has-IP << 16 | has-transport << 17).
+__global__ void __launch_bounds__(256) tx_scatter_kernel(PktBatchArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.n) {
+        return;
+    }
+    const uint2 r = A.tx_rec[i];
+    const uintptr_t a = (uintptr_t)A.base + (A.off ? A.off[i] : (uint64_t)i * A.stride);
+    if (r.y & 0x10000u) {
+        store_csum<1>(a, 10u, r.x & 0xFFFFu);
+    }
+    if (r.y & 0x20000u) {
+        store_csum<1>(a, r.y & 0xFFFFu, r.x >> 16);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_tx_scatter(const PktBatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(tx_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
     if (a.off) {

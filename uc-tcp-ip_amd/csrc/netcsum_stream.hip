@@ -59,19 +59,6 @@ __device__ __forceinline__ u32x4 opaque_tuple(u32x4 v) {
     return v;
 }
 
-// Sum of bytes [0, m) of this lane's chunk, m per lane in [0, 16] (VALU only: no scalar mask work).
-__device__ __forceinline__ uint32_t low_bytes(u32x4 v, int m) {
-    uint32_t acc = 0u;
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int k = min(max(m - 4 * i, 0), 4);
-        const uint32_t mask = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
-        acc = __builtin_amdgcn_sad_u16(d[i] & mask, 0u, acc);
-    }
-    return acc;
-}
-
 // This lane's share of the bytes of a 1-KiB piece that lie below piece offset x (wave-uniform,
 // 0..1024): its whole chunk if the chunk ends at or below x, the low (x - 16*lane) bytes if x falls
 // inside it, nothing above. A span [xs, xe) of the piece is prefix(xe) - prefix(xs), exactly.
