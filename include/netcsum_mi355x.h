@@ -295,7 +295,9 @@ typedef enum netcsum_tune_key {
                                          byte stores, 1 / 2 rewrite the whole aligned 32 / 64-B
                                          sectors holding the fields (strided batches with stride
                                          >= 192 B, sector-aligned d_base, >= 16 lanes per packet;
-                                         elsewhere two-byte stores)                                 */
+                                         elsewhere two-byte stores), 3 two-phase (checksums recorded
+                                         densely, then scattered by a second kernel; stream-ordered
+                                         scratch of 8 B per packet)                                 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);
