@@ -330,7 +330,8 @@ def test_small_aligned_kernel_vs_oracle(L):
             for base_off in (0, 4):
                 for kernel, tile, grid, chunks in ((0, -1, 0, 0), (5, 0, 1, 0), (5, 0, 3, 0), (5, 1, 0, 0),
                                                    (5, 7, 0, 0), (5, 2, 3, 0), (7, -1, 0, 0), (7, -1, 1, 2),
-                                                   (7, -1, 3, 3), (7, -1, 2, 4)):
+                                                   (7, -1, 3, 3), (7, -1, 2, 4), (7, 1, 0, 0), (7, 1, 3, 4),
+                                                   (7, 4, 0, 2), (7, 4, 2, 3), (7, 2, 5, 3)):
                     netcsum.tune(netcsum.TUNE_KERNEL, kernel)
                     netcsum.tune(netcsum.TUNE_TILE, tile)
                     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)

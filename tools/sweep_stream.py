@@ -84,11 +84,13 @@ def sweep_c3(rounds, dev, st):
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
     nb = nh * 20 // 16 * 16
     variants = [("read", dict(grid=8192, nt=1, probe=1)), ("c3", dict(kernel=5))]
-    c3spec = os.environ.get("SWEEP_C3_SPEC", "2,3,4:1,2,4")
-    c3k, c3m = ([int(x) for x in part.split(",")] for part in c3spec.split(":"))
-    for k in c3k:
-        for mult in c3m:
-            variants.append(("c3", dict(kernel=7, k=k, mult=mult)))
+    c3spec = os.environ.get("SWEEP_C3_SPEC", "2,3,4:1,2,4:-1")     # stages : grid mults : headers per lane
+    parts = c3spec.split(":") + ["-1"] * (3 - len(c3spec.split(":")))
+    c3k, c3m, c3h = ([int(x) for x in part.split(",")] for part in parts)
+    for h in c3h:
+        for k in c3k:
+            for mult in c3m:
+                variants.append(("c3", dict(kernel=7, k=k, mult=mult, tile=h)))
     res, ref = {}, None
     for r in range(rounds):
         for kind, kw in variants:

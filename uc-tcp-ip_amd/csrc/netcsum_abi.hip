@@ -149,18 +149,21 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
     }
     if (c.kernel == 7) {
         if (netcsum::hdr_supported(a)) {
-            // Defaults from the r1y sweeps (C3, 16 M x 20 B): 2 tiles in flight per wave, 4 tiles
-            // per wave (grid = tiles / 16): 5.77 TB/s vs 5.46 for kernel 5; GRID_MULT > 1 instead
-            // sizes the grid as resident blocks x CUs x mult.
+            // Defaults from the r1y / r1h sweeps (C3, 16 M x 20 B): 2 headers per lane (128-header
+            // tiles), 3 tiles in flight per wave, 4 tiles per wave (grid = tiles / 16): 5.89 TB/s vs
+            // 5.77 for one header per lane and 5.54 for kernel 5; GRID_MULT > 1 instead sizes the
+            // grid as resident blocks x CUs x mult.
+            c.tile = netcsum::hdr_lanes_h(a, tile);           // TILE = headers per lane (1, 2, 4; auto 2)
             int st = g_tune_chunks.load();
-            if (!(st == 2 || st == 3 || st == 4)) st = 2;
+            if (!(st == 2 || st == 3 || st == 4)) st = (c.tile == 2) ? 3 : 2;
             c.chunks_per_pass = st;
             c.group_lanes = 1;
             c.nt = true;
             c.blocks_needed = 0;
             if (c.grid <= 0) {
-                c.grid = c.grid_mult > 1 ? netcsum::hdr_occupancy(a, st) * c.cus * c.grid_mult
-                                         : (int)std::max<uint64_t>(1u, ((uint64_t)a.n_seg + 1023u) / 1024u);
+                const uint64_t tiles = ((uint64_t)a.n_seg + 64u * c.tile - 1u) / (64u * c.tile);
+                c.grid = c.grid_mult > 1 ? netcsum::hdr_occupancy(a, st, c.tile) * c.cus * c.grid_mult
+                                         : (int)std::max<uint64_t>(1u, (tiles + 15u) / 16u);
             }
             return c;
         }

@@ -2,19 +2,22 @@
 // (config C3: 16 M x 20 B IPv4 headers; NetUtil_16BitOnesCplChkSumHdrCalc / ...HdrVerify,
 // net_util.c:159-195 / :245-284, whose sum is NetUtil_16BitSumHdrCalc, net_util.c:1160-1208).
 //
-// One lane per header, as in seg_small_kernel (netcsum_small.hip), but the bytes do not reach the
-// lanes through per-lane 20-B-strided loads: a wave's TILE of 64 consecutive headers is one
-// contiguous byte range, fetched as whole 1-KiB LDS-DMA pieces (raw buffer loads with the `lds`
-// modifier: 64 lanes x 16 B, 8 aligned cache lines per wave-instruction, the hardware range check
-// drops the lanes past the tile), and each lane then reads its header's ND dwords back from the LDS
-// image (ds_read_b32 at a 4-B-aligned offset; an odd dword stride such as 5 is bank-conflict free).
+// H headers per lane (lane l takes headers l, 64 + l, ...), as in seg_small_kernel
+// (netcsum_small.hip), but the bytes do not reach the lanes through per-lane 20-B-strided loads: a
+// wave's TILE of 64*H consecutive headers is one contiguous byte range, fetched as whole 1-KiB
+// LDS-DMA pieces (raw buffer loads with the `lds` modifier: 64 lanes x 16 B, 8 aligned cache lines per
+// wave-instruction, the hardware range check drops the lanes past the tile), and each lane then
+// reads its headers' ND dwords back from the LDS image (ds_read_b32 at a 4-B-aligned offset; an odd
+// dword stride such as 5 is bank-conflict free). H > 1 fills the pieces better: a 64-header tile of
+// 20-B headers is 1.26 KiB in two pieces (63 % of the lanes carry bytes), 128 headers 2.5 KiB in
+// three (84 %).
 //
 // Pipeline: each wave keeps S tiles in flight in an LDS ring (S x P KiB per wave). Nothing orders a
 // ds_read behind an LDS-DMA except the wave's own vmcnt, so the waits are counted by hand: every
-// iteration issues exactly P DMA and ONE store (a raw buffer store whose inactive lanes carry an
-// out-of-range offset, so the instruction always issues; the prologue pairs each of its S-1 tiles
-// with a dropped store), hence consuming tile i while tiles i+1 .. i+S-1 are in flight waits
-// vmcnt((S-1)(P+1)).
+// iteration issues exactly P DMA and H stores (raw buffer stores whose inactive lanes carry an
+// out-of-range offset, so the instructions always issue; the prologue pairs each of its S-1 tiles
+// with H dropped stores), hence consuming tile i while tiles i+1 .. i+S-1 are in flight waits
+// vmcnt((S-1)(P+H)).
 //
 // Tiles are dealt round-robin over the grid's waves (wave g: tiles g, g+W, g+2W, ...), so at any
 // time the waves in flight read one dense, advancing window of HBM (the read-probe pattern).
@@ -55,14 +58,15 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// P KiB pieces per tile, S tiles in flight per wave.
-template <int P, int S>
+// P KiB pieces per tile, S tiles in flight per wave, H headers per lane (64*H per tile).
+template <int P, int S, int H>
 __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t nd) {
     __shared__ uint32_t img[4][S][P * 256];                    // per wave: S stages x P KiB
+    constexpr uint32_t TH = 64u * (uint32_t)H;                 // headers per tile
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = A.n_seg;
-    const uint32_t ntiles = (n + 63u) >> 6;
+    const uint32_t ntiles = (n + TH - 1u) / TH;
     const uint32_t W = gridDim.x * 4u;
     const uint32_t t0 = blockIdx.x * 4u + w;
     if (t0 >= ntiles) {
@@ -81,8 +85,8 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
         const uint32_t slot = i % (uint32_t)S;
         const uint32_t t = t0 + i * W;
         const bool live = i < cnt;
-        const uint32_t h0 = live ? t * 64u : 0u;
-        const uint32_t nh = live ? min(64u, n - h0) : 0u;
+        const uint32_t h0 = live ? t * TH : 0u;
+        const uint32_t nh = live ? min(TH, n - h0) : 0u;
         const uintptr_t a0 = base + (uint64_t)h0 * st;
         const uintptr_t i0 = a0 & ~(uintptr_t)15;
         const uint32_t bytes = nh ? (uint32_t)(a0 - i0) + (nh - 1u) * st + len : 0u;
@@ -94,85 +98,109 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
         }
     };
 
-    // Prologue: S-1 tiles, each followed by a dropped store (out-of-range offset), so that from the
-    // first iteration on exactly (S-1)(P+1) VMEM ops are younger than the tile being consumed.
+    // Prologue: S-1 tiles, each followed by H dropped stores (out-of-range offset), so that from the
+    // first iteration on exactly (S-1)(P+H) VMEM ops are younger than the tile being consumed.
 #pragma unroll
     for (int j = 0; j < S - 1; ++j) {
         issue((uint32_t)j);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, ro, (int)kOOB, 0, 0);
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {                       // distinct offsets: no store merging
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, ro, (int)(kOOB + 2u * (uint32_t)(j * H + hh)), 0, 0);
+        }
     }
     for (uint32_t i = 0; i < cnt; ++i) {
         issue(i + (uint32_t)S - 1u);
-        wait_vm<(S - 1) * (P + 1)>();                         // tile i landed in LDS
+        wait_vm<(S - 1) * (P + H)>();                         // tile i landed in LDS
         const uint32_t slot = i % (uint32_t)S;
-        const uint32_t h0 = (t0 + i * W) * 64u;
-        const uint32_t nh = min(64u, n - h0);
+        const uint32_t h0 = (t0 + i * W) * TH;
+        const uint32_t nh = min(TH, n - h0);
         const uintptr_t a0 = base + (uint64_t)h0 * st;
-        const uint32_t dw0 = ((uint32_t)(a0 & 15u) + lane * st) >> 2;   // header's first dword in the image
         const uint32_t* im = &img[w][slot][0];
-        uint32_t acc = 0u;
-        for (uint32_t d = 0; d + 1u < nd; ++d) {
-            acc = __builtin_amdgcn_sad_u16(im[dw0 + d], 0u, acc);
+        uint32_t sres[H];
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+            const uint32_t j = 64u * (uint32_t)hh + lane;      // header within the tile
+            const uint32_t dw0 = ((uint32_t)(a0 & 15u) + j * st) >> 2;   // its first dword in the image
+            uint32_t acc = 0u;
+            for (uint32_t d = 0; d + 1u < nd; ++d) {
+                acc = __builtin_amdgcn_sad_u16(im[dw0 + d], 0u, acc);
+            }
+            acc = __builtin_amdgcn_sad_u16(im[dw0 + nd - 1u] & last_mask, 0u, acc);
+            sres[hh] = fold16(acc);
         }
-        acc = __builtin_amdgcn_sad_u16(im[dw0 + nd - 1u] & last_mask, 0u, acc);
-        const uint32_t s = fold16(acc);
-        const uint32_t h = h0 + lane;
-        if (verify) {
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(s == 0xFFFFu ? 1u : 0u), ro,
-                                                 (int)(lane < nh ? h : kOOB), 0, 0);
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(~s), ro, (int)(lane < nh ? 2u * h : kOOB), 0, 0);
+#pragma unroll
+        for (int hh = 0; hh < H; ++hh) {
+            const uint32_t j = 64u * (uint32_t)hh + lane;
+            const uint32_t h = h0 + j;
+            const uint32_t s = sres[hh];
+            if (verify) {
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(s == 0xFFFFu ? 1u : 0u), ro,
+                                                     (int)(j < nh ? h : kOOB), 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(~s), ro, (int)(j < nh ? 2u * h : kOOB), 0, 0);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // image reads done before the slot refills
     }
     wait_vm<0>();                                              // trailing dummy DMA
 }
 
-template <int P, int S>
+template <int P, int S, int H>
 hipError_t launch_hdr_t(const SegBatchArgs& a, int grid, hipStream_t s) {
-    const uint32_t tiles = (a.n_seg + 63u) / 64u;
-    const uint32_t g = grid > 0 ? (uint32_t)grid : (tiles + 3u) / 4u;
-    hipLaunchKernelGGL((seg_hdr_kernel<P, S>), dim3(std::max<uint32_t>(1u, std::min<uint32_t>(g, (tiles + 3u) / 4u))),
+    const uint32_t tiles = (a.n_seg + 64u * H - 1u) / (64u * H);
+    const uint32_t g = grid > 0 ? (uint32_t)grid : (tiles + 15u) / 16u;      // default: 4 tiles per wave
+    hipLaunchKernelGGL((seg_hdr_kernel<P, S, H>), dim3(std::max<uint32_t>(1u, std::min<uint32_t>(g, (tiles + 3u) / 4u))),
                        dim3(256), 0, s, a, (a.seg_len + 3u) >> 2);
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Pieces per 64-header tile: the image starts at the 16-B boundary below the tile (lead <= 12).
-uint32_t hdr_pieces(const SegBatchArgs& a) {
-    return (uint32_t)((12u + 63u * a.seg_stride + a.seg_len + 1023u) / 1024u);
+// Pieces per tile of 64*H headers: the image starts at the 16-B boundary below the tile (lead <= 12).
+uint32_t hdr_pieces(const SegBatchArgs& a, int h) {
+    return (uint32_t)((12u + (64u * (uint32_t)h - 1u) * a.seg_stride + a.seg_len + 1023u) / 1024u);
 }
 
 bool hdr_supported(const SegBatchArgs& a) {
-    return small_supported(a) && a.seg_stride <= 64u && hdr_pieces(a) <= 5u && a.n_seg < 0x3FFFFFFFu;
+    return small_supported(a) && a.seg_stride <= 64u && hdr_pieces(a, 1) <= 5u && a.n_seg < 0x3FFFFFFFu;
 }
 
-// grid <= 0: one wave per tile (4 tiles per block). grid > 0: that many blocks, tiles dealt
-// round-robin over their waves.
-int hdr_occupancy(const SegBatchArgs& a, int stages) {
-    const uint32_t p = hdr_pieces(a);
-    const int S = stages == 2 ? 2 : (stages == 3 ? 3 : 4);
+// Headers per lane: the requested 1, 2 or 4 where its tile fits 6 pieces; auto (h <= 0) = 2.
+int hdr_lanes_h(const SegBatchArgs& a, int h) {
+    if (h != 1 && h != 2 && h != 4) h = 2;
+    while (h > 1 && hdr_pieces(a, h) > 6u) h >>= 1;
+    return h;
+}
+
+#define NETCSUM_HDR_LIST(X) \
+    X(1, 2, 1) X(1, 3, 1) X(1, 4, 1) X(2, 2, 1) X(2, 3, 1) X(2, 4, 1) X(3, 2, 1) X(3, 3, 1) X(3, 4, 1) \
+    X(4, 2, 1) X(4, 3, 1) X(4, 4, 1) X(5, 2, 1) X(5, 3, 1) X(5, 4, 1)                                  \
+    X(1, 2, 2) X(1, 3, 2) X(2, 2, 2) X(2, 3, 2) X(3, 2, 2) X(3, 3, 2) X(4, 2, 2) X(4, 3, 2)            \
+    X(5, 2, 2) X(5, 3, 2) X(6, 2, 2) X(6, 3, 2)                                                        \
+    X(1, 2, 4) X(2, 2, 4) X(3, 2, 4) X(4, 2, 4) X(5, 2, 4) X(6, 2, 4)
+
+// Resident 256-thread blocks per CU. stages 2..4 (H = 2: 2..3, H = 4: 2).
+int hdr_occupancy(const SegBatchArgs& a, int stages, int h) {
+    h = hdr_lanes_h(a, h);
+    const uint32_t p = hdr_pieces(a, h);
+    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 1 ? 4 : (h == 2 ? 3 : 2));
     int occ = 0;
     hipError_t e = hipErrorInvalidValue;
-#define NETCSUM_H(P_, S_) \
-    if (p == P_ && S == S_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, seg_hdr_kernel<P_, S_>, 256, 0);
-    NETCSUM_H(1, 2) NETCSUM_H(1, 3) NETCSUM_H(1, 4) NETCSUM_H(2, 2) NETCSUM_H(2, 3) NETCSUM_H(2, 4)
-    NETCSUM_H(3, 2) NETCSUM_H(3, 3) NETCSUM_H(3, 4) NETCSUM_H(4, 2) NETCSUM_H(4, 3) NETCSUM_H(4, 4) \
-    NETCSUM_H(5, 2) NETCSUM_H(5, 3) NETCSUM_H(5, 4)
+#define NETCSUM_H(P_, S_, H_) \
+    if (p == P_ && S == S_ && h == H_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, seg_hdr_kernel<P_, S_, H_>, 256, 0);
+    NETCSUM_HDR_LIST(NETCSUM_H)
 #undef NETCSUM_H
     return (e == hipSuccess && occ > 0) ? occ : 1;
 }
 
-hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int grid, hipStream_t s) {
+hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s) {
     if (!hdr_supported(a)) return hipErrorInvalidValue;
-    const uint32_t p = hdr_pieces(a);
-    const int S = stages == 2 ? 2 : (stages == 3 ? 3 : 4);
-#define NETCSUM_H(P_, S_) \
-    if (p == P_ && S == S_) return launch_hdr_t<P_, S_>(a, grid, s);
-    NETCSUM_H(1, 2) NETCSUM_H(1, 3) NETCSUM_H(1, 4) NETCSUM_H(2, 2) NETCSUM_H(2, 3) NETCSUM_H(2, 4)
-    NETCSUM_H(3, 2) NETCSUM_H(3, 3) NETCSUM_H(3, 4) NETCSUM_H(4, 2) NETCSUM_H(4, 3) NETCSUM_H(4, 4) \
-    NETCSUM_H(5, 2) NETCSUM_H(5, 3) NETCSUM_H(5, 4)
+    h = hdr_lanes_h(a, h);
+    const uint32_t p = hdr_pieces(a, h);
+    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 1 ? 4 : (h == 2 ? 3 : 2));
+#define NETCSUM_H(P_, S_, H_) \
+    if (p == P_ && S == S_ && h == H_) return launch_hdr_t<P_, S_, H_>(a, grid, s);
+    NETCSUM_HDR_LIST(NETCSUM_H)
 #undef NETCSUM_H
     return hipErrorInvalidValue;
 }

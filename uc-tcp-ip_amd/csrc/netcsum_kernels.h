@@ -80,8 +80,9 @@ hipError_t launch_seg_batch(const SegBatchArgs& a, const LaunchCfg& c, hipStream
 bool small_supported(const SegBatchArgs& a);  // strided, no pseudo, 1..64 B, base/stride 4-B aligned
 hipError_t launch_small_batch(const SegBatchArgs& a, int grid, hipStream_t s);
 bool hdr_supported(const SegBatchArgs& a);     // small_supported and stride <= 64: LDS-image header tiles
-int hdr_occupancy(const SegBatchArgs& a, int stages);
-hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int grid, hipStream_t s);
+int hdr_lanes_h(const SegBatchArgs& a, int h);  // headers per lane kernel 7 uses for a request (auto: h <= 0)
+int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
+hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256
 bool stream_dense(const SegBatchArgs& a);      // strided, stride == len >= 1024: the default for kernel 6
 uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves);

@@ -963,8 +963,10 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
                                   "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel"};
     const int kid = (c.kernel >= 1 && c.kernel <= 7) ? c.kernel : 0;
     if (kid == 7) {
-        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<S=%d> block=256 grid=%d", c.chunks_per_pass,
-                 c.grid);
+        const int h = hdr_lanes_h(a, c.tile);
+        const int smax = h == 1 ? 4 : (h == 2 ? 3 : 2);          // stages the H instantiations exist for
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<S=%d,H=%d> block=256 grid=%d",
+                 c.chunks_per_pass < smax ? c.chunks_per_pass : smax, h, c.grid);
         return;
     }
     if (kid == 6) {
@@ -989,7 +991,7 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
         return launch_stream_batch(a, c.chunks_per_pass, c.stream_spw, c.nt, s);   // K = pieces in flight
     }
     if (c.kernel == 7) {
-        return launch_hdr_batch(a, c.chunks_per_pass, c.grid, s);                 // K = tiles in flight
+        return launch_hdr_batch(a, c.chunks_per_pass, c.tile, c.grid, s);                 // K = tiles in flight
     }
     if (c.kernel == 4) {
         return launch_tile_dispatch(a, c, s);
