@@ -50,6 +50,18 @@ struct PktStage {
     uintptr_t a;         // packet start address
 };
 
+// Pins a stage's loaded chunks behind everything issued before this point (an empty asm with a
+// memory clobber that reads and writes them): the consume of the stage cannot be hoisted into the
+// next stage's issue, so the wave issues all K loads of the next stage before it waits for this one
+// (the Tx instantiation otherwise stalled on `s_waitcnt vmcnt(8)` between its issue loads).
+template <int K>
+__device__ __forceinline__ void pin_chunks(u32x4 (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        asm volatile("" : "+v"(v[k]) : : "memory");
+    }
+}
+
 // The packet's frame starts at the 16-B boundary below it (fmask 15), or for Tx sector write-back at
 // the sector boundary below it (fmask 31 / 63); chunk c of the frame is [q0 + 16c, q0 + 16c + 16).
 template <int G, int K, bool NT>
@@ -429,12 +441,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
         pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane, fmask);
+        pin_chunks<K>(S0.v);
         pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
         pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane, fmask);
+        pin_chunks<K>(S1.v);
         pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
         i = nx;
     }
