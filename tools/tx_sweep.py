@@ -54,21 +54,26 @@ def main():
                              reps=40)
             print(json.dumps({"variant": {"rx_group": g}, "ms_med": round(ms_g, 4),
                               "GBps_med": round(n * L / ms_g / 1e6, 1)}), flush=True)
-        for wb, nt, tile in [(w, t, j) for w in wbs for t in (1, 0) for j in (1, 2, 4)]:
+        grids = [int(x) for x in os.environ.get("TX_SWEEP_GRIDS", "0").split(",")]
+        tiles = [int(x) for x in os.environ.get("TX_SWEEP_TILES", "1,2,4").split(",")]
+        nts = [int(x) for x in os.environ.get("TX_SWEEP_NT", "1,0").split(",")]
+        for wb, nt, tile, grid in [(w, t, j, q) for w in wbs for t in nts for j in tiles for q in grids]:
                 netcsum.tune(netcsum.TUNE_TX_WRITEBACK, wb)
                 netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
                 netcsum.tune(netcsum.TUNE_TILE, tile)
+                netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
                 pk.copy_(pristine)
                 netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st)
                 torch.cuda.synchronize()
                 same = bool(torch.equal(pk, want))
                 ms = events_ms(lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st), st,
                                reps=40)
-                print(json.dumps({"variant": {"group": g, "wb": wb, "nt": nt, "tile": tile}, "ms_med": round(ms, 4),
+                print(json.dumps({"variant": {"group": g, "wb": wb, "nt": nt, "tile": tile, "grid": grid},
+                                  "ms_med": round(ms, 4),
                                   "GBps_med": round(n * (L + 4) / ms / 1e6, 1), "same_as_two_byte": same}),
                       flush=True)
     for k, val in ((netcsum.TUNE_TX_WRITEBACK, -1), (netcsum.TUNE_NT_LOADS, -1), (netcsum.TUNE_TILE, -1),
-                   (netcsum.TUNE_GROUP_LANES, 0)):
+                   (netcsum.TUNE_GROUP_LANES, 0), (netcsum.TUNE_GRID_BLOCKS, 0)):
         netcsum.tune(k, val)
 
 
