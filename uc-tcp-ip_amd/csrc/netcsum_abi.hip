@@ -534,9 +534,11 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         void* rec = nullptr;
         NC_HIP(hipMallocAsync(&rec, (size_t)n_pkt * 8u, st));
         a.tx_rec = static_cast<uint2*>(rec);
-        NC_HIP(netcsum::launch_pkt_batch(a, c, tx, st));
-        NC_HIP(netcsum::launch_tx_scatter(a, st));
-        NC_HIP(hipFreeAsync(rec, st));
+        hipError_t e = netcsum::launch_pkt_batch(a, c, tx, st);
+        if (e == hipSuccess) e = netcsum::launch_tx_scatter(a, st);
+        const hipError_t ef = hipFreeAsync(rec, st);            // freed on the error path too
+        NC_HIP(e);
+        NC_HIP(ef);
         return NET_UTIL_ERR_NONE;
     }
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, static_cast<hipStream_t>(hip_stream)));
