@@ -288,16 +288,10 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
-    NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
+    NETCSUM_TUNE_TILE          = 9    /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).
-                                         Kernel 6: J > 0 = segments per wave run (<= 128; auto 16) */
-    NETCSUM_TUNE_TX_WRITEBACK  = 10   /* TxFinalizeIPv4 checksum stores: -1 auto (default), 0 two-
-                                         byte stores, 1 / 2 rewrite the whole aligned 32 / 64-B
-                                         sectors holding the fields (strided batches with stride
-                                         >= 192 B, sector-aligned d_base, >= 16 lanes per packet;
-                                         elsewhere two-byte stores), 3 two-phase (checksums recorded
-                                         densely, then scattered by a second kernel; stream-ordered
-                                         scratch of 8 B per packet)                                 */
+                                         Kernel 6: J > 0 = segments per wave run (<= 128; auto 16).
+                                         Kernel 7: headers per lane, 1, 2 or 4 (auto 2)              */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -86,11 +86,7 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_WRITEBACK, 4) == 219
-    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_WRITEBACK, -2) == 219
-    for v in (-1, 0, 1, 2, 3):
-        assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_WRITEBACK, v) == 200
-    L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_WRITEBACK, -1)
+    assert L.NetUtil_MI355X_Tune(10, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Fill(3, 10, 0, 0, 0, None) == 219                   # not 8-B aligned
     assert L.NetUtil_MI355X_ReadStream(16, 17, 8, None) == 219                # not a multiple of 16
 

@@ -20,13 +20,11 @@ def _defaults():
         netcsum.tune(k, 0)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_TILE, -1)
-    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, -1)
     yield
     for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES):
         netcsum.tune(k, 0)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_TILE, -1)
-    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, -1)
 
 
 def _rx_gpu(buf, offs, lens):
@@ -106,14 +104,13 @@ def test_tx_finalize_writes_reference_checksums_then_rx_accepts(udp_tx_csum):
 
 
 @pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (2048, 1514), (200, 184), (192, 48)])
-@pytest.mark.parametrize("wb", [-1, 0, 1, 2, 3])
-def test_tx_finalize_strided_writeback_modes(stride, pkt_len, wb):
-    """Strided Tx finalize under every write-back form (TUNE_TX_WRITEBACK: 0 two-byte stores, 1 / 2
-    whole 32 / 64-B sectors): packets finalized exactly as the packet oracle does, and every byte
-    between packets (stride > pkt_len) and past the last one left as it was. Strides that are not
-    multiples of 64 put packets at every sector offset; 48-B slots make the 64-B sectors overrun
-    the packet, which must fall back to two-byte stores."""
-    rng = random.Random(stride * 7 + pkt_len * 3 + wb)
+@pytest.mark.parametrize("group", [0, 16, 32])
+def test_tx_finalize_strided_vs_oracle(stride, pkt_len, group):
+    """Strided Tx finalize (uniform buffer stores addressed from the wave's first packet): packets
+    finalized exactly as the packet oracle does, and every byte between packets (stride > pkt_len)
+    and past the last one left as it was; strides that are not multiples of 16 put packets at every
+    alignment; lane groups of 16 / 32 (and the auto choice, 8 lanes for small packets)."""
+    rng = random.Random(stride * 7 + pkt_len * 3 + group)
     n = 600
     kinds = ["tcp", "tcp", "udp", "udp0", "icmp", "igmp", "other", "frag", "tcp_short", "bad_ver"]
     buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
@@ -123,9 +120,7 @@ def test_tx_finalize_strided_writeback_modes(stride, pkt_len, wb):
         if len(p) >= 12 and rng.random() < 0.5:
             p[10:12] = rng.randbytes(2)                           # stale IP checksum field
         buf[i * stride:i * stride + len(p)] = np.frombuffer(bytes(p), np.uint8)
-    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, wb)
-    if pkt_len < 1000:
-        netcsum.tune(netcsum.TUNE_GROUP_LANES, 16)                # write-back needs >= 16 lanes per packet
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     b = torch.from_numpy(buf).to(DEV)
     assert b.data_ptr() % 64 == 0
     f = torch.zeros(n, dtype=torch.uint8, device=DEV)

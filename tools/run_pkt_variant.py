@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run ONE packet-batch configuration N times (for rocprofv3 --pmc passes; GPU box only): fused Rx
 validation or Tx finalize over 1 M x 1500-B IPv4/TCP datagrams, strided.
-Usage: python tools/run_pkt_variant.py <rx|tx> [reps] [wb=0|1|2] [nt=0|1] [tile=N]"""
+Usage: python tools/run_pkt_variant.py <rx|tx> [reps] [nt=0|1] [tile=N]"""
 import os
 import sys
 
@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import netcsum  # noqa: E402
 from bench import SEED  # noqa: E402
 
-KEYS = {"wb": netcsum.TUNE_TX_WRITEBACK, "nt": netcsum.TUNE_NT_LOADS, "tile": netcsum.TUNE_TILE,
+KEYS = {"nt": netcsum.TUNE_NT_LOADS, "tile": netcsum.TUNE_TILE,
         "group": netcsum.TUNE_GROUP_LANES}
 
 

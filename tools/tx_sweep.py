@@ -33,7 +33,6 @@ def main():
     pristine = pk.clone()
     flags = torch.zeros(n, dtype=torch.uint8, device=dev)
 
-    netcsum.tune(netcsum.TUNE_TX_WRITEBACK, 0)
     netcsum.tx_finalize_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)
     torch.cuda.synchronize()
     want = pk.clone()
@@ -46,7 +45,7 @@ def main():
     print(json.dumps({"variant": "rx_fused", "ms_med": round(ms_rx, 4),
                       "GBps_med": round(n * L / ms_rx / 1e6, 1), "oracle_sample_ok": oracle_ok}), flush=True)
     groups = [int(g) for g in os.environ.get("TX_SWEEP_GROUPS", "0").split(",")]
-    wbs = [int(w) for w in os.environ.get("TX_SWEEP_WB", "0,1,2,3").split(",")]
+    wbs = [0]
     for g in groups:
         netcsum.tune(netcsum.TUNE_GROUP_LANES, g)
         if g:
@@ -58,7 +57,6 @@ def main():
         tiles = [int(x) for x in os.environ.get("TX_SWEEP_TILES", "1,2,4").split(",")]
         nts = [int(x) for x in os.environ.get("TX_SWEEP_NT", "1,0").split(",")]
         for wb, nt, tile, grid in [(w, t, j, q) for w in wbs for t in nts for j in tiles for q in grids]:
-                netcsum.tune(netcsum.TUNE_TX_WRITEBACK, wb)
                 netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
                 netcsum.tune(netcsum.TUNE_TILE, tile)
                 netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
@@ -70,9 +68,9 @@ def main():
                                reps=40)
                 print(json.dumps({"variant": {"group": g, "wb": wb, "nt": nt, "tile": tile, "grid": grid},
                                   "ms_med": round(ms, 4),
-                                  "GBps_med": round(n * (L + 4) / ms / 1e6, 1), "same_as_two_byte": same}),
+                                  "GBps_med": round(n * (L + 4) / ms / 1e6, 1), "same_as_first": same}),
                       flush=True)
-    for k, val in ((netcsum.TUNE_TX_WRITEBACK, -1), (netcsum.TUNE_NT_LOADS, -1), (netcsum.TUNE_TILE, -1),
+    for k, val in ((netcsum.TUNE_NT_LOADS, -1), (netcsum.TUNE_TILE, -1),
                    (netcsum.TUNE_GROUP_LANES, 0), (netcsum.TUNE_GRID_BLOCKS, 0)):
         netcsum.tune(k, val)
 

@@ -30,8 +30,6 @@ std::atomic<int> g_tune_chunks{0};
 std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
 std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
-std::atomic<int> g_tune_tx_wb{-1};                // -1: auto Tx write-back form (kTxSectorAuto)
-constexpr uint32_t kTxSectorAuto = 0u;            // sector bytes auto mode uses where eligible (0: two-byte stores)
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -503,23 +501,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         g = d_off ? 32 : std::max(8, pow2_group((chunks + 5u) / 6u));
     }
     c.group_lanes = pow2_group((uint32_t)g);
-    bool two_phase = false;
-    if (tx) {
-        // Whole-sector write-back (PktBatchArgs::wb_sector): strided batches only, packets at least
-        // 192 B apart (no two packets' checksum fields share a sector: fields lie within the first
-        // 78 B), a sector-aligned base (no frame starts before the buffer), >= 16 lanes per packet
-        // (header fields within the frame's first 16*G bytes).
-        const int wb = g_tune_tx_wb.load();
-        two_phase = wb == 3;
-        const uint32_t sec = wb == 1 ? 32u : (wb == 2 ? 64u : (wb < 0 ? kTxSectorAuto : 0u));
-        if (sec != 0u && d_off == nullptr && stride >= 192u && ((uintptr_t)d_base % sec) == 0u &&
-            c.group_lanes >= 16) {
-            a.wb_sector = sec;
-        }
-    }
-    const uint32_t lead_max = a.wb_sector ? a.wb_sector - 1u : 15u;
-    const uint32_t chunks_f = d_off ? chunks : ((uint32_t)pkt_len + lead_max + 15u) / 16u;
-    c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks_f + c.group_lanes - 1u) / c.group_lanes));
+    c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks + c.group_lanes - 1u) / c.group_lanes));
     // Rx streams with nt loads; Tx re-writes header lines it has just read and is faster with plain
     // loads (profiles/r1tc_tx_sweep.jsonl: 0.323 vs 0.356 ms at tile 2).
     const int nt = g_tune_nt.load();
@@ -527,20 +509,6 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     c.grid = g_tune_grid.load();
     const int tile = g_tune_tile.load();
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
-    if (two_phase) {
-        // Two-phase Tx: the fused kernel records each packet's checksums densely (8 B), a second
-        // kernel scatters them into the headers; the record buffer is stream-ordered.
-        hipStream_t st = static_cast<hipStream_t>(hip_stream);
-        void* rec = nullptr;
-        NC_HIP(hipMallocAsync(&rec, (size_t)n_pkt * 8u, st));
-        a.tx_rec = static_cast<uint2*>(rec);
-        hipError_t e = netcsum::launch_pkt_batch(a, c, tx, st);
-        if (e == hipSuccess) e = netcsum::launch_tx_scatter(a, st);
-        const hipError_t ef = hipFreeAsync(rec, st);            // freed on the error path too
-        NC_HIP(e);
-        NC_HIP(ef);
-        return NET_UTIL_ERR_NONE;
-    }
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
@@ -654,10 +622,6 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_TILE:
         if (value < -1 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tile.store(value);
-        return NET_UTIL_ERR_NONE;
-    case NETCSUM_TUNE_TX_WRITEBACK:
-        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
-        g_tune_tx_wb.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:
         if (value != 0 && value != 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

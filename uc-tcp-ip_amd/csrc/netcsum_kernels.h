@@ -50,9 +50,6 @@ struct PktBatchArgs {
     uint8_t*        flags_out;     // NETCSUM_PKT_* per packet (optional for Tx)
     uint32_t        tile;          // segments (packets) per group per block tile (0 = grid-stride)
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
-    uint32_t        wb_sector;     // Tx: 0 = two-byte checksum stores; 32 / 64 = whole aligned sectors
-                                   // (each packet's frame then starts at the sector below it)
-    uint2*          tx_rec;        // Tx two-phase: per-packet store records (tx_scatter_kernel), else null
 };
 
 struct ChainBatchArgs {
@@ -71,7 +68,6 @@ struct ChainBatchArgs {
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
 
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s);
-hipError_t launch_tx_scatter(const PktBatchArgs& a, hipStream_t s);   // phase 2 of the two-phase Tx
 
 bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation
 const char* last_launch();                  // description of this thread's last batch launch

@@ -62,12 +62,12 @@ __device__ __forceinline__ void pin_chunks(u32x4 (&v)[K]) {
     }
 }
 
-// The packet's frame starts at the 16-B boundary below it (fmask 15), or for Tx sector write-back at
-// the sector boundary below it (fmask 31 / 63); chunk c of the frame is [q0 + 16c, q0 + 16c + 16).
+// The packet's frame starts at the 16-B boundary below it; chunk c of the frame is
+// [q0 + 16c, q0 + 16c + 16).
 template <int G, int K, bool NT>
-__device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane, uint32_t fmask) {
+__device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane) {
     st.a = a;
-    st.lead = (uint32_t)(a & fmask);
+    st.lead = (uint32_t)(a & 15u);
     st.avail = avail;
     const uintptr_t q0 = a - st.lead;
     const uint32_t nch = (avail + st.lead + 15u) >> 4;
@@ -208,59 +208,72 @@ __device__ __forceinline__ void store_csum(uintptr_t a, uint32_t off, uint32_t h
     p[1] = (uint8_t)(host_val >> 8);
 }
 
-__device__ __forceinline__ u32x4 patch_byte(u32x4 v, uint32_t pos, uint32_t b) {   // byte pos of a chunk
-    const uint32_t sh = 8u * (pos & 3u);
-    const uint32_t m = ~(0xFFu << sh), x = (b & 0xFFu) << sh;
-    const uint32_t d = pos >> 2;
-    v.x = (d == 0u) ? ((v.x & m) | x) : v.x;
-    v.y = (d == 1u) ? ((v.y & m) | x) : v.y;
-    v.z = (d == 2u) ? ((v.z & m) | x) : v.z;
-    v.w = (d == 3u) ? ((v.w & m) | x) : v.w;
-    return v;
+constexpr uint32_t kOOB = 0xFFFFFFFFu;     // buffer offset at/after every num_records: store dropped
+constexpr int kRsrcWord3 = 0x00020000;     // gfx9-family raw buffer V# word 3
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
 }
 
-// The host-order value `val` memcpy'd to frame bytes f, f+1, where they fall in chunk c.
-__device__ __forceinline__ u32x4 patch_field(u32x4 v, uint32_t c, uint32_t f, uint32_t val) {
-    if ((f >> 4) == c) v = patch_byte(v, f & 15u, val & 0xFFu);
-    if (((f + 1u) >> 4) == c) v = patch_byte(v, (f + 1u) & 15u, val >> 8);
-    return v;
+__device__ __forceinline__ void store_byte(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xFFu), r, (int)off, 0, 0);
 }
 
-// Whole-sector write-back: the aligned `sec`-byte sectors that hold a checksum byte are rewritten
-// whole from the chunks already in registers (slot k = 0: lane c holds frame chunk c, and the frame
-// starts at the sector boundary below the packet), so HBM sees full-sector writes instead of 2-byte
-// partial ones. The rewritten bytes outside the fields are the values just read (callers own the
-// batch buffer; the host enables this only where no other packet's fields share a sector). Returns
-// false — nothing stored — when a sector would reach past the packet's bytes or past slot 0; the
-// caller then stores the fields two bytes at a time. The decision is uniform over the group.
-template <int G, int K>
-__device__ __forceinline__ bool tx_sector_writeback(const PktStage<K>& st, uint32_t cip, uint32_t cl4, uint32_t l4off,
-                                                    uint32_t sec, int lane) {
-    const uint32_t lead = st.lead;
-    const uint32_t lim = min(lead + st.avail, 16u * (uint32_t)G);
-    const uint32_t sh = (sec == 64u) ? 6u : 5u;
-    const uint32_t fi = lead + 10u;                              // IPv4 header checksum
-    const uint32_t ci0 = (fi >> sh) << (sh - 4u), ci1 = (((fi + 1u) >> sh) + 1u) << (sh - 4u);
-    const bool l4 = cl4 != ~0u;
-    const uint32_t fl = lead + (l4 ? l4off : 10u);
-    const uint32_t cl0 = (fl >> sh) << (sh - 4u), cl1 = (((fl + 1u) >> sh) + 1u) << (sh - 4u);
-    if (16u * max(ci1, cl1) > lim) {
-        return false;
-    }
-    const uint32_t c = (uint32_t)lane;
-    if ((c >= ci0 && c < ci1) || (c >= cl0 && c < cl1)) {
-        u32x4 w = patch_field(st.v[0], c, fi, cip);
-        if (l4) {
-            w = patch_field(w, c, fl, cl4);
+// A packet's stores, deferred: the kernel issues them right AFTER the next stage's loads, so no
+// wait for a stage's loads can also wait for the previous packet's stores (the VMEM counter retires
+// in issue order). Measured (profiles/r1tx11_tx_sweep.jsonl): no change for Tx — its extra time over
+// Rx is the 2 M scattered header writes themselves (Tx with the stores compiled out: 0.250 ms).
+struct PktStore {
+    uintptr_t a;       // packet address
+    uint32_t  vals;    // Tx: IP checksum | transport checksum << 16 (host order)
+    uint32_t  meta;    // transport field offset | flags << 16 | store IP << 24 | store L4 << 25 | lane stores << 26
+    uint32_t  idx;     // packet index (flags)
+};
+
+// BS (strided batches): every store is a raw buffer store executed by ALL lanes, the lanes that store
+// nothing carrying an out-of-range offset, so every path issues the same VMEM stores and the
+// compiler's vmcnt bookkeeping stays exact (stores under a lane-0 branch make it conservative).
+template <int G, bool TX, bool BS>
+__device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs& A) {
+    const uint32_t f = (ps.meta >> 16) & 0xFFu;
+    const bool me = (ps.meta >> 26) & 1u;
+    const bool si = TX && ((ps.meta >> 24) & 1u), sl = TX && ((ps.meta >> 25) & 1u);
+    const uint32_t l4off = ps.meta & 0xFFFFu;
+    if constexpr (BS) {
+        // Packets of one stage lie within a few strides of the wave's lane-0 packet (the lowest
+        // address of the stage; if lane 0 stores nothing, no lane does), so a V# based there
+        // reaches them with 32-bit offsets.
+        const uintptr_t wb = (((uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(ps.a >> 32))) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ps.a);
+        const uint32_t o = (uint32_t)(ps.a - wb);
+        if constexpr (TX) {
+            const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0xFFFFFFFFu);
+            store_byte(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
+            store_byte(rp, ps.vals >> 8, si ? o + 11u : kOOB);
+            store_byte(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
+            store_byte(rp, ps.vals >> 24, sl ? o + l4off + 1u : kOOB);
         }
-        *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(st.a - lead + 16u * c) = w;
+        const __amdgpu_buffer_rsrc_t rf = byte_rsrc(A.flags_out, A.flags_out ? A.n : 0u);
+        store_byte(rf, f, me ? ps.idx : kOOB);
+    } else {
+        if (!me) {
+            return;
+        }
+        if (si) {
+            store_csum<G>(ps.a, 10u, ps.vals & 0xFFFFu);
+        }
+        if (sl) {
+            store_csum<G>(ps.a, l4off, ps.vals >> 16);
+        }
+        if (A.flags_out) {
+            A.flags_out[ps.idx] = (uint8_t)f;
+        }
     }
-    return true;
 }
 
 template <int G, int K, bool NT, bool TX>
-__device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
-                                            int lane, int gbase) {
+__device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
+                                                int lane, int gbase) {
     // One sum over [lead, lead + end) (end = transport end, or the IP header end when the transport
     // part is not checked), plus the IP header alone from the k = 0 chunks (lead + hlen < 16*G).
     // Both are exact integer sums of the same frame half-words, so the transport part is their
@@ -334,13 +347,15 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
     }
     sip = fold16(group_sum<G>(sip));
     sl4 = fold16(group_sum<G>(sl4) + p.pseudo_le);
-    if (!valid) {                                                // a dummy stage stores nothing
-        return;
-    }
     uint32_t f = p.flags;
-    if constexpr (TX) {
-        uint32_t cip = ~0u, cl4 = ~0u;                           // values to store; ~0u = none
-        if (!(f & F_MALFORMED)) {
+    uint32_t cip = ~0u, cl4 = ~0u;                               // Tx values to store; ~0u = none
+    if (!(f & F_MALFORMED)) {
+        if constexpr (!TX) {
+            f |= (sip == 0xFFFFu) ? F_IP_OK : 0u;
+            if (p.check_l4) {
+                f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
+            }
+        } else {
             cip = (~sip) & 0xFFFFu;                              // net_ipv4.c:9578-9586
             f |= F_IP_OK;
             if (p.check_l4) {
@@ -353,40 +368,14 @@ __device__ __forceinline__ void pkt_consume(const PktStage<K>& st, const PktBatc
                 cl4 = 0u;                                        // no UDP checksum (net_udp.c:2935)
             }
         }
-        bool two_byte = cip != ~0u;
-        if (A.tx_rec != nullptr) {                               // two-phase: record, scatter later
-            if (lane == 0) {
-                A.tx_rec[idx] = make_uint2((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16),
-                                           (p.l4_csum_off & 0xFFFFu) | (cip != ~0u ? 0x10000u : 0u) |
-                                               (cl4 != ~0u ? 0x20000u : 0u));
-            }
-            two_byte = false;
-        } else if (two_byte && A.wb_sector != 0u) {
-            two_byte = !tx_sector_writeback<G, K>(st, cip, cl4, p.l4_csum_off, A.wb_sector, lane);
-        }
-        if (lane != 0) {
-            return;
-        }
-        if (two_byte) {
-            store_csum<G>(st.a, 10u, cip);
-            if (cl4 != ~0u) {
-                store_csum<G>(st.a, p.l4_csum_off, cl4);
-            }
-        }
-    } else {
-        if (lane != 0) {
-            return;
-        }
-        if (!(f & F_MALFORMED)) {
-            f |= (sip == 0xFFFFu) ? F_IP_OK : 0u;
-            if (p.check_l4) {
-                f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
-            }
-        }
     }
-    if (A.flags_out) {
-        A.flags_out[idx] = (uint8_t)f;
-    }
+    PktStore ps;
+    ps.a = st.a;
+    ps.vals = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
+    ps.meta = (p.l4_csum_off & 0xFFFFu) | ((f & 0xFFu) << 16) | (cip != ~0u ? 1u << 24 : 0u) |
+              (cl4 != ~0u ? 1u << 25 : 0u) | ((valid && lane == 0) ? 1u << 26 : 0u);
+    ps.idx = idx;
+    return ps;
 }
 
 template <bool VARLEN>
@@ -428,30 +417,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
     }
     const uintptr_t base = (uintptr_t)A.base;
     const uintptr_t z = zero_addr();
-    const uint32_t fmask = (TX && A.wb_sector != 0u) ? A.wb_sector - 1u : 15u;
     PktStage<K> S0, S1;
     uint64_t off;
     uint32_t avail;
     uint32_t i = first;
     bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
-    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane, fmask);
+    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+    PktStore pend{z, 0u, 0u, 0u};                                // nothing to store yet
     for (uint32_t j = 0u; j < iters; j += 2u) {                  // one scalar exit (see seg_pipe_kernel)
         uint32_t nx = i + step;
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane, fmask);
+        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
+        pkt_store<G, TX, !VARLEN>(pend, A);                      // previous packet's stores, after the loads
         pin_chunks<K>(S0.v);
-        pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane, fmask);
+        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+        pkt_store<G, TX, !VARLEN>(pend, A);
         pin_chunks<K>(S1.v);
-        pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
         i = nx;
     }
+    pkt_store<G, TX, !VARLEN>(pend, A);
 }
 
 template <int G, int K, bool VARLEN, bool TX>
@@ -485,29 +477,7 @@ hipError_t launch_pkt_v(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s
     }
 }
 
-// Phase 2 of the two-phase Tx finalize: one thread per packet stores the checksums recorded by
-// phase 1 (x: IP | transport << 16; y: transport field offset | has-IP << 16 | has-transport << 17).
-__global__ void __launch_bounds__(256) tx_scatter_kernel(PktBatchArgs A) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= A.n) {
-        return;
-    }
-    const uint2 r = A.tx_rec[i];
-    const uintptr_t a = (uintptr_t)A.base + (A.off ? A.off[i] : (uint64_t)i * A.stride);
-    if (r.y & 0x10000u) {
-        store_csum<1>(a, 10u, r.x & 0xFFFFu);
-    }
-    if (r.y & 0x20000u) {
-        store_csum<1>(a, r.y & 0xFFFFu, r.x >> 16);
-    }
-}
-
 }  // namespace
-
-hipError_t launch_tx_scatter(const PktBatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(tx_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
 
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
     if (a.off) {
