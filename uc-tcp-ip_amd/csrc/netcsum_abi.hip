@@ -147,9 +147,9 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
     }
     if (c.kernel == 7) {
         if (netcsum::hdr_supported(a)) {
-            // Defaults from the r1y / r1h sweeps (C3, 16 M x 20 B): 2 headers per lane (128-header
-            // tiles), 3 tiles in flight per wave, 4 tiles per wave (grid = tiles / 16): 5.89 TB/s vs
-            // 5.77 for one header per lane and 5.54 for kernel 5; GRID_MULT > 1 instead sizes the
+            // Defaults from the r1h2 sweep (C3, 16 M x 20 B): 2 headers per lane (128-header
+            // tiles), 3 tiles in flight per wave, 4 tiles per wave (grid = tiles / 16): 5.77 TB/s vs
+            // 5.55 for one header per lane and 5.44 for kernel 5; GRID_MULT > 1 instead sizes the
             // grid as resident blocks x CUs x mult.
             c.tile = netcsum::hdr_lanes_h(a, tile);           // TILE = headers per lane (1, 2, 4; auto 2)
             int st = g_tune_chunks.load();

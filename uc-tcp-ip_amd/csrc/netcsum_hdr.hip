@@ -13,11 +13,14 @@
 // three (84 %).
 //
 // Pipeline: each wave keeps S tiles in flight in an LDS ring (S x P KiB per wave). Nothing orders a
-// ds_read behind an LDS-DMA except the wave's own vmcnt, so the waits are counted by hand: every
-// iteration issues exactly P DMA and H stores (raw buffer stores whose inactive lanes carry an
-// out-of-range offset, so the instructions always issue; the prologue pairs each of its S-1 tiles
-// with H dropped stores), hence consuming tile i while tiles i+1 .. i+S-1 are in flight waits
-// vmcnt((S-1)(P+H)).
+// ds_read behind an LDS-DMA except the wave's own vmcnt, so the waits are counted by hand, and they
+// count only what is certain to retire after the tile being consumed: the DMAs of the m REAL tiles
+// issued after it (loads retire in order among themselves), wait vmcnt(m*P). Stores are not counted
+// (they may retire out of order with the loads; counting them could let the wait pass early, not
+// counting them can only wait longer), and no dummy loads are issued past a wave's last tile (a load
+// whose lanes are all out of range may retire at once). An earlier form that counted H stores and
+// dummy tiles per iteration read a not-yet-landed tile about once in 140 runs of a 1025-header batch
+// (tools/hdr_race_probe.py).
 //
 // Tiles are dealt round-robin over the grid's waves (wave g: tiles g, g+W, g+2W, ...), so at any
 // time the waves in flight read one dense, advancing window of HBM (the read-probe pattern).
@@ -80,16 +83,14 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
     const bool verify = A.verify != 0u;
     const __amdgpu_buffer_rsrc_t ro = rsrc(A.out, verify ? n : 2u * n);
 
-    // Issue tile i (i >= cnt: a dummy whose lanes are all out of range) into ring slot i % S.
+    // Issue tile i (< cnt) into ring slot i % S.
     auto issue = [&](uint32_t i) {
         const uint32_t slot = i % (uint32_t)S;
-        const uint32_t t = t0 + i * W;
-        const bool live = i < cnt;
-        const uint32_t h0 = live ? t * TH : 0u;
-        const uint32_t nh = live ? min(TH, n - h0) : 0u;
+        const uint32_t h0 = (t0 + i * W) * TH;
+        const uint32_t nh = min(TH, n - h0);
         const uintptr_t a0 = base + (uint64_t)h0 * st;
         const uintptr_t i0 = a0 & ~(uintptr_t)15;
-        const uint32_t bytes = nh ? (uint32_t)(a0 - i0) + (nh - 1u) * st + len : 0u;
+        const uint32_t bytes = (uint32_t)(a0 - i0) + (nh - 1u) * st + len;
         const __amdgpu_buffer_rsrc_t r = rsrc(reinterpret_cast<const void*>(i0), (bytes + 15u) & ~15u);
 #pragma unroll
         for (int p = 0; p < P; ++p) {
@@ -98,19 +99,27 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
         }
     };
 
-    // Prologue: S-1 tiles, each followed by H dropped stores (out-of-range offset), so that from the
-    // first iteration on exactly (S-1)(P+H) VMEM ops are younger than the tile being consumed.
+    // Prologue: the first S-1 tiles (those that exist).
 #pragma unroll
     for (int j = 0; j < S - 1; ++j) {
-        issue((uint32_t)j);
-#pragma unroll
-        for (int hh = 0; hh < H; ++hh) {                       // distinct offsets: no store merging
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, ro, (int)(kOOB + 2u * (uint32_t)(j * H + hh)), 0, 0);
+        if ((uint32_t)j < cnt) {
+            issue((uint32_t)j);
         }
     }
     for (uint32_t i = 0; i < cnt; ++i) {
-        issue(i + (uint32_t)S - 1u);
-        wait_vm<(S - 1) * (P + H)>();                         // tile i landed in LDS
+        if (i + (uint32_t)S - 1u < cnt) {
+            issue(i + (uint32_t)S - 1u);
+        }
+        const uint32_t m = min((uint32_t)S - 1u, cnt - 1u - i);   // real tiles issued after tile i
+        if (m == (uint32_t)S - 1u) {                          // tile i landed in LDS
+            wait_vm<(S - 1) * P>();
+        } else if (m == 2u) {
+            wait_vm<(S > 3 ? 2 : 0) * P>();
+        } else if (m == 1u) {
+            wait_vm<(S > 2 ? 1 : 0) * P>();
+        } else {
+            wait_vm<0>();
+        }
         const uint32_t slot = i % (uint32_t)S;
         const uint32_t h0 = (t0 + i * W) * TH;
         const uint32_t nh = min(TH, n - h0);
@@ -142,7 +151,6 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // image reads done before the slot refills
     }
-    wait_vm<0>();                                              // trailing dummy DMA
 }
 
 template <int P, int S, int H>
@@ -175,15 +183,16 @@ int hdr_lanes_h(const SegBatchArgs& a, int h) {
 #define NETCSUM_HDR_LIST(X) \
     X(1, 2, 1) X(1, 3, 1) X(1, 4, 1) X(2, 2, 1) X(2, 3, 1) X(2, 4, 1) X(3, 2, 1) X(3, 3, 1) X(3, 4, 1) \
     X(4, 2, 1) X(4, 3, 1) X(4, 4, 1) X(5, 2, 1) X(5, 3, 1) X(5, 4, 1)                                  \
-    X(1, 2, 2) X(1, 3, 2) X(2, 2, 2) X(2, 3, 2) X(3, 2, 2) X(3, 3, 2) X(4, 2, 2) X(4, 3, 2)            \
-    X(5, 2, 2) X(5, 3, 2) X(6, 2, 2) X(6, 3, 2)                                                        \
-    X(1, 2, 4) X(2, 2, 4) X(3, 2, 4) X(4, 2, 4) X(5, 2, 4) X(6, 2, 4)
+    X(1, 2, 2) X(1, 3, 2) X(1, 4, 2) X(2, 2, 2) X(2, 3, 2) X(2, 4, 2) X(3, 2, 2) X(3, 3, 2) X(3, 4, 2) \
+    X(4, 2, 2) X(4, 3, 2) X(4, 4, 2) X(5, 2, 2) X(5, 3, 2) X(5, 4, 2) X(6, 2, 2) X(6, 3, 2) X(6, 4, 2) \
+    X(1, 2, 4) X(1, 3, 4) X(2, 2, 4) X(2, 3, 4) X(3, 2, 4) X(3, 3, 4) X(4, 2, 4) X(4, 3, 4)            \
+    X(5, 2, 4) X(5, 3, 4) X(6, 2, 4) X(6, 3, 4)
 
-// Resident 256-thread blocks per CU. stages 2..4 (H = 2: 2..3, H = 4: 2).
+// Resident 256-thread blocks per CU. stages 2..4 (H = 4: 2..3).
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h) {
     h = hdr_lanes_h(a, h);
     const uint32_t p = hdr_pieces(a, h);
-    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 1 ? 4 : (h == 2 ? 3 : 2));
+    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 4 ? 3 : 4);
     int occ = 0;
     hipError_t e = hipErrorInvalidValue;
 #define NETCSUM_H(P_, S_, H_) \
@@ -197,7 +206,7 @@ hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, 
     if (!hdr_supported(a)) return hipErrorInvalidValue;
     h = hdr_lanes_h(a, h);
     const uint32_t p = hdr_pieces(a, h);
-    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 1 ? 4 : (h == 2 ? 3 : 2));
+    const int S = std::min(stages == 3 ? 3 : (stages == 4 ? 4 : 2), h == 4 ? 3 : 4);
 #define NETCSUM_H(P_, S_, H_) \
     if (p == P_ && S == S_ && h == H_) return launch_hdr_t<P_, S_, H_>(a, grid, s);
     NETCSUM_HDR_LIST(NETCSUM_H)

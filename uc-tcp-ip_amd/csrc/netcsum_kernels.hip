@@ -964,7 +964,7 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     const int kid = (c.kernel >= 1 && c.kernel <= 7) ? c.kernel : 0;
     if (kid == 7) {
         const int h = hdr_lanes_h(a, c.tile);
-        const int smax = h == 1 ? 4 : (h == 2 ? 3 : 2);          // stages the H instantiations exist for
+        const int smax = h == 4 ? 3 : 4;                          // stages the H instantiations exist for
         snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<S=%d,H=%d> block=256 grid=%d",
                  c.chunks_per_pass < smax ? c.chunks_per_pass : smax, h, c.grid);
         return;
