@@ -142,10 +142,14 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
                       f"= same source -O3 -march=native on {threads} threads"}
 
 
+CURRENT_PMC = "r1m_pmc.json"   # newest FETCH_SIZE/WRITE_SIZE summary of the default bench kernel
+
+
 def load_traffic(path, n_seg, kernel_fn):
     """HBM bytes per launch of THIS kernel form at this size, from the newest matching PMC summary."""
-    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")),
-                                       key=os.path.getmtime)
+    # The current summary first (file mtimes are arbitrary in a fresh checkout), then any other.
+    cands = [path] if path else (sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))) +
+                                 [os.path.join(REPO, "profiles", CURRENT_PMC)])
     for p in reversed(cands):
         try:
             d = json.load(open(p))
