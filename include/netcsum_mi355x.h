@@ -166,6 +166,7 @@ NET_ERR  NetUtil_MI355X_ChkSumBatchStridedHost(const void  *h_seg,
 #define NETCSUM_PKT_MALFORMED     0x10u
 #define NETCSUM_PKT_FRAGMENT      0x20u
 #define NETCSUM_PKT_L4_MALFORMED  0x40u
+#define NETCSUM_PKT_EXT_HDR       0x80u   /* IPv6 only: next header is an extension header */
 
 NET_ERR  NetUtil_MI355X_RxValidateIPv4     (const void      *d_base,
                                             const uint64_t  *d_off,
@@ -177,6 +178,42 @@ NET_ERR  NetUtil_MI355X_RxValidateIPv4     (const void      *d_base,
                                             void            *hip_stream);
 
 NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            int              udp_tx_csum,
+                                            void            *hip_stream);
+
+/* ============================================================================================
+ * (2b') IPv6 packet batches (the 40-B pseudo-header of net_ipv6.h:844-852). Same
+ * layout and arguments as (2b); packet i starts at its 40-B IPv6 header. Flags:
+ *   IP_OK       header well-formed (version 6, 40 + payload length <= bytes present); IPv6 has no
+ *               header checksum (MALFORMED otherwise)
+ *   L4_CHECKED / L4_OK / UDP_NO_CSUM / L4_MALFORMED   as (2b), for a transport header directly after
+ *               the IPv6 header, pseudo-header {src, dst, payload length, 0, next header}:
+ *               TCP (net_tcp.c:7871-7879), UDP (net_udp.c:1947-1957), ICMPv6 (58): types 128-131 and
+ *               134-137 with the pseudo-header (net_icmpv6.c:2923-2942); types 1, 3, 4 HdrVerify over
+ *               the message alone, as the reference does (net_icmpv6.c:2910-2920); other types get no
+ *               verdict (the reference rejects them before any checksum, net_icmpv6.c:2945)
+ *   EXT_HDR     next header is an IPv6 extension header (0, 43, 44, 50, 51, 60, 135, 139, 140, 253,
+ *               254): no transport verdict in the batch
+ * TxFinalizeIPv6 writes the TCP / UDP / ICMPv6 checksum in place (net_tcp.c:29839-29862,
+ *   net_udp.c:2909-2937, net_icmpv6.c:1439 and :949-965); UDP 0x0000 -> 0xFFFF, udp_tx_csum = 0
+ *   writes 0; no header checksum to write.
+ * ============================================================================================ */
+NET_ERR  NetUtil_MI355X_RxValidateIPv6     (const void      *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            void            *hip_stream);
+
+NET_ERR  NetUtil_MI355X_TxFinalizeIPv6     (void            *d_base,
                                             const uint64_t  *d_off,
                                             const uint16_t  *d_len,
                                             uint64_t         stride,

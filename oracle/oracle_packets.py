@@ -138,3 +138,124 @@ def tx_finalize(pkt: bytes, udp_tx_csum: bool = True):
     c, _ = oracle.hdr_calc(hb.ptr, hlen)
     pkt[10:12] = c.to_bytes(2, "little")
     return bytes(pkt), f | IP_OK
+
+
+# ---------------------------------------------------------------------------------------------
+# IPv6 (40-B fixed header). Pseudo-header {src(16), dst(16), upper-layer length (32), zero (16),
+# next header (16, network order)} = NET_IPv6_PSEUDO_HDR (net_ipv6.h:844-852), as the call sites fill it:
+#   TCP     Rx DataVerify(NET_BUF{TCP_V6}, pseudo{.., 6}, 40)         net_tcp.c:7871-7879
+#           Tx DataCalc                                               net_tcp.c:29839-29862
+#   UDP     Rx field 0 -> accepted, no checksum; else DataVerify      net_udp.c:1940-1957, 1971
+#           Tx DataCalc, 0 -> 0xFFFF; disabled -> 0                   net_udp.c:2909-2937
+#   ICMPv6  Rx types 1, 3, 4: HdrVerify(msg, len) -- no pseudo-header net_icmpv6.c:2910-2920
+#              types 128-131, 134-137: DataVerify(NET_BUF{ICMP_V6}, pseudo{.., 58}, 40)  :2923-2942
+#              other types: rejected before the checksum (no verdict) :2945-2948
+#           Tx DataCalc(NET_BUF{ICMP_V6}, pseudo, 40) for every type   net_icmpv6.c:1439 (the error
+#              messages' ~HdrCalc(pseudo) field trick, :949-965, is tested equal in tests/)
+# Extension headers (next header 0, 43, 44, 50, 51, 60, 135, 139, 140, 253, 254) -> EXT_HDR only.
+# ---------------------------------------------------------------------------------------------
+EXT_HDR = 128
+IPV6_EXT = {0, 43, 44, 50, 51, 60, 135, 139, 140, 253, 254}
+ICMPV6_PSEUDO_TYPES = {128, 129, 130, 131, 134, 135, 136, 137}
+ICMPV6_NOPSEUDO_TYPES = {1, 3, 4}
+
+
+def _parse6(pkt: bytes):
+    if len(pkt) < 40 or pkt[0] >> 4 != 6:
+        return None
+    plen = struct.unpack("!H", pkt[4:6])[0]
+    if 40 + plen > len(pkt):
+        return None
+    return plen, pkt[6], pkt[8:40]
+
+
+def pseudo6(addrs: bytes, length: int, nh: int) -> bytes:
+    return addrs + struct.pack("!IHH", length, 0, nh)
+
+
+def _l4_chain6(pkt: bytes, proto_type: int, l4len: int, icmp=False):
+    if icmp:
+        return netcsum.Chain([{"data": pkt, "proto": proto_type, "icmp_ix": 40, "icmp_hdr_len": 0,
+                               "data_len": l4len}])
+    return netcsum.Chain([{"data": pkt, "proto": proto_type, "transport_ix": 40, "transport_hdr_len": 0,
+                           "data_len": l4len}])
+
+
+def rx_validate_v6(pkt: bytes) -> int:
+    pkt = bytes(pkt)
+    p = _parse6(pkt)
+    if p is None:
+        return MALFORMED
+    plen, nh, addrs = p
+    f = IP_OK
+    if nh == 6:
+        if plen < 20:
+            return f | L4_MALFORMED
+        ch = _l4_chain6(pkt, netcsum.NET_PROTOCOL_TYPE_TCP_V6, plen)
+        ph = netcsum.HostBytes(pseudo6(addrs, plen, 6))
+        v, _ = oracle.data_verify(ch.ptr, ph.ptr, 40)
+        return f | L4_CHECKED | (L4_OK if v else 0)
+    if nh == 17:
+        if plen < 8:
+            return f | L4_MALFORMED
+        if struct.unpack("!H", pkt[44:46])[0] != plen:
+            return f | L4_MALFORMED
+        if pkt[46:48] == b"\x00\x00":
+            return f | UDP_NO_CSUM | L4_OK
+        ch = _l4_chain6(pkt, netcsum.NET_PROTOCOL_TYPE_UDP_V6, plen)
+        ph = netcsum.HostBytes(pseudo6(addrs, plen, 17))
+        v, _ = oracle.data_verify(ch.ptr, ph.ptr, 40)
+        return f | L4_CHECKED | (L4_OK if v else 0)
+    if nh == 58:
+        if plen < 4:
+            return f | L4_MALFORMED
+        t = pkt[40]
+        if t in ICMPV6_NOPSEUDO_TYPES:
+            hb = netcsum.HostBytes(pkt[40:40 + plen])
+            v, _ = oracle.hdr_verify(hb.ptr, plen)
+        elif t in ICMPV6_PSEUDO_TYPES:
+            ch = _l4_chain6(pkt, netcsum.NET_PROTOCOL_TYPE_ICMP_V6, plen, icmp=True)
+            ph = netcsum.HostBytes(pseudo6(addrs, plen, 58))
+            v, _ = oracle.data_verify(ch.ptr, ph.ptr, 40)
+        else:
+            return f
+        return f | L4_CHECKED | (L4_OK if v else 0)
+    return f | (EXT_HDR if nh in IPV6_EXT else 0)
+
+
+def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True):
+    """-> (finalized packet bytes, flags)."""
+    pkt = bytearray(pkt)
+    p = _parse6(bytes(pkt))
+    if p is None:
+        return bytes(pkt), MALFORMED
+    plen, nh, addrs = p
+    f = IP_OK
+
+    def calc(proto_type, nhv, icmp=False):
+        ch = _l4_chain6(bytes(pkt), proto_type, plen, icmp)
+        ph = netcsum.HostBytes(pseudo6(addrs, plen, nhv))
+        c, _ = oracle.data_calc(ch.ptr, ph.ptr, 40)
+        return c
+
+    if nh == 6 and plen >= 20:
+        pkt[56:58] = b"\x00\x00"
+        pkt[56:58] = calc(netcsum.NET_PROTOCOL_TYPE_TCP_V6, 6).to_bytes(2, "little")
+        f |= L4_CHECKED | L4_OK
+    elif nh == 17 and plen >= 8 and struct.unpack("!H", bytes(pkt[44:46]))[0] == plen:
+        pkt[46:48] = b"\x00\x00"
+        if udp_tx_csum:
+            c = calc(netcsum.NET_PROTOCOL_TYPE_UDP_V6, 17)
+            pkt[46:48] = (c or 0xFFFF).to_bytes(2, "little")
+            f |= L4_CHECKED | L4_OK
+        else:
+            f |= UDP_NO_CSUM
+    elif nh == 58 and plen >= 4:
+        pkt[42:44] = b"\x00\x00"
+        pkt[42:44] = calc(netcsum.NET_PROTOCOL_TYPE_ICMP_V6, 58, icmp=True).to_bytes(2, "little")
+        f |= L4_CHECKED | L4_OK
+    elif nh in (6, 17, 58):
+        f |= L4_MALFORMED
+    elif nh in IPV6_EXT:
+        f |= EXT_HDR
+    return bytes(pkt), f

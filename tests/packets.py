@@ -84,3 +84,54 @@ def packed_batch(pkts, rng: random.Random, trailer=True, lead=1):
     parts.append(bytes(64))
     buf = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
     return buf, np.array(offs, np.uint64), np.array(lens, np.uint16)
+
+
+KINDS6 = ["tcp", "tcp", "udp", "udp", "udp0", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other", "ext",
+          "other", "bad_ver", "bad_plen", "udp_badlen", "tcp_short", "corrupt_l4"]
+
+
+def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) -> bytes:
+    """Random IPv6 datagram of one kind, finalized by the packet oracle (except the malformed and
+    corrupted kinds). ICMPv6 error messages (types 1, 3, 4) are finalized as the reference's Tx does
+    (pseudo-header included), so its Rx verdict for them (no pseudo-header) is usually a failure."""
+    payload = rng.randint(0, 1600) if payload is None else payload
+    data = rng.randbytes(payload)
+    nh = 6
+    if kind in ("tcp", "tcp_short", "corrupt_l4"):
+        thl = rng.choice([20, 20, 32, 60])
+        l4 = struct.pack("!HHIIBBHHH", rng.getrandbits(16), rng.getrandbits(16), rng.getrandbits(32),
+                         rng.getrandbits(32), (thl // 4) << 4, 0x18, 0xFFFF, 0, 0) + bytes(thl - 20) + data
+        if kind == "tcp_short":
+            l4 = l4[:rng.randint(0, 19)]
+    elif kind in ("udp", "udp0", "udp_badlen"):
+        nh = 17
+        ulen = 8 + len(data)
+        if kind == "udp_badlen":
+            ulen = (ulen + rng.choice([-3, -1, 1, 5])) & 0xFFFF
+        l4 = struct.pack("!HHHH", rng.getrandbits(16), rng.getrandbits(16), ulen, 0) + data
+    elif kind.startswith("icmp"):
+        nh = 58
+        t = {"icmp_echo": rng.choice([128, 129]), "icmp_err": rng.choice([1, 3, 4]),
+             "icmp_nd": rng.choice([130, 131, 134, 135, 136, 137]),
+             "icmp_other": rng.choice([2, 132, 133, 143, 200])}[kind]
+        l4 = struct.pack("!BBH", t, rng.getrandbits(8), 0) + data
+    elif kind == "ext":
+        nh = rng.choice(sorted(op.IPV6_EXT))
+        l4 = data
+    else:
+        nh = rng.choice([4, 41, 47, 89, 132, 59])
+        l4 = data
+    hdr = struct.pack("!IHBB16s16s", (6 << 28) | rng.getrandbits(20), len(l4), nh, 64, rng.randbytes(16),
+                      rng.randbytes(16))
+    pkt = hdr + l4
+    if kind not in ("bad_ver", "bad_plen"):
+        pkt, _ = op.tx_finalize_v6(pkt, udp_tx_csum=(kind != "udp0"))
+    b = bytearray(pkt)
+    if kind == "bad_ver":
+        b[0] = (rng.choice([0, 4, 15]) << 4) | (b[0] & 0xF)
+    if kind == "bad_plen":
+        b[4:6] = struct.pack("!H", len(l4) + rng.randint(1, 40))
+    if kind == "corrupt_l4" and len(b) > 60:
+        k = rng.randint(8, len(b) - 1)                            # addresses are covered too
+        b[k] ^= 1 << rng.randint(0, 7)
+    return bytes(b)

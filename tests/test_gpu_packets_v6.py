@@ -1,0 +1,143 @@
+"""GPU parity of the IPv6 packet batches (NetUtil_MI355X_RxValidateIPv6 / TxFinalizeIPv6) against
+the IPv6 packet oracle (oracle/oracle_packets.py *_v6, pinned to an independent RFC 8200 checksum in
+tests/test_oracle_packets_v6.py): every packet kind, packed odd-aligned and strided layouts, every lane
+group width, grid-stride and tiled launches, Tx write-back in place."""
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle_packets as op
+from packets import KINDS6, make_packet_v6, packed_batch
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _defaults():
+    def reset():
+        for k in (netcsum.TUNE_GRID_BLOCKS, netcsum.TUNE_GROUP_LANES):
+            netcsum.tune(k, 0)
+        netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+        netcsum.tune(netcsum.TUNE_TILE, -1)
+    reset()
+    yield
+    reset()
+
+
+def _dev(buf, offs, lens):
+    return (torch.from_numpy(buf).to(DEV), torch.from_numpy(offs.view(np.int64)).to(DEV),
+            torch.from_numpy(lens.view(np.int16)).to(DEV))
+
+
+def _rx_gpu(buf, offs, lens):
+    b, o, ln = _dev(buf, offs, lens)
+    f = torch.zeros(len(offs), dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv6(b, len(offs), f, off=o, lens=ln)
+    torch.cuda.synchronize()
+    return f.cpu().numpy()
+
+
+@pytest.mark.parametrize("group", [0, 8, 16, 32, 64])
+@pytest.mark.parametrize("grid,tile", [(0, -1), (3, 0)])
+def test_rx_validate_v6_mixed_varlen(group, grid, tile):
+    rng = random.Random(600 + group * 7 + grid)
+    pkts = [make_packet_v6(rng, rng.choice(KINDS6)) for _ in range(1500)]
+    buf, offs, lens = packed_batch(pkts, rng)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+    netcsum.tune(netcsum.TUNE_TILE, tile)
+    got = _rx_gpu(buf, offs, lens)
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())],
+                    np.uint8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(pkts[i][:48].hex(), int(got[i]), int(want[i])) for i in bad[:5]]
+
+
+def test_rx_validate_v6_strided_c2_shape():
+    """1500-B TCP/IPv6 datagrams, strided (the C2 shape with real IPv6/TCP headers), nt on and off."""
+    rng = random.Random(611)
+    n, L = 4000, 1500
+    buf = np.zeros(n * L + 64, np.uint8)
+    for i in range(n):
+        p = make_packet_v6(rng, rng.choice(["tcp", "tcp", "corrupt_l4", "udp"]), payload=L - 60)[:L]
+        buf[i * L:i * L + len(p)] = np.frombuffer(p, np.uint8)
+    want = np.array([op.rx_validate_v6(bytes(buf[i * L:(i + 1) * L])) for i in range(n)], np.uint8)
+    b = torch.from_numpy(buf).to(DEV)
+    for nt in (-1, 0, 1):
+        netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+        f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.rx_validate_ipv6(b, n, f, stride=L, pkt_len=L)
+        torch.cuda.synchronize()
+        assert np.array_equal(f.cpu().numpy(), want), nt
+
+
+@pytest.mark.parametrize("udp_tx_csum", [True, False])
+@pytest.mark.parametrize("group", [0, 8, 64])
+def test_tx_finalize_v6_varlen_then_rx_accepts(udp_tx_csum, group):
+    rng = random.Random(620 + udp_tx_csum + group)
+    kinds = ["tcp", "udp", "udp", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other", "ext", "other",
+             "udp_badlen", "tcp_short", "bad_ver", "bad_plen"]
+    pkts = []
+    for _ in range(2000):
+        p = bytearray(make_packet_v6(rng, rng.choice(kinds)))
+        if len(p) >= 60 and rng.random() < 0.5:
+            for fo in (42, 46, 56):                               # stale transport checksum fields
+                p[fo:fo + 2] = rng.randbytes(2)
+        pkts.append(bytes(p))
+    buf, offs, lens = packed_batch(pkts, rng)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    b, o, ln = _dev(buf, offs, lens)
+    f = torch.zeros(len(pkts), dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv6(b, len(pkts), f, off=o, lens=ln, udp_tx_csum=udp_tx_csum)
+    torch.cuda.synchronize()
+    out, flags = b.cpu().numpy(), f.cpu().numpy()
+    for i, (off, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        pkt = bytes(buf[off:off + n])
+        want_pkt, want_f = op.tx_finalize_v6(pkt, udp_tx_csum)
+        assert bytes(out[off:off + n]) == want_pkt, (i, pkt[:48].hex())
+        assert flags[i] == want_f, (i, int(flags[i]), want_f)
+    assert np.array_equal(out[:offs[0]], buf[:offs[0]])
+    got = _rx_gpu(out, offs, lens)
+    want = np.array([op.rx_validate_v6(bytes(out[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())],
+                    np.uint8)
+    assert np.array_equal(got, want)
+    tcp_udp = np.array([len(p) >= 48 and p[0] >> 4 == 6 and p[6] in (6, 17) for p in pkts])
+    checked = tcp_udp & ((got & op.L4_CHECKED) != 0)
+    assert checked.sum() > 100 and ((got[checked] & op.L4_OK) != 0).all()
+
+
+@pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (200, 184), (96, 72)])
+@pytest.mark.parametrize("group", [0, 16, 32])
+def test_tx_finalize_v6_strided_vs_oracle(stride, pkt_len, group):
+    """Strided IPv6 Tx: packets finalized exactly as the oracle does, bytes between packets untouched."""
+    rng = random.Random(stride * 5 + pkt_len + group)
+    n = 600
+    kinds = ["tcp", "tcp", "udp", "udp0", "icmp_echo", "icmp_err", "ext", "other", "tcp_short", "bad_ver"]
+    buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
+    for i in range(n):
+        p = make_packet_v6(rng, rng.choice(kinds), payload=rng.randint(0, max(0, pkt_len - 110)))[:pkt_len]
+        buf[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv6(b, n, f, stride=stride, pkt_len=pkt_len)
+    torch.cuda.synchronize()
+    out = b.cpu().numpy()
+    want = buf.copy()
+    want_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        pk, want_f[i] = op.tx_finalize_v6(bytes(buf[i * stride:i * stride + pkt_len]), True)
+        want[i * stride:i * stride + pkt_len] = np.frombuffer(pk, np.uint8)
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, [(int(j), int(j) // stride, int(j) % stride, int(out[j]), int(want[j])) for j in bad[:8]]
+    assert np.array_equal(f.cpu().numpy(), want_f)
+
+
+def test_v6_empty_batch_and_null_flags():
+    b = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    assert netcsum.rx_validate_ipv6(b, 0, None, stride=64, pkt_len=64) == netcsum.NET_UTIL_ERR_NONE
+    assert netcsum.rx_validate_ipv6(b, 1, None, stride=64, pkt_len=64, check=False) != netcsum.NET_UTIL_ERR_NONE

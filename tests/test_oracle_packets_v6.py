@@ -1,0 +1,107 @@
+"""CPU checks of the IPv6 packet oracle (oracle/oracle_packets.py *_v6, tests/packets.py
+make_packet_v6): the restatement agrees with an independent RFC 1071 / RFC 8200 §8.1 checksum written
+here from the RFC text, Tx-finalized packets validate on Rx, the reference's ICMPv6 quirks hold, and
+every malformation class maps to its flag."""
+import random
+import struct
+
+import netcsum
+import oracle
+import oracle_packets as op
+from packets import KINDS6, make_packet_v6
+
+
+def rfc1071(data: bytes) -> int:
+    """Plain RFC 1071: one's-complement of the one's-complement sum of big-endian 16-bit words."""
+    if len(data) & 1:
+        data += b"\x00"
+    s = sum(struct.unpack(f"!{len(data) // 2}H", data))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+def rfc_l4_checksum(pkt: bytes, field: int) -> int:
+    """RFC 8200 §8.1 upper-layer checksum of an IPv6 packet (network-order value), field zeroed."""
+    plen = struct.unpack("!H", pkt[4:6])[0]
+    l4 = bytearray(pkt[40:40 + plen])
+    l4[field:field + 2] = b"\x00\x00"
+    return rfc1071(pkt[8:40] + struct.pack("!IHH", plen, 0, pkt[6]) + bytes(l4))
+
+
+def test_tx_matches_independent_rfc_checksum():
+    rng = random.Random(61)
+    for _ in range(300):
+        kind = rng.choice(["tcp", "udp", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other"])
+        pkt = make_packet_v6(rng, kind, payload=rng.randint(0, 700))
+        field = {6: 16, 17: 6, 58: 2}[pkt[6]]
+        got = struct.unpack("!H", pkt[40 + field:42 + field])[0]
+        want = rfc_l4_checksum(pkt, field)
+        if pkt[6] == 17 and want == 0:
+            want = 0xFFFF
+        assert got == want, kind
+
+
+def test_tx_then_rx_per_kind():
+    rng = random.Random(62)
+    for _ in range(400):
+        kind = rng.choice(["tcp", "udp", "icmp_echo", "icmp_nd", "icmp_other", "ext", "other", "udp0"])
+        f = op.rx_validate_v6(make_packet_v6(rng, kind))
+        assert f & op.IP_OK
+        if kind in ("tcp", "udp", "icmp_echo", "icmp_nd"):
+            assert f == op.IP_OK | op.L4_CHECKED | op.L4_OK, (kind, f)
+        elif kind == "udp0":
+            assert f == op.IP_OK | op.UDP_NO_CSUM | op.L4_OK
+        elif kind == "ext":
+            assert f == op.IP_OK | op.EXT_HDR
+        else:
+            assert f == op.IP_OK, (kind, f)
+
+
+def test_icmpv6_error_types_are_verified_without_pseudo_header():
+    """net_icmpv6.c:2910-2920: types 1/3/4 are checked by HdrVerify over the message alone, so the
+    verdict equals 'RFC 1071 over the message == 0' (a pseudo-header-correct message usually fails)."""
+    rng = random.Random(63)
+    fails = 0
+    for _ in range(200):
+        pkt = make_packet_v6(rng, "icmp_err", payload=rng.randint(0, 300))
+        plen = struct.unpack("!H", pkt[4:6])[0]
+        f = op.rx_validate_v6(pkt)
+        ok = rfc1071(pkt[40:40 + plen]) == 0
+        assert f == op.IP_OK | op.L4_CHECKED | (op.L4_OK if ok else 0)
+        fails += not ok
+    assert fails > 190
+
+
+def test_icmpv6_error_tx_trick_equals_datacalc_with_pseudo():
+    """net_icmpv6.c:949-965 computes error-message checksums as HdrCalc(msg) with the field set to
+    ~HdrCalc(pseudo); the oracle's Tx uses DataCalc(msg, pseudo). Same value."""
+    rng = random.Random(64)
+    for _ in range(200):
+        pkt = make_packet_v6(rng, "icmp_err", payload=rng.randint(0, 300))
+        plen = struct.unpack("!H", pkt[4:6])[0]
+        ph = netcsum.HostBytes(op.pseudo6(pkt[8:40], plen, 58))
+        c1, _ = oracle.hdr_calc(ph.ptr, 40)
+        msg = bytearray(pkt[40:40 + plen])
+        msg[2:4] = ((~c1) & 0xFFFF).to_bytes(2, "little")         # host-order store, as the C does
+        mb = netcsum.HostBytes(bytes(msg))
+        c2, _ = oracle.hdr_calc(mb.ptr, plen)
+        assert c2.to_bytes(2, "little") == pkt[42:44]
+
+
+def test_malformed_and_corrupt_flags():
+    rng = random.Random(65)
+    for _ in range(40):
+        assert op.rx_validate_v6(make_packet_v6(rng, "bad_ver")) == op.MALFORMED
+        assert op.rx_validate_v6(make_packet_v6(rng, "bad_plen")) == op.MALFORMED
+        assert op.rx_validate_v6(make_packet_v6(rng, "udp_badlen")) == op.IP_OK | op.L4_MALFORMED
+        assert op.rx_validate_v6(make_packet_v6(rng, "tcp_short")) == op.IP_OK | op.L4_MALFORMED
+        p = make_packet_v6(rng, "corrupt_l4", payload=rng.randint(30, 500))
+        assert op.rx_validate_v6(p) == op.IP_OK | op.L4_CHECKED
+    assert op.rx_validate_v6(b"\x60" + bytes(38)) == op.MALFORMED
+
+
+def test_every_v6_kind_generates():
+    rng = random.Random(66)
+    for k in KINDS6:
+        assert isinstance(op.rx_validate_v6(make_packet_v6(rng, k)), int)

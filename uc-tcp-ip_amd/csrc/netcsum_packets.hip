@@ -40,7 +40,7 @@ namespace netcsum {
 namespace {
 
 constexpr uint32_t F_IP_OK = 0x01u, F_L4_OK = 0x02u, F_L4_CHECKED = 0x04u, F_UDP_NO_CSUM = 0x08u,
-                   F_MALFORMED = 0x10u, F_FRAGMENT = 0x20u, F_L4_MALFORMED = 0x40u;
+                   F_MALFORMED = 0x10u, F_FRAGMENT = 0x20u, F_L4_MALFORMED = 0x40u, F_EXT_HDR = 0x80u;
 
 template <int K>
 struct PktStage {
@@ -114,13 +114,115 @@ __device__ __forceinline__ uint32_t own_byte(u32x4 v0, uint32_t f, int lane) {
 
 struct PktInfo {
     uint32_t flags;
-    uint32_t hlen;
+    uint32_t hlen;         // IPv4: IP header length. IPv6: bytes before the transport sum's start
+                           // (8: the addresses open the sum; 40: ICMPv6 errors summed without pseudo)
     uint32_t l4_end;       // packet offset one past the transport part
     uint32_t l4_csum_off;  // packet offset of the transport checksum field (~0u: none)
     uint32_t pseudo_le;    // little-endian word sum of the pseudo-header (0: none)
     uint32_t proto;
     bool     check_l4;
 };
+
+__device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+
+// IPv6 (40-B fixed header, RFC 8200): no header checksum; the transport sums take the 40-B
+// pseudo-header {src, dst, upper-layer length (32 bit), 0, next header} of net_ipv6.h:844-852.
+// The addresses are packet bytes [8, 40), contiguous with the transport part, so the transport sum
+// runs over [8, end) and only the length and next-header words are added in registers.
+//   TCP (6)      DataVerify / DataCalc + pseudo                     net_tcp.c:7871-7879, 29839-29850
+//   UDP (17)     as IPv4: 0 = no checksum (Rx), 0 -> 0xFFFF (Tx)    net_udp.c:1947-1957, 2909-2931
+//   ICMPv6 (58)  Rx: types 1, 3, 4 (destination unreachable, time exceeded, parameter problem)
+//                    HdrVerify over the message WITHOUT the pseudo-header  net_icmpv6.c:2910-2920
+//                    types 128-131, 134-137 (echo, MLD, NDP) DataVerify + pseudo  net_icmpv6.c:2923-2942
+//                    other types: rejected before any checksum (INVALID_TYPE)     net_icmpv6.c:2945-2948
+//                Tx: every message through the pseudo-header (DataCalc + pseudo, net_icmpv6.c:1439;
+//                    the error messages' ~HdrCalc(pseudo) field trick, net_icmpv6.c:949-965, gives
+//                    the same value), no 0 -> 0xFFFF substitution
+// Any other next header (extension headers included) gets no transport verdict; the extension
+// header values of RFC 8200 §4 / IANA are flagged EXT_HDR (the stack's ext-header walk,
+// net_ipv6.c, is outside the per-packet batch).
+__device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
+    return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 60u || nh == 135u ||
+           nh == 139u || nh == 140u || nh == 253u || nh == 254u;
+}
+
+template <bool TX>
+__device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
+    PktInfo p{};
+    p.l4_csum_off = ~0u;
+    const uint32_t d0 = pkt_dword(v0, lead, 0u, gbase);
+    const uint32_t d1 = pkt_dword(v0, lead, 4u, gbase);
+    const uint32_t plen = be16_at(d1, 0);
+    const uint32_t tot = 40u + plen;
+    p.proto = (d1 >> 16) & 0xFFu;
+    if (avail < 40u || ((d0 >> 4) & 0xFu) != 6u || tot > avail) {
+        p.flags = F_MALFORMED;
+        p.l4_end = 0u;
+        p.hlen = 0u;
+        return p;
+    }
+    p.l4_end = tot;
+    p.hlen = 8u;
+    const uint32_t pseudo = (p.proto << 8) + swap16(plen);      // length high half is 0 (plen < 2^16)
+    switch (p.proto) {
+    case 6u:
+        if (plen < 20u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = 40u + 16u;
+        p.pseudo_le = pseudo;
+        break;
+    case 17u: {
+        if (plen < 8u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        const uint32_t du = pkt_dword(v0, lead, 44u, gbase);
+        if (be16_at(du, 0) != plen) {                            // net_udp.c:1903-1907
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = 40u + 6u;
+        if (!TX && (du >> 16) == 0u) {
+            p.flags |= F_UDP_NO_CSUM | F_L4_OK;
+            return p;
+        }
+        if (TX && !udp_tx_csum) {
+            p.flags |= F_UDP_NO_CSUM;
+            return p;
+        }
+        p.check_l4 = true;
+        p.pseudo_le = pseudo;
+        break;
+    }
+    case 58u:
+        if (plen < 4u) {
+            p.flags |= F_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = 40u + 2u;
+        if constexpr (TX) {
+            p.check_l4 = true;
+            p.pseudo_le = pseudo;
+        } else {
+            const uint32_t type = pkt_dword(v0, lead, 40u, gbase) & 0xFFu;
+            if (type == 1u || type == 3u || type == 4u) {
+                p.check_l4 = true;
+                p.hlen = 40u;                                    // message alone, no pseudo-header
+            } else if ((type >= 128u && type <= 131u) || (type >= 134u && type <= 137u)) {
+                p.check_l4 = true;
+                p.pseudo_le = pseudo;
+            }
+        }
+        break;
+    default:
+        p.flags |= ipv6_ext_hdr(p.proto) ? F_EXT_HDR : 0u;
+        break;
+    }
+    return p;
+}
 
 template <bool TX>
 __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
@@ -271,7 +373,7 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
     }
 }
 
-template <int G, int K, bool NT, bool TX>
+template <int G, int K, bool NT, bool TX, bool V6>
 __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
                                                 int lane, int gbase) {
     // One sum over [lead, lead + end) (end = transport end, or the IP header end when the transport
@@ -286,7 +388,8 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     // lane afterwards (low_bytes), instead of masking every chunk: the packet kernels are VALU-issue
     // bound (profiles/r1txp_pmc.json), and per-chunk edge masks executed on every k slot dominated.
     const uint32_t lead = st.lead;
-    PktInfo p = pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
+    PktInfo p = V6 ? pkt_parse_v6<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
+                   : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
     const uint32_t nch = (rend + 15u) >> 4;
@@ -332,7 +435,7 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     }
     uint32_t acc_ip = ip_raw, acc_l4 = acc - ip_raw;
     if (TX) {
-        if (!(p.flags & F_MALFORMED)) {
+        if (!V6 && !(p.flags & F_MALFORMED)) {
             acc_ip -= own_byte(st.v[0], lead + 10u, lane) + own_byte(st.v[0], lead + 11u, lane);
         }
         if (p.check_l4) {
@@ -351,12 +454,14 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     uint32_t cip = ~0u, cl4 = ~0u;                               // Tx values to store; ~0u = none
     if (!(f & F_MALFORMED)) {
         if constexpr (!TX) {
-            f |= (sip == 0xFFFFu) ? F_IP_OK : 0u;
+            f |= (V6 || sip == 0xFFFFu) ? F_IP_OK : 0u;          // IPv6: well-formed (no header checksum)
             if (p.check_l4) {
                 f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
             }
         } else {
-            cip = (~sip) & 0xFFFFu;                              // net_ipv4.c:9578-9586
+            if constexpr (!V6) {
+                cip = (~sip) & 0xFFFFu;                          // net_ipv4.c:9578-9586
+            }
             f |= F_IP_OK;
             if (p.check_l4) {
                 cl4 = (~sl4) & 0xFFFFu;
@@ -392,7 +497,7 @@ __device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint
 
 // 4 waves per SIMD: the Tx instantiations otherwise take 131 VGPRs (3 waves), 25 % less memory
 // parallelism than Rx (122 VGPRs); capped at 128 they do not spill (profiles/r1txp_pmc.json).
-template <int G, int K, bool VARLEN, bool NT, bool TX>
+template <int G, int K, bool VARLEN, bool NT, bool TX, bool V6>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pkt_batch_kernel(PktBatchArgs A) {
     static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
     const int lane = (int)(threadIdx.x & (G - 1));
@@ -432,7 +537,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);                      // previous packet's stores, after the loads
         pin_chunks<K>(S0.v);
-        pend = pkt_consume<G, K, NT, TX>(S0, A, i, v0, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX, V6>(S0, A, i, v0, lane, gbase);
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
@@ -440,13 +545,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);
         pin_chunks<K>(S1.v);
-        pend = pkt_consume<G, K, NT, TX>(S1, A, i, v1, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX, V6>(S1, A, i, v1, lane, gbase);
         i = nx;
     }
     pkt_store<G, TX, !VARLEN>(pend, A);
 }
 
-template <int G, int K, bool VARLEN, bool TX>
+template <int G, int K, bool VARLEN, bool TX, bool V6>
 hipError_t launch_pkt_gk(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
     const uint32_t gpb = 256u / G;
     int grid;
@@ -457,33 +562,38 @@ hipError_t launch_pkt_gk(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t 
         grid = c.grid > 0 ? c.grid : (int)(((uint64_t)a.n + gpb - 1u) / gpb);
     }
     if (c.nt) {
-        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, true, TX>), dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, true, TX, V6>), dim3(grid), dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, false, TX>), dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, false, TX, V6>), dim3(grid), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }
 
-template <bool VARLEN, bool TX>
+template <bool VARLEN, bool TX, bool V6>
 hipError_t launch_pkt_v(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
     switch (c.group_lanes) {
-    case 8:  return c.chunks_per_pass <= 4 ? launch_pkt_gk<8, 4, VARLEN, TX>(a, c, s)
-                                           : launch_pkt_gk<8, 8, VARLEN, TX>(a, c, s);
-    case 16: return c.chunks_per_pass <= 3 ? launch_pkt_gk<16, 3, VARLEN, TX>(a, c, s)
-                                           : launch_pkt_gk<16, 6, VARLEN, TX>(a, c, s);
-    case 32: return c.chunks_per_pass <= 3 ? launch_pkt_gk<32, 3, VARLEN, TX>(a, c, s)
-                                           : launch_pkt_gk<32, 6, VARLEN, TX>(a, c, s);
-    default: return launch_pkt_gk<64, 4, VARLEN, TX>(a, c, s);
+    case 8:  return c.chunks_per_pass <= 4 ? launch_pkt_gk<8, 4, VARLEN, TX, V6>(a, c, s)
+                                           : launch_pkt_gk<8, 8, VARLEN, TX, V6>(a, c, s);
+    case 16: return c.chunks_per_pass <= 3 ? launch_pkt_gk<16, 3, VARLEN, TX, V6>(a, c, s)
+                                           : launch_pkt_gk<16, 6, VARLEN, TX, V6>(a, c, s);
+    case 32: return c.chunks_per_pass <= 3 ? launch_pkt_gk<32, 3, VARLEN, TX, V6>(a, c, s)
+                                           : launch_pkt_gk<32, 6, VARLEN, TX, V6>(a, c, s);
+    default: return launch_pkt_gk<64, 4, VARLEN, TX, V6>(a, c, s);
     }
+}
+
+template <bool V6>
+hipError_t launch_pkt_ver(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
+    if (a.off) {
+        return tx ? launch_pkt_v<true, true, V6>(a, c, s) : launch_pkt_v<true, false, V6>(a, c, s);
+    }
+    return tx ? launch_pkt_v<false, true, V6>(a, c, s) : launch_pkt_v<false, false, V6>(a, c, s);
 }
 
 }  // namespace
 
-hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
-    if (a.off) {
-        return tx ? launch_pkt_v<true, true>(a, c, s) : launch_pkt_v<true, false>(a, c, s);
-    }
-    return tx ? launch_pkt_v<false, true>(a, c, s) : launch_pkt_v<false, false>(a, c, s);
+hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, bool ipv6, hipStream_t s) {
+    return ipv6 ? launch_pkt_ver<true>(a, c, tx, s) : launch_pkt_ver<false>(a, c, tx, s);
 }
 
 }  // namespace netcsum
