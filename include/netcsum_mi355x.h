@@ -198,8 +198,14 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
  *               134-137 with the pseudo-header (net_icmpv6.c:2923-2942); types 1, 3, 4 HdrVerify over
  *               the message alone, as the reference does (net_icmpv6.c:2910-2920); other types get no
  *               verdict (the reference rejects them before any checksum, net_icmpv6.c:2945)
- *   EXT_HDR     next header is an IPv6 extension header (0, 43, 44, 50, 51, 60, 135, 139, 140, 253,
- *               254): no transport verdict in the batch
+ *   Extension headers: Hop-by-Hop (0, first only), Routing (43) and Destination Options (60) are
+ *               skipped (up to 4; upper-layer length = payload length - their bytes, net_ipv6.c:5682)
+ *               while the chain and the transport fields lie in the first 16*G - (address % 16) bytes
+ *               of the packet (G = the launch's lanes per packet: 32 for d_off batches, 8-64 by
+ *               pkt_len for strided ones, or NETCSUM_TUNE_GROUP_LANES); a Fragment header (44) gives
+ *               FRAGMENT; a header running past the payload gives MALFORMED
+ *   EXT_HDR     any other extension header (50, 51, 59, 135, 139, 140, 253, 254), a late Hop-by-Hop
+ *               header, or a chain past that window: no transport verdict in the batch
  * TxFinalizeIPv6 writes the TCP / UDP / ICMPv6 checksum in place (net_tcp.c:29839-29862,
  *   net_udp.c:2909-2937, net_icmpv6.c:1439 and :949-965); UDP 0x0000 -> 0xFFFF, udp_tx_csum = 0
  *   writes 0; no header checksum to write.

@@ -152,42 +152,67 @@ def tx_finalize(pkt: bytes, udp_tx_csum: bool = True):
 #              other types: rejected before the checksum (no verdict) :2945-2948
 #           Tx DataCalc(NET_BUF{ICMP_V6}, pseudo, 40) for every type   net_icmpv6.c:1439 (the error
 #              messages' ~HdrCalc(pseudo) field trick, :949-965, is tested equal in tests/)
-# Extension headers (next header 0, 43, 44, 50, 51, 60, 135, 139, 140, 253, 254) -> EXT_HDR only.
+# Extension headers (net_ipv6.c:8290-8360): Hop-by-Hop (0, first only), Routing (43), Destination
+# Options (60), length (HdrExtLen + 1) * 8 (net_ipv6.c:8601), are skipped -- up to 4, and only while
+# the chain and the transport fields (transport offset + 24) lie within the first `window` bytes of
+# the packet's frame (the batch kernel's first-pass chunks; window(G, lead) = 16 G - lead) -- and the
+# upper-layer length becomes payload - extension bytes (net_ipv6.c:5682). Fragment (44) -> FRAGMENT;
+# an extension header past the payload -> MALFORMED; any other extension header, a Hop-by-Hop
+# header after the first, or a chain beyond the window -> EXT_HDR. No transport verdict for those.
 # ---------------------------------------------------------------------------------------------
 EXT_HDR = 128
-IPV6_EXT = {0, 43, 44, 50, 51, 60, 135, 139, 140, 253, 254}
+IPV6_EXT = {0, 43, 44, 50, 51, 59, 60, 135, 139, 140, 253, 254}
 ICMPV6_PSEUDO_TYPES = {128, 129, 130, 131, 134, 135, 136, 137}
 ICMPV6_NOPSEUDO_TYPES = {1, 3, 4}
 
 
-def _parse6(pkt: bytes):
+def _parse6(pkt: bytes, window: int = 1 << 30):
+    """-> None (malformed) or (flags_so_far, transport offset, upper-layer length, next header, addrs)."""
     if len(pkt) < 40 or pkt[0] >> 4 != 6:
         return None
     plen = struct.unpack("!H", pkt[4:6])[0]
-    if 40 + plen > len(pkt):
+    tot = 40 + plen
+    if tot > len(pkt):
         return None
-    return plen, pkt[6], pkt[8:40]
+    nh, off = pkt[6], 40
+    for _ in range(4):
+        if nh not in (0, 43, 60):
+            break
+        if (nh == 0 and off != 40) or off + 8 > window:
+            return EXT_HDR, off, 0, nh, pkt[8:40]
+        nh, off = pkt[off], off + (pkt[off + 1] + 1) * 8
+        if off > tot:
+            return None
+    if nh == 44:
+        return FRAGMENT, off, 0, nh, pkt[8:40]
+    if nh in IPV6_EXT or (off != 40 and off + 24 > window):
+        return EXT_HDR, off, 0, nh, pkt[8:40]
+    return 0, off, tot - off, nh, pkt[8:40]
 
 
 def pseudo6(addrs: bytes, length: int, nh: int) -> bytes:
     return addrs + struct.pack("!IHH", length, 0, nh)
 
 
-def _l4_chain6(pkt: bytes, proto_type: int, l4len: int, icmp=False):
+def _l4_chain6(pkt: bytes, proto_type: int, l4len: int, icmp=False, ix=40):
     if icmp:
-        return netcsum.Chain([{"data": pkt, "proto": proto_type, "icmp_ix": 40, "icmp_hdr_len": 0,
+        return netcsum.Chain([{"data": pkt, "proto": proto_type, "icmp_ix": ix, "icmp_hdr_len": 0,
                                "data_len": l4len}])
-    return netcsum.Chain([{"data": pkt, "proto": proto_type, "transport_ix": 40, "transport_hdr_len": 0,
+    return netcsum.Chain([{"data": pkt, "proto": proto_type, "transport_ix": ix, "transport_hdr_len": 0,
                            "data_len": l4len}])
 
 
-def rx_validate_v6(pkt: bytes) -> int:
+def rx_validate_v6(pkt: bytes, window: int = 1 << 30) -> int:
     pkt = bytes(pkt)
-    p = _parse6(pkt)
+    p = _parse6(pkt, window)
     if p is None:
         return MALFORMED
-    plen, nh, addrs = p
-    f = IP_OK
+    fx, off, plen, nh, addrs = p
+    f = IP_OK | fx
+    if fx:
+        return f
+    if off != 40:                              # transport after extension headers
+        pkt = pkt[:40] + pkt[off:]
     if nh == 6:
         if plen < 20:
             return f | L4_MALFORMED
@@ -220,17 +245,24 @@ def rx_validate_v6(pkt: bytes) -> int:
         else:
             return f
         return f | L4_CHECKED | (L4_OK if v else 0)
-    return f | (EXT_HDR if nh in IPV6_EXT else 0)
+    return f
 
 
-def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True):
+def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
     """-> (finalized packet bytes, flags)."""
-    pkt = bytearray(pkt)
-    p = _parse6(bytes(pkt))
+    pkt = bytes(pkt)
+    p = _parse6(pkt, window)
     if p is None:
-        return bytes(pkt), MALFORMED
-    plen, nh, addrs = p
-    f = IP_OK
+        return pkt, MALFORMED
+    fx, off, plen, nh, addrs = p
+    f = IP_OK | fx
+    if fx:
+        return pkt, f
+    if off != 40:                              # finalize the transport part as if it followed the header
+        hdr = pkt[:4] + struct.pack("!HB", plen, nh) + pkt[7:40]
+        body, fl = tx_finalize_v6(hdr + pkt[off:], udp_tx_csum)
+        return pkt[:off] + body[40:], fl
+    pkt = bytearray(pkt)
 
     def calc(proto_type, nhv, icmp=False):
         ch = _l4_chain6(bytes(pkt), proto_type, plen, icmp)
@@ -256,6 +288,4 @@ def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True):
         f |= L4_CHECKED | L4_OK
     elif nh in (6, 17, 58):
         f |= L4_MALFORMED
-    elif nh in IPV6_EXT:
-        f |= EXT_HDR
     return bytes(pkt), f

@@ -87,7 +87,18 @@ def packed_batch(pkts, rng: random.Random, trailer=True, lead=1):
 
 
 KINDS6 = ["tcp", "tcp", "udp", "udp", "udp0", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other", "ext",
-          "other", "bad_ver", "bad_plen", "udp_badlen", "tcp_short", "corrupt_l4"]
+          "other", "bad_ver", "bad_plen", "udp_badlen", "tcp_short", "corrupt_l4", "ext_ok", "ext_ok",
+          "ext_frag", "ext_long", "ext_bad", "ext_hbh_late"]
+EXT_OPAQUE = [50, 51, 59, 135, 139, 140, 253, 254]       # extension headers the batch does not walk
+
+
+def _ext_chain(rng: random.Random, kinds, final_nh: int) -> tuple[int, bytes]:
+    """Extension headers of the given types (units of 8 B each) ending in final_nh -> (first nh, bytes)."""
+    out, nh = b"", final_nh
+    for t, units in reversed(kinds):
+        out = struct.pack("!BB", nh, units - 1) + rng.randbytes(units * 8 - 2) + out
+        nh = t
+    return nh, out
 
 
 def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) -> bytes:
@@ -116,10 +127,29 @@ def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) ->
              "icmp_other": rng.choice([2, 132, 133, 143, 200])}[kind]
         l4 = struct.pack("!BBH", t, rng.getrandbits(8), 0) + data
     elif kind == "ext":
-        nh = rng.choice(sorted(op.IPV6_EXT))
+        nh = rng.choice(EXT_OPAQUE)
         l4 = data
+    elif kind.startswith("ext_"):
+        inner = rng.choice(["tcp", "udp", "icmp_echo", "icmp_err"])
+        body = make_packet_v6(rng, inner, payload)[40:]
+        inner_nh = {"tcp": 6, "udp": 17}.get(inner, 58)
+        if kind == "ext_ok":                                   # <= 48 B: inside every group's window
+            chain = [(0, 1)] if rng.random() < 0.5 else []
+            chain += [(rng.choice([43, 60]), rng.choice([1, 2])) for _ in range(rng.randint(0 if chain else 1, 2))]
+            nh, ext = _ext_chain(rng, chain, inner_nh)
+        elif kind == "ext_frag":
+            nh, ext = _ext_chain(rng, [(60, 1)] * rng.randint(0, 1) + [(44, 1)], inner_nh)
+        elif kind == "ext_long":                               # 1032+ B: beyond every window
+            nh, ext = _ext_chain(rng, [(60, rng.randint(129, 200))], inner_nh)
+        elif kind == "ext_hbh_late":
+            nh, ext = _ext_chain(rng, [(60, 1), (0, 1)], inner_nh)
+        else:                                                  # ext_bad: length past the payload
+            nh, ext = _ext_chain(rng, [(43, 1)], inner_nh)
+            ext = ext[:1] + bytes([rng.randint(20, 255)]) + ext[2:]
+            body = body[:rng.randint(0, 40)]
+        l4 = ext + body
     else:
-        nh = rng.choice([4, 41, 47, 89, 132, 59])
+        nh = rng.choice([4, 41, 47, 89, 132])
         l4 = data
     hdr = struct.pack("!IHBB16s16s", (6 << 28) | rng.getrandbits(20), len(l4), nh, 64, rng.randbytes(16),
                       rng.randbytes(16))
@@ -135,3 +165,9 @@ def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) ->
         k = rng.randint(8, len(b) - 1)                            # addresses are covered too
         b[k] ^= 1 << rng.randint(0, 7)
     return bytes(b)
+
+
+def v6_window(group: int, addr: int) -> int:
+    """Bytes of a packet at device address `addr` that the IPv6 batch kernel's first-pass chunks hold
+    (extension-header chains are walked only inside them): 16 * G - (addr % 16)."""
+    return 16 * group - (addr & 15)

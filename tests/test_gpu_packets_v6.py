@@ -3,13 +3,14 @@ the IPv6 packet oracle (oracle/oracle_packets.py *_v6, pinned to an independent 
 tests/test_oracle_packets_v6.py): every packet kind, packed odd-aligned and strided layouts, every lane
 group width, grid-stride and tiled launches, Tx write-back in place."""
 import random
+import struct
 
 import numpy as np
 import pytest
 
 import netcsum
 import oracle_packets as op
-from packets import KINDS6, make_packet_v6, packed_batch
+from packets import KINDS6, make_packet_v6, packed_batch, v6_window
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -33,6 +34,14 @@ def _dev(buf, offs, lens):
             torch.from_numpy(lens.view(np.int16)).to(DEV))
 
 
+def _auto_group(varlen, pkt_len=0):
+    """The ABI's lane-group choice for packet batches (netcsum_abi.hip pkt_batch)."""
+    if varlen:
+        return 32
+    want = max(1, ((pkt_len + 30) // 16 + 5) // 6)
+    return max(8, next((g for g in (1, 4, 8, 16, 32, 64) if g >= want), 64))
+
+
 def _rx_gpu(buf, offs, lens):
     b, o, ln = _dev(buf, offs, lens)
     f = torch.zeros(len(offs), dtype=torch.uint8, device=DEV)
@@ -51,10 +60,12 @@ def test_rx_validate_v6_mixed_varlen(group, grid, tile):
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
     netcsum.tune(netcsum.TUNE_TILE, tile)
     got = _rx_gpu(buf, offs, lens)
-    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())],
-                    np.uint8)
+    g = group or _auto_group(True)
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]), v6_window(g, o))
+                     for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(pkts[i][:48].hex(), int(got[i]), int(want[i])) for i in bad[:5]]
+    assert (want & op.EXT_HDR).any() and (want & op.FRAGMENT).any()
 
 
 def test_rx_validate_v6_strided_c2_shape():
@@ -80,7 +91,8 @@ def test_rx_validate_v6_strided_c2_shape():
 def test_tx_finalize_v6_varlen_then_rx_accepts(udp_tx_csum, group):
     rng = random.Random(620 + udp_tx_csum + group)
     kinds = ["tcp", "udp", "udp", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other", "ext", "other",
-             "udp_badlen", "tcp_short", "bad_ver", "bad_plen"]
+             "udp_badlen", "tcp_short", "bad_ver", "bad_plen", "ext_ok", "ext_ok", "ext_frag", "ext_long",
+             "ext_bad", "ext_hbh_late"]
     pkts = []
     for _ in range(2000):
         p = bytearray(make_packet_v6(rng, rng.choice(kinds)))
@@ -95,19 +107,20 @@ def test_tx_finalize_v6_varlen_then_rx_accepts(udp_tx_csum, group):
     netcsum.tx_finalize_ipv6(b, len(pkts), f, off=o, lens=ln, udp_tx_csum=udp_tx_csum)
     torch.cuda.synchronize()
     out, flags = b.cpu().numpy(), f.cpu().numpy()
+    g = group or _auto_group(True)
     for i, (off, n) in enumerate(zip(offs.tolist(), lens.tolist())):
         pkt = bytes(buf[off:off + n])
-        want_pkt, want_f = op.tx_finalize_v6(pkt, udp_tx_csum)
+        want_pkt, want_f = op.tx_finalize_v6(pkt, udp_tx_csum, v6_window(g, off))
         assert bytes(out[off:off + n]) == want_pkt, (i, pkt[:48].hex())
         assert flags[i] == want_f, (i, int(flags[i]), want_f)
     assert np.array_equal(out[:offs[0]], buf[:offs[0]])
     got = _rx_gpu(out, offs, lens)
-    want = np.array([op.rx_validate_v6(bytes(out[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())],
-                    np.uint8)
+    want = np.array([op.rx_validate_v6(bytes(out[o:o + n]), v6_window(g, o))
+                     for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     assert np.array_equal(got, want)
     tcp_udp = np.array([len(p) >= 48 and p[0] >> 4 == 6 and p[6] in (6, 17) for p in pkts])
     checked = tcp_udp & ((got & op.L4_CHECKED) != 0)
-    assert checked.sum() > 100 and ((got[checked] & op.L4_OK) != 0).all()
+    assert checked.sum() > 50 and ((got[checked] & op.L4_OK) != 0).all()
 
 
 @pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (200, 184), (96, 72)])
@@ -116,13 +129,16 @@ def test_tx_finalize_v6_strided_vs_oracle(stride, pkt_len, group):
     """Strided IPv6 Tx: packets finalized exactly as the oracle does, bytes between packets untouched."""
     rng = random.Random(stride * 5 + pkt_len + group)
     n = 600
-    kinds = ["tcp", "tcp", "udp", "udp0", "icmp_echo", "icmp_err", "ext", "other", "tcp_short", "bad_ver"]
+    kinds = ["tcp", "tcp", "udp", "udp0", "icmp_echo", "icmp_err", "ext", "other", "tcp_short", "bad_ver",
+             "ext_ok", "ext_frag", "ext_hbh_late"]
     buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
     for i in range(n):
         p = make_packet_v6(rng, rng.choice(kinds), payload=rng.randint(0, max(0, pkt_len - 110)))[:pkt_len]
         buf[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
     netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    g = group or _auto_group(False, pkt_len)
     b = torch.from_numpy(buf).to(DEV)
+    assert b.data_ptr() % 64 == 0
     f = torch.zeros(n, dtype=torch.uint8, device=DEV)
     netcsum.tx_finalize_ipv6(b, n, f, stride=stride, pkt_len=pkt_len)
     torch.cuda.synchronize()
@@ -130,7 +146,8 @@ def test_tx_finalize_v6_strided_vs_oracle(stride, pkt_len, group):
     want = buf.copy()
     want_f = np.zeros(n, np.uint8)
     for i in range(n):
-        pk, want_f[i] = op.tx_finalize_v6(bytes(buf[i * stride:i * stride + pkt_len]), True)
+        pk, want_f[i] = op.tx_finalize_v6(bytes(buf[i * stride:i * stride + pkt_len]), True,
+                                          v6_window(g, i * stride))
         want[i * stride:i * stride + pkt_len] = np.frombuffer(pk, np.uint8)
     bad = np.nonzero(out != want)[0]
     assert bad.size == 0, [(int(j), int(j) // stride, int(j) % stride, int(out[j]), int(want[j])) for j in bad[:8]]
@@ -141,3 +158,28 @@ def test_v6_empty_batch_and_null_flags():
     b = torch.zeros(64, dtype=torch.uint8, device=DEV)
     assert netcsum.rx_validate_ipv6(b, 0, None, stride=64, pkt_len=64) == netcsum.NET_UTIL_ERR_NONE
     assert netcsum.rx_validate_ipv6(b, 1, None, stride=64, pkt_len=64, check=False) != netcsum.NET_UTIL_ERR_NONE
+
+
+@pytest.mark.parametrize("group", [8, 16, 64])
+def test_rx_v6_extension_chains_at_the_window_edge(group):
+    """Extension-header chains of every length around the group's window (16 G bytes of the frame
+    minus the packet's lead): walked when the transport fields fit, EXT_HDR when they do not, at
+    every lead 0-15."""
+    rng = random.Random(700 + group)
+    pkts = []
+    for units in range(1, 2 * group + 5):
+        for _ in range(3):
+            inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 200))
+            nh_in = inner[6]
+            ext = struct.pack("!BB", nh_in, units - 1) + rng.randbytes(units * 8 - 2)
+            body = ext + inner[40:]
+            hdr = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40]
+            pkts.append(op.tx_finalize_v6(hdr + body)[0])
+    rng.shuffle(pkts)
+    buf, offs, lens = packed_batch(pkts, rng)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    got = _rx_gpu(buf, offs, lens)
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]), v6_window(group, o))
+                     for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
+    assert np.array_equal(got, want)
+    assert (want & op.EXT_HDR).any() and ((want & op.L4_OK) != 0).any()

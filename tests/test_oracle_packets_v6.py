@@ -105,3 +105,31 @@ def test_every_v6_kind_generates():
     rng = random.Random(66)
     for k in KINDS6:
         assert isinstance(op.rx_validate_v6(make_packet_v6(rng, k)), int)
+
+
+def test_extension_headers_walked_and_flagged():
+    """Hop-by-Hop / Routing / Destination Options are skipped (upper-layer length = payload - their
+    bytes), the transport checksum then equals the RFC checksum of the transport part with that
+    length; Fragment -> FRAGMENT; opaque ones, late Hop-by-Hop and over-long chains -> EXT_HDR."""
+    rng = random.Random(67)
+    for _ in range(200):
+        pkt = make_packet_v6(rng, "ext_ok", payload=rng.randint(0, 300))
+        f = op.rx_validate_v6(pkt)
+        assert f & op.IP_OK and not f & (op.EXT_HDR | op.FRAGMENT | op.MALFORMED)
+        fx, off, ulen, nh, _ = op._parse6(pkt)
+        assert fx == 0 and off > 40 and nh in (6, 17, 58)
+        flat = pkt[:4] + struct.pack("!HB", ulen, nh) + pkt[7:40] + pkt[off:]
+        if nh in (6, 17):
+            field = {6: 16, 17: 6}[nh]
+            want = rfc_l4_checksum(flat, field)
+            got = struct.unpack("!H", flat[40 + field:42 + field])[0]
+            assert got == (want or 0xFFFF if nh == 17 else want)
+            assert f == op.IP_OK | op.L4_CHECKED | op.L4_OK
+        # the window bound: a chain that does not fit leaves the transport unchecked
+        assert op.rx_validate_v6(pkt, window=off + 23) & op.EXT_HDR
+    for _ in range(50):
+        assert op.rx_validate_v6(make_packet_v6(rng, "ext_frag")) == op.IP_OK | op.FRAGMENT
+        assert op.rx_validate_v6(make_packet_v6(rng, "ext_hbh_late")) == op.IP_OK | op.EXT_HDR
+        assert op.rx_validate_v6(make_packet_v6(rng, "ext_bad")) == op.MALFORMED
+        assert op.rx_validate_v6(make_packet_v6(rng, "ext_long"), window=1024) == op.IP_OK | op.EXT_HDR
+        assert op.rx_validate_v6(make_packet_v6(rng, "ext")) == op.IP_OK | op.EXT_HDR

@@ -118,6 +118,7 @@ struct PktInfo {
                            // (8: the addresses open the sum; 40: ICMPv6 errors summed without pseudo)
     uint32_t l4_end;       // packet offset one past the transport part
     uint32_t l4_csum_off;  // packet offset of the transport checksum field (~0u: none)
+    uint32_t ext_end;      // IPv6: packet offset of the transport header (40 + extension headers)
     uint32_t pseudo_le;    // little-endian word sum of the pseudo-header (0: none)
     uint32_t proto;
     bool     check_l4;
@@ -138,15 +139,22 @@ __device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 
 //                Tx: every message through the pseudo-header (DataCalc + pseudo, net_icmpv6.c:1439;
 //                    the error messages' ~HdrCalc(pseudo) field trick, net_icmpv6.c:949-965, gives
 //                    the same value), no 0 -> 0xFFFF substitution
-// Any other next header (extension headers included) gets no transport verdict; the extension
-// header values of RFC 8200 §4 / IANA are flagged EXT_HDR (the stack's ext-header walk,
-// net_ipv6.c, is outside the per-packet batch).
+// Extension headers (net_ipv6.c:8290-8360, RxPktProcessExtHdr): Hop-by-Hop (0, first only),
+// Routing (43) and Destination Options (60) — length (HdrExtLen + 1) * 8, net_ipv6.c:8601 — are
+// skipped, up to 4 of them, while the chain and the transport fields stay inside the bytes the
+// group's first chunks hold (16 * G from the frame start); the transport part then starts after
+// them and the pseudo-header length is the payload length minus their bytes (IP_DatagramLen =
+// IP_TotLen - IPv6_ExtHdrLen, net_ipv6.c:5682). A Fragment header (44) means FRAGMENT: the
+// transport checksum covers the reassembled datagram. Any other extension header (AH, ESP,
+// Mobility, No Next Header, experimental values), a chain past that window or a Hop-by-Hop header
+// after the first gets EXT_HDR and no transport verdict; an extension header running past the
+// payload is MALFORMED (INVALID_EH_LEN).
 __device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
-    return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 60u || nh == 135u ||
-           nh == 139u || nh == 140u || nh == 253u || nh == 254u;
+    return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 59u || nh == 60u ||
+           nh == 135u || nh == 139u || nh == 140u || nh == 253u || nh == 254u;
 }
 
-template <bool TX>
+template <int G, bool TX>
 __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
     PktInfo p{};
     p.l4_csum_off = ~0u;
@@ -155,6 +163,7 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
     const uint32_t plen = be16_at(d1, 0);
     const uint32_t tot = 40u + plen;
     p.proto = (d1 >> 16) & 0xFFu;
+    p.ext_end = 40u;
     if (avail < 40u || ((d0 >> 4) & 0xFu) != 6u || tot > avail) {
         p.flags = F_MALFORMED;
         p.l4_end = 0u;
@@ -163,28 +172,56 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
     }
     p.l4_end = tot;
     p.hlen = 8u;
-    const uint32_t pseudo = (p.proto << 8) + swap16(plen);      // length high half is 0 (plen < 2^16)
+    // window: transport fields up to off + 24 and the dword reads below stay in the k = 0 chunks
+    constexpr uint32_t kWin = 16u * (uint32_t)G;
+    uint32_t off = 40u;
+    for (int e = 0; e < 4 && (p.proto == 0u || p.proto == 43u || p.proto == 60u); ++e) {
+        if ((p.proto == 0u && off != 40u) || lead + off + 8u > kWin) {
+            p.flags |= F_EXT_HDR;
+            return p;
+        }
+        const uint32_t d = pkt_dword(v0, lead, off, gbase);
+        off += (((d >> 8) & 0xFFu) + 1u) * 8u;
+        p.proto = d & 0xFFu;
+        if (off > tot) {
+            p.flags = F_MALFORMED;
+            p.l4_end = 0u;
+            p.hlen = 0u;
+            return p;
+        }
+    }
+    if (p.proto == 44u) {
+        p.flags |= F_FRAGMENT;
+        return p;
+    }
+    if (ipv6_ext_hdr(p.proto) || (off != 40u && lead + off + 24u > kWin)) {
+        p.flags |= F_EXT_HDR;
+        return p;
+    }
+    p.ext_end = off;
+    const uint32_t ulen = tot - off;                             // upper-layer packet length
+    const uint32_t pseudo = (p.proto << 8) + swap16(ulen);       // length high half is 0 (< 2^16)
     switch (p.proto) {
     case 6u:
-        if (plen < 20u) {
+        if (ulen < 20u) {
             p.flags |= F_L4_MALFORMED;
             return p;
         }
         p.check_l4 = true;
-        p.l4_csum_off = 40u + 16u;
+        p.l4_csum_off = off + 16u;
         p.pseudo_le = pseudo;
         break;
     case 17u: {
-        if (plen < 8u) {
+        if (ulen < 8u) {
             p.flags |= F_L4_MALFORMED;
             return p;
         }
-        const uint32_t du = pkt_dword(v0, lead, 44u, gbase);
-        if (be16_at(du, 0) != plen) {                            // net_udp.c:1903-1907
+        const uint32_t du = pkt_dword(v0, lead, off + 4u, gbase);
+        if (be16_at(du, 0) != ulen) {                            // net_udp.c:1903-1907
             p.flags |= F_L4_MALFORMED;
             return p;
         }
-        p.l4_csum_off = 40u + 6u;
+        p.l4_csum_off = off + 6u;
         if (!TX && (du >> 16) == 0u) {
             p.flags |= F_UDP_NO_CSUM | F_L4_OK;
             return p;
@@ -198,19 +235,19 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
         break;
     }
     case 58u:
-        if (plen < 4u) {
+        if (ulen < 4u) {
             p.flags |= F_L4_MALFORMED;
             return p;
         }
-        p.l4_csum_off = 40u + 2u;
+        p.l4_csum_off = off + 2u;
         if constexpr (TX) {
             p.check_l4 = true;
             p.pseudo_le = pseudo;
         } else {
-            const uint32_t type = pkt_dword(v0, lead, 40u, gbase) & 0xFFu;
+            const uint32_t type = pkt_dword(v0, lead, off, gbase) & 0xFFu;
             if (type == 1u || type == 3u || type == 4u) {
                 p.check_l4 = true;
-                p.hlen = 40u;                                    // message alone, no pseudo-header
+                p.hlen = off;                                    // message alone, no pseudo-header
             } else if ((type >= 128u && type <= 131u) || (type >= 134u && type <= 137u)) {
                 p.check_l4 = true;
                 p.pseudo_le = pseudo;
@@ -218,7 +255,6 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
         }
         break;
     default:
-        p.flags |= ipv6_ext_hdr(p.proto) ? F_EXT_HDR : 0u;
         break;
     }
     return p;
@@ -388,7 +424,7 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     // lane afterwards (low_bytes), instead of masking every chunk: the packet kernels are VALU-issue
     // bound (profiles/r1txp_pmc.json), and per-chunk edge masks executed on every k slot dominated.
     const uint32_t lead = st.lead;
-    PktInfo p = V6 ? pkt_parse_v6<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
+    PktInfo p = V6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
                    : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
@@ -434,6 +470,9 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
         }
     }
     uint32_t acc_ip = ip_raw, acc_l4 = acc - ip_raw;
+    if (V6 && p.ext_end > 40u && p.hlen == 8u) {                 // addresses + transport, not the ext headers
+        acc_l4 -= low_bytes(st.v[0], (int)(lead + p.ext_end) - l16) - low_bytes(st.v[0], (int)(lead + 40u) - l16);
+    }
     if (TX) {
         if (!V6 && !(p.flags & F_MALFORMED)) {
             acc_ip -= own_byte(st.v[0], lead + 10u, lane) + own_byte(st.v[0], lead + 11u, lane);
