@@ -353,8 +353,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
 }
 
+// Cache policy of the Tx checksum-field stores (buffer-instruction cpol bits: 1 = sc0, 2 = nt,
+// 16 = sc1). Compile-time knob for store-policy experiments (tools/tx_store_policy.sh); 0 = default.
+#ifndef NETCSUM_TX_STORE_AUX
+#define NETCSUM_TX_STORE_AUX 0
+#endif
+
+template <int AUX = 0>
 __device__ __forceinline__ void store_byte(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xFFu), r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xFFu), r, (int)off, 0, AUX);
 }
 
 // A packet's stores, deferred: the kernel issues them right AFTER the next stage's loads, so no
@@ -386,10 +393,10 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
         const uint32_t o = (uint32_t)(ps.a - wb);
         if constexpr (TX) {
             const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0xFFFFFFFFu);
-            store_byte(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
-            store_byte(rp, ps.vals >> 8, si ? o + 11u : kOOB);
-            store_byte(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
-            store_byte(rp, ps.vals >> 24, sl ? o + l4off + 1u : kOOB);
+            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
+            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 8, si ? o + 11u : kOOB);
+            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
+            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 24, sl ? o + l4off + 1u : kOOB);
         }
         const __amdgpu_buffer_rsrc_t rf = byte_rsrc(A.flags_out, A.flags_out ? A.n : 0u);
         store_byte(rf, f, me ? ps.idx : kOOB);

@@ -20,7 +20,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libnetcsum_mi355x.so")
+# NETCSUM_LIB: an experiment build of the same library (tools/ variant sweeps); default = the in-tree build
+LIB_PATH = os.environ.get("NETCSUM_LIB") or os.path.join(HERE, "libnetcsum_mi355x.so")
 HEADER_PATHS = [os.path.join(REPO, "include", "netcsum_mi355x.h")]
 
 # NET_ERR values (Source/net_err.h:73,122-126,193 + the MI355X additions in netcsum_types.h)
