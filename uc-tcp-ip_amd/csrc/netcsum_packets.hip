@@ -392,7 +392,11 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ps.a);
         const uint32_t o = (uint32_t)(ps.a - wb);
         if constexpr (TX) {
+#ifdef NETCSUM_TX_DROP_STORES   // experiment builds only: same instructions, every field store out of range
+            const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0u);
+#else
             const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0xFFFFFFFFu);
+#endif
             store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
             store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 8, si ? o + 11u : kOOB);
             store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
