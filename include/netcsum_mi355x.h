@@ -229,6 +229,28 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv6     (void            *d_base,
                                             int              udp_tx_csum,
                                             void            *hip_stream);
 
+/* Mixed IPv4 / IPv6 batches (a NIC ring carrying both): packet i goes through (2b) when the version
+ * nibble of its first byte is 4 (or anything but 6) and through (2b') when it is 6; same arguments,
+ * same flags, one launch. */
+NET_ERR  NetUtil_MI355X_RxValidateIP       (const void      *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            void            *hip_stream);
+
+NET_ERR  NetUtil_MI355X_TxFinalizeIP       (void            *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            int              udp_tx_csum,
+                                            void            *hip_stream);
+
 /* ============================================================================================
  * (2c) Batched NET_BUF chains. Chain i = its pseudo-header
  * (d_pseudo + i*pseudo_stride, pseudo_len bytes; none if pseudo_len = 0) followed by pieces

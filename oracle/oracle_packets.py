@@ -289,3 +289,14 @@ def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
     elif nh in (6, 17, 58):
         f |= L4_MALFORMED
     return bytes(pkt), f
+
+
+def rx_validate_ip(pkt: bytes, window: int = 1 << 30) -> int:
+    """Mixed batches: version nibble 6 -> IPv6, anything else -> IPv4 (include/netcsum_mi355x.h)."""
+    return rx_validate_v6(pkt, window) if len(pkt) and pkt[0] >> 4 == 6 else rx_validate(pkt)
+
+
+def tx_finalize_ip(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
+    if len(pkt) and pkt[0] >> 4 == 6:
+        return tx_finalize_v6(pkt, udp_tx_csum, window)
+    return tx_finalize(pkt, udp_tx_csum)

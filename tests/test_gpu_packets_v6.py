@@ -183,3 +183,56 @@ def test_rx_v6_extension_chains_at_the_window_edge(group):
                      for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     assert np.array_equal(got, want)
     assert (want & op.EXT_HDR).any() and ((want & op.L4_OK) != 0).any()
+
+
+@pytest.mark.parametrize("group", [0, 16, 64])
+@pytest.mark.parametrize("udp_tx_csum", [True, False])
+def test_mixed_ip_batch_rx_and_tx(group, udp_tx_csum):
+    """NetUtil_MI355X_RxValidateIP / TxFinalizeIP: one launch over a ring carrying IPv4 and IPv6
+    datagrams (every kind of both, incl. IPv4 packets with version 6 / IPv6 with version 4), each
+    dispatched on its version nibble, equal to the per-version oracles."""
+    from packets import KINDS, make_packet
+    rng = random.Random(800 + group + udp_tx_csum)
+    pkts = [make_packet_v6(rng, rng.choice(KINDS6)) if rng.random() < 0.5 else make_packet(rng, rng.choice(KINDS))
+            for _ in range(2000)]
+    buf, offs, lens = packed_batch(pkts, rng)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    g = group or _auto_group(True)
+    b, o, ln = _dev(buf, offs, lens)
+    f = torch.zeros(len(pkts), dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ip(b, len(pkts), f, off=o, lens=ln)
+    torch.cuda.synchronize()
+    want = np.array([op.rx_validate_ip(bytes(buf[p:p + n]), v6_window(g, p))
+                     for p, n in zip(offs.tolist(), lens.tolist())], np.uint8)
+    got = f.cpu().numpy()
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(pkts[i][:24].hex(), int(got[i]), int(want[i])) for i in bad[:5]]
+    netcsum.tx_finalize_ip(b, len(pkts), f, off=o, lens=ln, udp_tx_csum=udp_tx_csum)
+    torch.cuda.synchronize()
+    out, flags = b.cpu().numpy(), f.cpu().numpy()
+    for i, (p, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        want_pkt, want_f = op.tx_finalize_ip(bytes(buf[p:p + n]), udp_tx_csum, v6_window(g, p))
+        assert bytes(out[p:p + n]) == want_pkt, (i, pkts[i][:24].hex())
+        assert flags[i] == want_f, (i, int(flags[i]), want_f)
+
+
+def test_mixed_ip_strided_c2_shape():
+    """1500-B TCP datagrams, alternating IPv4 / IPv6, strided: Tx then Rx accepts every one."""
+    rng = random.Random(811)
+    from packets import make_packet
+    n, L = 2000, 1500
+    buf = np.zeros(n * L + 64, np.uint8)
+    for i in range(n):
+        p = make_packet_v6(rng, "tcp", payload=1390) if i % 2 else make_packet(rng, "tcp", payload=1380)
+        p = bytearray(p)
+        p[-2:] = b"\x00\x00"                                     # force a Tx rewrite of stale fields
+        buf[i * L:i * L + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ip(b, n, f, stride=L, pkt_len=L)
+    netcsum.rx_validate_ip(b, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    out = b.cpu().numpy()
+    want = np.array([op.rx_validate_ip(bytes(out[i * L:(i + 1) * L])) for i in range(n)], np.uint8)
+    assert np.array_equal(f.cpu().numpy(), want)
+    assert (want == (op.IP_OK | op.L4_CHECKED | op.L4_OK)).sum() > n * 0.9

@@ -127,6 +127,15 @@ def main():
     ms6 = events_ms(lambda: netcsum.rx_validate_ipv6(pk, n, flags, stride=L, pkt_len=L, stream=st), st)
     ok6 = bool(((flags & 0x07) == 0x07).all().item())
     ms6_tx = events_ms(lambda: netcsum.tx_finalize_ipv6(pk, n, None, stride=L, pkt_len=L, stream=st), st)
+    # every other datagram back to IPv4 (its header restored, checksums rewritten): a mixed ring
+    v[0::2, 0:12] = hdr
+    v[0::2, 12:20] = 0x0A
+    netcsum.tx_finalize_ip(pk, n, flags, stride=L, pkt_len=L, stream=st)
+    torch.cuda.synchronize()
+    msmx = events_ms(lambda: netcsum.rx_validate_ip(pk, n, flags, stride=L, pkt_len=L, stream=st), st)
+    okmx = bool(((flags & 0x07) == 0x07).all().item())
+    out["mixed_v4_v6_1500B_tcp"] = {"packets": n, "ms_rx": round(msmx, 4), "all_valid_rx": okmx,
+                                    "GiB_per_s_rx": round(n * L / msmx / 1e6 / 1.073741824, 1)}
     out["ipv6_1500B_tcp"] = {"packets": n, "ms_rx": round(ms6, 4), "ms_tx": round(ms6_tx, 4),
                              "GiB_per_s_rx": round(n * L / ms6 / 1e6 / 1.073741824, 1),
                              "GiB_per_s_tx": round(n * L / ms6_tx / 1e6 / 1.073741824, 1), "all_valid_rx": ok6}

@@ -477,7 +477,7 @@ NET_ERR NetUtil_MI355X_StreamSum32(const NETCSUM_SPAN* spans, uint32_t n_spans, 
 
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                          CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum, bool tx,
-                         bool ipv6, void* hip_stream) {
+                         int ip_ver, void* hip_stream) {
     if (n_pkt == 0) return NET_UTIL_ERR_NONE;
     if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr)) {
@@ -509,7 +509,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     c.grid = g_tune_grid.load();
     const int tile = g_tune_tile.load();
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
-    NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ipv6, static_cast<hipStream_t>(hip_stream)));
+    NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
 
@@ -552,25 +552,37 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
 NET_ERR NetUtil_MI355X_RxValidateIPv4(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
                                       uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, false, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, 4, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_TxFinalizeIPv4(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                       CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, false, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 4, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_RxValidateIPv6(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
                                       uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, true, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, 6, hip_stream);
+}
+
+NET_ERR NetUtil_MI355X_RxValidateIP(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
+                                    uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags,
+                                    void* hip_stream) {
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1, false, 0, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_TxFinalizeIPv6(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                       CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, true, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 6, hip_stream);
+}
+
+NET_ERR NetUtil_MI355X_TxFinalizeIP(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
+                                    CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
+                                    void* hip_stream) {
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 0, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern,

@@ -67,7 +67,8 @@ struct ChainBatchArgs {
 
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
 
-hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, bool ipv6, hipStream_t s);
+hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, int ip_ver,  // 4, 6, 0 = per packet
+                            hipStream_t s);
 
 bool tile_supported(int g, int p, int k);   // is (G, P, K) a compiled v4 instantiation
 const char* last_launch();                  // description of this thread's last batch launch

@@ -420,7 +420,7 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
     }
 }
 
-template <int G, int K, bool NT, bool TX, bool V6>
+template <int G, int K, bool NT, bool TX, int VER>
 __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const PktBatchArgs& A, uint32_t idx, bool valid,
                                                 int lane, int gbase) {
     // One sum over [lead, lead + end) (end = transport end, or the IP header end when the transport
@@ -435,7 +435,9 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     // lane afterwards (low_bytes), instead of masking every chunk: the packet kernels are VALU-issue
     // bound (profiles/r1txp_pmc.json), and per-chunk edge masks executed on every k slot dominated.
     const uint32_t lead = st.lead;
-    PktInfo p = V6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
+    // VER 4 / 6: one IP version per batch; VER 0: per packet by the version nibble (a mixed NIC ring)
+    const bool is6 = (VER == 6) || (VER == 0 && ((pkt_dword(st.v[0], lead, 0u, gbase) >> 4) & 0xFu) == 6u);
+    PktInfo p = is6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
                    : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
@@ -481,11 +483,11 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
         }
     }
     uint32_t acc_ip = ip_raw, acc_l4 = acc - ip_raw;
-    if (V6 && p.ext_end > 40u && p.hlen == 8u) {                 // addresses + transport, not the ext headers
+    if (is6 && p.ext_end > 40u && p.hlen == 8u) {                 // addresses + transport, not the ext headers
         acc_l4 -= low_bytes(st.v[0], (int)(lead + p.ext_end) - l16) - low_bytes(st.v[0], (int)(lead + 40u) - l16);
     }
     if (TX) {
-        if (!V6 && !(p.flags & F_MALFORMED)) {
+        if (!is6 && !(p.flags & F_MALFORMED)) {
             acc_ip -= own_byte(st.v[0], lead + 10u, lane) + own_byte(st.v[0], lead + 11u, lane);
         }
         if (p.check_l4) {
@@ -504,12 +506,12 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     uint32_t cip = ~0u, cl4 = ~0u;                               // Tx values to store; ~0u = none
     if (!(f & F_MALFORMED)) {
         if constexpr (!TX) {
-            f |= (V6 || sip == 0xFFFFu) ? F_IP_OK : 0u;          // IPv6: well-formed (no header checksum)
+            f |= (is6 || sip == 0xFFFFu) ? F_IP_OK : 0u;          // IPv6: well-formed (no header checksum)
             if (p.check_l4) {
                 f |= F_L4_CHECKED | ((sl4 == 0xFFFFu) ? F_L4_OK : 0u);
             }
         } else {
-            if constexpr (!V6) {
+            if (!is6) {
                 cip = (~sip) & 0xFFFFu;                          // net_ipv4.c:9578-9586
             }
             f |= F_IP_OK;
@@ -547,7 +549,7 @@ __device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint
 
 // 4 waves per SIMD: the Tx instantiations otherwise take 131 VGPRs (3 waves), 25 % less memory
 // parallelism than Rx (122 VGPRs); capped at 128 they do not spill (profiles/r1txp_pmc.json).
-template <int G, int K, bool VARLEN, bool NT, bool TX, bool V6>
+template <int G, int K, bool VARLEN, bool NT, bool TX, int VER>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pkt_batch_kernel(PktBatchArgs A) {
     static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
     const int lane = (int)(threadIdx.x & (G - 1));
@@ -587,7 +589,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);                      // previous packet's stores, after the loads
         pin_chunks<K>(S0.v);
-        pend = pkt_consume<G, K, NT, TX, V6>(S0, A, i, v0, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX, VER>(S0, A, i, v0, lane, gbase);
         i = nx;
         nx = i + step;
         v0 = j + 2u < cnt;
@@ -595,13 +597,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);
         pin_chunks<K>(S1.v);
-        pend = pkt_consume<G, K, NT, TX, V6>(S1, A, i, v1, lane, gbase);
+        pend = pkt_consume<G, K, NT, TX, VER>(S1, A, i, v1, lane, gbase);
         i = nx;
     }
     pkt_store<G, TX, !VARLEN>(pend, A);
 }
 
-template <int G, int K, bool VARLEN, bool TX, bool V6>
+template <int G, int K, bool VARLEN, bool TX, int VER>
 hipError_t launch_pkt_gk(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
     const uint32_t gpb = 256u / G;
     int grid;
@@ -612,38 +614,42 @@ hipError_t launch_pkt_gk(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t 
         grid = c.grid > 0 ? c.grid : (int)(((uint64_t)a.n + gpb - 1u) / gpb);
     }
     if (c.nt) {
-        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, true, TX, V6>), dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, true, TX, VER>), dim3(grid), dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, false, TX, V6>), dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((pkt_batch_kernel<G, K, VARLEN, false, TX, VER>), dim3(grid), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }
 
-template <bool VARLEN, bool TX, bool V6>
+template <bool VARLEN, bool TX, int VER>
 hipError_t launch_pkt_v(const PktBatchArgs& a, const LaunchCfg& c, hipStream_t s) {
     switch (c.group_lanes) {
-    case 8:  return c.chunks_per_pass <= 4 ? launch_pkt_gk<8, 4, VARLEN, TX, V6>(a, c, s)
-                                           : launch_pkt_gk<8, 8, VARLEN, TX, V6>(a, c, s);
-    case 16: return c.chunks_per_pass <= 3 ? launch_pkt_gk<16, 3, VARLEN, TX, V6>(a, c, s)
-                                           : launch_pkt_gk<16, 6, VARLEN, TX, V6>(a, c, s);
-    case 32: return c.chunks_per_pass <= 3 ? launch_pkt_gk<32, 3, VARLEN, TX, V6>(a, c, s)
-                                           : launch_pkt_gk<32, 6, VARLEN, TX, V6>(a, c, s);
-    default: return launch_pkt_gk<64, 4, VARLEN, TX, V6>(a, c, s);
+    case 8:  return c.chunks_per_pass <= 4 ? launch_pkt_gk<8, 4, VARLEN, TX, VER>(a, c, s)
+                                           : launch_pkt_gk<8, 8, VARLEN, TX, VER>(a, c, s);
+    case 16: return c.chunks_per_pass <= 3 ? launch_pkt_gk<16, 3, VARLEN, TX, VER>(a, c, s)
+                                           : launch_pkt_gk<16, 6, VARLEN, TX, VER>(a, c, s);
+    case 32: return c.chunks_per_pass <= 3 ? launch_pkt_gk<32, 3, VARLEN, TX, VER>(a, c, s)
+                                           : launch_pkt_gk<32, 6, VARLEN, TX, VER>(a, c, s);
+    default: return launch_pkt_gk<64, 4, VARLEN, TX, VER>(a, c, s);
     }
 }
 
-template <bool V6>
+template <int VER>
 hipError_t launch_pkt_ver(const PktBatchArgs& a, const LaunchCfg& c, bool tx, hipStream_t s) {
     if (a.off) {
-        return tx ? launch_pkt_v<true, true, V6>(a, c, s) : launch_pkt_v<true, false, V6>(a, c, s);
+        return tx ? launch_pkt_v<true, true, VER>(a, c, s) : launch_pkt_v<true, false, VER>(a, c, s);
     }
-    return tx ? launch_pkt_v<false, true, V6>(a, c, s) : launch_pkt_v<false, false, V6>(a, c, s);
+    return tx ? launch_pkt_v<false, true, VER>(a, c, s) : launch_pkt_v<false, false, VER>(a, c, s);
 }
 
 }  // namespace
 
-hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, bool ipv6, hipStream_t s) {
-    return ipv6 ? launch_pkt_ver<true>(a, c, tx, s) : launch_pkt_ver<false>(a, c, tx, s);
+hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, int ip_ver, hipStream_t s) {
+    switch (ip_ver) {
+    case 4:  return launch_pkt_ver<4>(a, c, tx, s);
+    case 6:  return launch_pkt_ver<6>(a, c, tx, s);
+    default: return launch_pkt_ver<0>(a, c, tx, s);
+    }
 }
 
 }  // namespace netcsum

@@ -196,6 +196,10 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_RxValidateIPv6.restype = i32
     L.NetUtil_MI355X_TxFinalizeIPv6.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, vp]
     L.NetUtil_MI355X_TxFinalizeIPv6.restype = i32
+    L.NetUtil_MI355X_RxValidateIP.argtypes = [vp, vp, vp, u64, u16, u32, vp, vp]
+    L.NetUtil_MI355X_RxValidateIP.restype = i32
+    L.NetUtil_MI355X_TxFinalizeIP.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, vp]
+    L.NetUtil_MI355X_TxFinalizeIP.restype = i32
     L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, u64, i32, vp]
     L.NetUtil_MI355X_Fill.restype = i32
     L.NetUtil_MI355X_ReadStream.argtypes = [vp, u64, vp, vp]
@@ -413,6 +417,26 @@ def tx_finalize_ipv6(base, n, flags=None, off=None, lens=None, stride=0, pkt_len
                                               int(bool(udp_tx_csum)), _stream(stream))
     if check:
         _check(err, "NetUtil_MI355X_TxFinalizeIPv6")
+    return err
+
+
+def rx_validate_ip(base, n, flags, off=None, lens=None, stride=0, pkt_len=0, stream=None, check=True):
+    """Mixed IPv4 / IPv6 batch: per packet by the version nibble."""
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_RxValidateIP(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
+                                            _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_RxValidateIP")
+    return err
+
+
+def tx_finalize_ip(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, udp_tx_csum=True,
+                   stream=None, check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_TxFinalizeIP(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
+                                            int(bool(udp_tx_csum)), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_TxFinalizeIP")
     return err
 
 
