@@ -155,11 +155,10 @@ __device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
 }
 
 template <int G, bool TX>
-__device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
+__device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum,
+                                                uint32_t d0, uint32_t d1) {   // packet dwords 0 and 1
     PktInfo p{};
     p.l4_csum_off = ~0u;
-    const uint32_t d0 = pkt_dword(v0, lead, 0u, gbase);
-    const uint32_t d1 = pkt_dword(v0, lead, 4u, gbase);
     const uint32_t plen = be16_at(d1, 0);
     const uint32_t tot = 40u + plen;
     p.proto = (d1 >> 16) & 0xFFu;
@@ -261,11 +260,10 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
 }
 
 template <bool TX>
-__device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum) {
+__device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum,
+                                             uint32_t d0, uint32_t d1) {      // packet dwords 0 and 1
     PktInfo p{};
     p.l4_csum_off = ~0u;
-    const uint32_t d0 = pkt_dword(v0, lead, 0u, gbase);
-    const uint32_t d1 = pkt_dword(v0, lead, 4u, gbase);
     const uint32_t d2 = pkt_dword(v0, lead, 8u, gbase);
     const uint32_t d3 = pkt_dword(v0, lead, 12u, gbase);
     const uint32_t d4 = pkt_dword(v0, lead, 16u, gbase);
@@ -436,9 +434,12 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     // bound (profiles/r1txp_pmc.json), and per-chunk edge masks executed on every k slot dominated.
     const uint32_t lead = st.lead;
     // VER 4 / 6: one IP version per batch; VER 0: per packet by the version nibble (a mixed NIC ring)
-    const bool is6 = (VER == 6) || (VER == 0 && ((pkt_dword(st.v[0], lead, 0u, gbase) >> 4) & 0xFu) == 6u);
-    PktInfo p = is6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u)
-                   : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u);
+    // (the first two dwords, read once, outside the per-version branch)
+    const uint32_t d0 = pkt_dword(st.v[0], lead, 0u, gbase);
+    const uint32_t d1 = pkt_dword(st.v[0], lead, 4u, gbase);
+    const bool is6 = (VER == 6) || (VER == 0 && ((d0 >> 4) & 0xFu) == 6u);
+    PktInfo p = is6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u, d0, d1)
+                   : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u, d0, d1);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
     const uint32_t nch = (rend + 15u) >> 4;
