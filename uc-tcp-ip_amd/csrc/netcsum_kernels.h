@@ -86,7 +86,7 @@ uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves);
 int stream_occupancy(int depth, const SegBatchArgs& a, bool nt);   // resident 256-thread blocks per CU
 hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t tag = 0u);   // tag != 0 (grid 1): completion word
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,
                        hipStream_t s);
 hipError_t launch_read_stream(const void* d_p, uint64_t n16, unsigned long long* d_sink, int grid, bool nt,

@@ -666,7 +666,8 @@ __global__ void __launch_bounds__(256) read_stream_lds_kernel(gu32x4* __restrict
 // needed — the per-packet path reads pinned host memory zero-copy and writes the result straight
 // back into pinned host memory, one launch per call).
 __global__ void __launch_bounds__(256) stream_exact_kernel(gu32x4* __restrict__ p, uint32_t n16,
-                                                           unsigned long long* __restrict__ sum, int direct) {
+                                                           unsigned long long* __restrict__ sum, int direct,
+                                                           uint32_t tag) {
     __shared__ unsigned long long wsum[4];
     uint32_t acc = 0u;
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += gridDim.x * blockDim.x) {
@@ -690,7 +691,12 @@ __global__ void __launch_bounds__(256) stream_exact_kernel(gu32x4* __restrict__ 
         for (uint32_t i = 0; i < (blockDim.x >> 6); ++i) {
             t += wsum[i];
         }
-        if (direct) {
+        if (direct && tag != 0u) {
+            // completion word for a host that polls instead of synchronising: tag in the high half,
+            // the reference's u32 sum in the low half, one system-scope release store
+            __hip_atomic_store(sum, ((unsigned long long)tag << 32) | (uint32_t)t, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (direct) {
             *sum = t;
         } else {
             atomicAdd(sum, t);
@@ -1018,9 +1024,10 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
 }
 
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
-                               hipStream_t s) {
+                               hipStream_t s, uint32_t tag) {
     hipLaunchKernelGGL(stream_exact_kernel, dim3(grid), dim3(256), 0, s,
-                       reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sum, grid == 1 ? 1 : 0);
+                       reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_p)), n16, d_sum, grid == 1 ? 1 : 0,
+                       grid == 1 ? tag : 0u);
     return hipGetLastError();
 }
 
