@@ -64,7 +64,7 @@ __device__ __forceinline__ void pin_chunks(u32x4 (&v)[K]) {
 
 // The packet's frame starts at the 16-B boundary below it; chunk c of the frame is
 // [q0 + 16c, q0 + 16c + 16).
-template <int G, int K, bool NT>
+template <int G, int K, bool NT, bool NT_TAIL = NT>   // NT_TAIL: policy of the chunks past slot 0
 __device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane) {
     st.a = a;
     st.lead = (uint32_t)(a & 15u);
@@ -75,7 +75,8 @@ __device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t c = (uint32_t)(k * G + lane);
-        st.v[k] = load16<NT>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z));
+        gu32x4* src = reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z);
+        st.v[k] = (k == 0) ? load16<NT>(src) : load16<NT_TAIL>(src);
     }
 }
 
@@ -553,6 +554,10 @@ __device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint
 template <int G, int K, bool VARLEN, bool NT, bool TX, int VER>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pkt_batch_kernel(PktBatchArgs A) {
     static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
+#ifndef NETCSUM_TX_SPLIT_NT      // experiment: Tx reads the header slot plain, the rest non-temporal
+#define NETCSUM_TX_SPLIT_NT 0
+#endif
+    constexpr bool kNtTail = NT || (TX && NETCSUM_TX_SPLIT_NT);
     const int lane = (int)(threadIdx.x & (G - 1));
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
     const uint32_t gpb = blockDim.x / G;
@@ -581,13 +586,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
     uint32_t i = first;
     bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
-    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+    pkt_issue<G, K, NT, kNtTail>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
     PktStore pend{z, 0u, 0u, 0u};                                // nothing to store yet
     for (uint32_t j = 0u; j < iters; j += 2u) {                  // one scalar exit (see seg_pipe_kernel)
         uint32_t nx = i + step;
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
+        pkt_issue<G, K, NT, kNtTail>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);                      // previous packet's stores, after the loads
         pin_chunks<K>(S0.v);
         pend = pkt_consume<G, K, NT, TX, VER>(S0, A, i, v0, lane, gbase);
@@ -595,7 +600,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+        pkt_issue<G, K, NT, kNtTail>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);
         pin_chunks<K>(S1.v);
         pend = pkt_consume<G, K, NT, TX, VER>(S1, A, i, v1, lane, gbase);
