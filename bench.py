@@ -142,7 +142,7 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
                       f"= same source -O3 -march=native on {threads} threads"}
 
 
-CURRENT_PMC = "r1p_pmc.json"   # newest FETCH_SIZE/WRITE_SIZE summary of the default bench kernel
+CURRENT_PMC = "r1q_pmc.json"   # newest FETCH_SIZE/WRITE_SIZE summary of the default bench kernel
 
 
 def load_traffic(path, n_seg, kernel_fn):
