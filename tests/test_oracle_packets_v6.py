@@ -133,3 +133,19 @@ def test_extension_headers_walked_and_flagged():
         assert op.rx_validate_v6(make_packet_v6(rng, "ext_bad")) == op.MALFORMED
         assert op.rx_validate_v6(make_packet_v6(rng, "ext_long"), window=1024) == op.IP_OK | op.EXT_HDR
         assert op.rx_validate_v6(make_packet_v6(rng, "ext")) == op.IP_OK | op.EXT_HDR
+
+
+def test_mixed_dispatch_follows_the_version_nibble():
+    """rx_validate_ip / tx_finalize_ip (the mixed-ring oracle): version 6 -> IPv6 rules, anything
+    else -> IPv4 rules (an IPv4 packet relabelled 6 is judged as IPv6, and vice versa)."""
+    from packets import make_packet
+    rng = random.Random(68)
+    for _ in range(100):
+        p4 = make_packet(rng, "tcp")
+        p6 = make_packet_v6(rng, "tcp")
+        assert op.rx_validate_ip(p4) == op.rx_validate(p4)
+        assert op.rx_validate_ip(p6) == op.rx_validate_v6(p6)
+        swapped = bytes([0x60 | (p4[0] & 0xF)]) + p4[1:]
+        assert op.rx_validate_ip(swapped) == op.rx_validate_v6(swapped)
+        assert op.tx_finalize_ip(p6) == op.tx_finalize_v6(p6)
+    assert op.rx_validate_ip(b"") == op.MALFORMED
