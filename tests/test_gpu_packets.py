@@ -135,3 +135,42 @@ def test_tx_finalize_strided_vs_oracle(stride, pkt_len, group):
     bad = np.nonzero(out != want)[0]
     assert bad.size == 0, [(int(j), int(j) // stride, int(j) % stride, int(out[j]), int(want[j])) for j in bad[:8]]
     assert np.array_equal(f.cpu().numpy(), want_f)
+
+
+@pytest.mark.parametrize("group", [0, 64])
+def test_ipv4_extreme_sizes(group):
+    """IPv4 datagrams at the size limits: 20-B header only, minimal UDP / TCP / ICMP, and total
+    lengths up to 65535 B (the 16-bit limit) with and without IP options, packed at odd offsets;
+    Rx verdicts and Tx write-back equal the packet oracle."""
+    rng = random.Random(950 + group)
+    pkts = [make_packet(rng, "other", payload=0), make_packet(rng, "udp", payload=0),
+            make_packet(rng, "tcp", payload=0), make_packet(rng, "icmp", payload=0)]
+    for kind in ("tcp", "udp", "icmp", "tcp"):
+        p = make_packet(rng, kind, payload=0)
+        room = 65535 - len(p)
+        pkts.append(make_packet(random.Random(rng.random()), kind, payload=0))
+        big = None
+        for _ in range(20):                                      # options / TCP header length vary
+            r = random.Random(rng.random())
+            cand = make_packet(r, kind, payload=room - 60)
+            if len(cand) <= 65535:
+                big = cand
+                break
+        assert big is not None
+        pkts.append(big)
+    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    buf, offs, lens = packed_batch(pkts, rng, trailer=False)
+    got = _rx_gpu(buf, offs, lens)
+    want = np.array([op.rx_validate(bytes(buf[o:o + n])) for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
+    assert np.array_equal(got, want), (got, want)
+    b = torch.from_numpy(buf).to(DEV)
+    o_ = torch.from_numpy(offs.view(np.int64)).to(DEV)
+    ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    f = torch.zeros(len(pkts), dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b, len(pkts), f, off=o_, lens=ln)
+    torch.cuda.synchronize()
+    out = b.cpu().numpy()
+    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        want_pkt, want_f = op.tx_finalize(bytes(buf[o:o + n]), True)
+        assert bytes(out[o:o + n]) == want_pkt, i
+        assert f.cpu().numpy()[i] == want_f, i
