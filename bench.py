@@ -4,9 +4,13 @@
 BASELINE.json metric: "GiB/s checksummed, device-resident, batched 1500 B TCP segments @1/2/4/8 GPU".
 Workload at N=1 (configs[1], "C2"): 1 048 576 uniform 1500-B TCP segments + one 12-B IPv4 pseudo-
 header each, resident in HBM; one STEP = one NetUtil_MI355X_ChkSumBatchStrided launch producing
-all 1 M DataCalc checksums. Weak scaling: every rank checksums its own 1 M-segment shard (distinct
-bytes per rank) with no collective on the data path; the only communication is the barrier and
-the max-over-ranks of the timed region.
+all 1 M DataCalc checksums. At N>1 (configs[4], "C5"): each rank owns a 16 M-segment shard of the
+global 128 M x 1500 B batch (contiguous index ranges), one launch per step. Weak
+scaling: distinct bytes per rank, no collective on the data path; the only communication is the
+barrier and the max-over-ranks of the timed region.
+
+Clock ramp: the first ~100 launches after an idle gap run up to 25 % slower, so before
+the W counted warm-up steps the step is repeated untimed for --ramp-seconds (default 0.5 s).
 
 value     = Σ_ranks n_seg*(1500+12) bytes * steps / max_rank(wall time of the K timed steps) / 2^30
 roofline  = dominant kernel (the form the library picks for C2: seg_stream_kernel) algorithmic bytes
@@ -42,7 +46,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--segments", type=int, default=1 << 20, help="segments per GPU (C2: 1 M)")
+    ap.add_argument("--segments", type=int, default=None,
+                    help="segments per GPU (default: C2's 1 M at N=1, C5's 16 M shard at N>1)")
+    ap.add_argument("--ramp-seconds", type=float, default=0.5,
+                    help="untimed clock-ramp phase before the counted warm-up (same launch)")
     ap.add_argument("--seg-len", type=int, default=1500)
     ap.add_argument("--pseudo-len", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -110,12 +117,74 @@ def _time_cpu(fn, seconds):
             return reps, el
 
 
+def host_cpus():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota and by the
+    OMP_NUM_THREADS share the GPU box sets for one GPU (its mask shows every CPU of a shared host;
+    running past the share only throttles or starves neighbours). Returns (threads, details)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = min(aff, quota) if quota else aff
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    return threads, {"nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def c1_per_call(oracle, netcsum, gpu):
+    """Config C1 (BASELINE configs[0]): one 64-B UDP datagram of the loopback echo (UDP length 72,
+    IPv4 total 92), the per-datagram sequence DataCalc -> HdrCalc -> HdrVerify -> DataVerify
+    (SURVEY §3.1/§3.2). CPU: the oracle's C loop (reference C path restatement, 1 thread). GPU: the
+    product's four drop-in functions called from Python (ctypes, ~0.3 us per call included)."""
+    import struct
+    payload = bytes((k * 13) & 0xFF for k in range(64))
+    src, dst = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
+    ip = struct.pack("!BBHHHBBH4s4s", 0x45, 0, 92, 1, 0x4000, 64, 17, 0, src, dst)
+    frame = ip + struct.pack("!HHHH", 5000, 7, 72, 0) + payload
+    ch = netcsum.Chain([{"data": frame, "proto": netcsum.NET_PROTOCOL_TYPE_UDP_V4, "transport_ix": 20,
+                         "transport_hdr_len": 8, "data_len": 64}])
+    ph = netcsum.HostBytes(struct.pack("!4s4sBBH", src, dst, 0, 17, 72))
+    hb = netcsum.HostBytes(ip)
+    iters = 200_000
+    oracle.c1_loop(ch.ptr, ph.ptr, 12, hb.ptr, 1000)
+    t0 = time.perf_counter()
+    oracle.c1_loop(ch.ptr, ph.ptr, 12, hb.ptr, iters)
+    cpu_us = (time.perf_counter() - t0) / (iters * 4) * 1e6
+    res = {"datagram": "64-B UDP payload, UDP length 72, IPv4 total 92, 12-B pseudo-header",
+           "sequence": "DataCalc, HdrCalc, HdrVerify, DataVerify", "cpu_us_per_call": round(cpu_us, 4),
+           "cpu_kind": "port (oracle/net_util_oracle.c -O2, 1 thread, C loop)"}
+    if gpu:
+        want = (oracle.data_calc(ch.ptr, ph.ptr, 12), oracle.hdr_calc(hb.ptr, 20))
+        got = (netcsum.DataCalc(ch.ptr, ph.ptr, 12), netcsum.HdrCalc(hb.ptr, 20))
+        reps = 500
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            netcsum.DataCalc(ch.ptr, ph.ptr, 12)
+            netcsum.HdrCalc(hb.ptr, 20)
+            netcsum.HdrVerify(hb.ptr, 20)
+            netcsum.DataVerify(ch.ptr, ph.ptr, 12)
+        gpu_us = (time.perf_counter() - t0) / (reps * 4) * 1e6
+        res.update({"gpu_dropin_us_per_call": round(gpu_us, 3), "gpu_matches_oracle": got == want,
+                    "gpu_over_cpu": round(gpu_us / cpu_us, 1)})
+    return res
+
+
 def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
     """Oracle (reference C path restatement) on a bounded sample of the C2 workload: gcc -O2 on all
-    threads (the reported value), gcc -O2 on one thread, and the same source built -O3 -march=native
-    for this host on all threads ("best CPU")."""
+    usable host CPUs (the reported value), gcc -O2 on one thread, and the same source built -O3
+    -march=native for this host on all threads ("best CPU")."""
     import tempfile
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, cpu_info = host_cpus()
     n = 1 << 18                                      # 256 Ki segments = 396 MB: larger than the host LLC
     seg, ph = host_c2_shard(oracle, 0, n, L, plen)
     sample_b = n * (L + plen)
@@ -133,32 +202,61 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
                 best = round(rb * sample_b / eb / 2 ** 30, 3)
     except Exception as e:                           # noqa: BLE001 — a missing compiler only drops this line
         best = f"unavailable: {e}"
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port", **cpu_info,
+            "value_per_core": round(gib / threads, 3),
             "value_1thread": round(r1 * sample_b / e1 / 2 ** 30, 3),
             "value_best_cpu_O3_native": best, "cpu_model": cpu_model(),
             "sample": f"{reps} passes x {n} segments x ({L}+{plen}) B (C2 shape, {sample_b / 1e6:.0f} MB), "
                       f"oracle/net_util_oracle.c -O2 OpenMP static, {el:.2f} s wall x {threads} threads "
                       f"= {el * threads:.0f} core-s; 1-thread line {r1} passes in {e1:.2f} s; best-CPU line "
-                      f"= same source -O3 -march=native on {threads} threads"}
+                      f"= same source -O3 -march=native on {threads} threads; threads = affinity mask "
+                      f"capped by the cgroup CPU quota"}
 
 
-CURRENT_PMC = "r1q_pmc.json"   # newest FETCH_SIZE/WRITE_SIZE summary of the default bench kernel
+# Sources that define each dominant kernel: a PMC summary is valid only for the exact sources it was
+# collected from (tools/pmc_summary.py records their hash; bench.py recomputes it here).
+KERNEL_SOURCES = {
+    "seg_stream_kernel": ["netcsum_stream.hip", "netcsum_device.h", "netcsum_kernels.h"],
+}
 
 
-def load_traffic(path, n_seg, kernel_fn):
-    """HBM bytes per launch of THIS kernel form at this size, from the newest matching PMC summary."""
-    # The current summary first (file mtimes are arbitrary in a fresh checkout), then any other.
-    cands = [path] if path else (sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))) +
-                                 [os.path.join(REPO, "profiles", CURRENT_PMC)])
+def kernel_src_sha(kernel_fn):
+    import hashlib
+    files = KERNEL_SOURCES.get(kernel_fn)
+    if not files:
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        h.update(open(os.path.join(REPO, "uc-tcp-ip_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(path, n_seg, kernel_desc):
+    """HBM bytes per launch of THIS kernel (name, template form, launch geometry and source hash)
+    at this size, from a rocprofv3 PMC summary under profiles/. Returns (bytes, source, problem):
+    a summary whose kernel or sources differ from the launched one is refused and reported."""
+    kernel_fn = kernel_desc.split("::")[-1].split("<")[0]
+    sha = kernel_src_sha(kernel_fn)
+    cands = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+    stale = []
     for p in reversed(cands):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if (d.get("n_seg") == n_seg and "hbm_bytes_per_launch" in d
-                and kernel_fn in d.get("dominant_kernel", "")):
-            return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, REPO)
-    return None, None
+        if d.get("n_seg") != n_seg or "hbm_bytes_per_launch" not in d:
+            continue
+        if d.get("kernel_desc") != kernel_desc:
+            continue
+        if d.get("kernel_src_sha") != sha:
+            stale.append(os.path.relpath(p, REPO))
+            continue
+        return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, REPO), None
+    why = (f"no PMC summary for {kernel_desc} at n_seg={n_seg} with kernel_src_sha={sha}"
+           + (f" (stale: {', '.join(stale)})" if stale else ""))
+    print(f"[bench] roofline.traffic unavailable: {why} — run tools/gpu_run.sh to re-collect",
+          file=sys.stderr, flush=True)
+    return None, None, why
 
 
 def main():
@@ -185,6 +283,8 @@ def main():
         netcsum.tune(keymap[k], int(v))
 
     n, L, plen = args.segments, args.seg_len, args.pseudo_len
+    if n is None:
+        n = (1 << 20) if world == 1 else (1 << 24)       # C2 at N=1; the C5 shard (16 M) at N>1
     start, n = shard_range(rank, n)
     seg, ph = make_c2_shard(torch, netcsum, start, n, L, plen, dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
@@ -193,6 +293,13 @@ def main():
     def step():
         netcsum.batch_strided(seg, L, L, ph, plen, plen, n, out, netcsum.OP_DATA_CALC, stream=stream)
 
+    # untimed clock ramp (by time, independent of --warmup), then the W counted warm-up steps
+    t_ramp, ramp_launches = time.perf_counter(), 0
+    while time.perf_counter() - t_ramp < args.ramp_seconds or ramp_launches < 8:
+        for _ in range(8):
+            step()
+        ramp_launches += 8
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -265,8 +372,7 @@ def main():
         value = total_bytes / wall / 2 ** 30
         algo_bytes = n * (L + plen + 2)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        kernel_fn = kernel_desc.split("::")[-1].split("<")[0]
-        traffic, traffic_src = load_traffic(args.traffic_json, n, kernel_fn)
+        traffic, traffic_src, traffic_err = load_traffic(args.traffic_json, n, kernel_desc)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -275,14 +381,17 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "ramp_launches": ramp_launches,
             "ms_per_step": round(wall / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (device-generated splitmix64 bytes, seed 0x5EED0001, rank shard = slice of one global stream; IPv4 pseudo-headers from the global index)",
-            "config": {"workload": "C2: 1500 B TCP segments + 12 B IPv4 pseudo-header, device-resident, "
-                                   "NetUtil_16BitOnesCplChkSumDataCalc per segment",
+            "config": {"workload": (("C2: 1 M x " if world == 1 and n == 1 << 20 else
+                                     f"C5 shard: {n} x " if n == 1 << 24 else f"{n} x ")
+                                    + f"{L} B TCP segments + {plen} B IPv4 pseudo-header per GPU, device-resident, "
+                                    "NetUtil_16BitOnesCplChkSumDataCalc per segment"),
                        "segments_per_gpu": n, "seg_len": L, "pseudo_len": plen,
                        "global_batch": n * world, "parallelism": f"shard{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -292,6 +401,8 @@ def main():
                          "kernel_ms": round(kern_ms, 5), "kernel_ms_median": round(kern_med_ms, 5),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "traffic_source": traffic_src,
+                         "traffic_error": traffic_err,
+                         "kernel_src_sha": kernel_src_sha(kernel_desc.split("::")[-1].split("<")[0]),
                          "read_stream_probe_GBps": round(n16 / (rs_ms * 1e-3) / 1e9, 1),
                          "frac_of_read_stream_probe": round(achieved / (n16 / (rs_ms * 1e-3) / 1e9), 4)},
             "parity_sample_ok": parity_all,
@@ -302,6 +413,11 @@ def main():
                 line["cpu_baseline"] = cpu_baseline(oracle, n, L, plen, args.cpu_seconds)
             except Exception as e:
                 line["cpu_baseline"] = {"value": None, "error": str(e)}
+            try:
+                import oracle
+                line["c1_per_datagram"] = c1_per_call(oracle, netcsum, gpu=True)
+            except Exception as e:
+                line["c1_per_datagram"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
 
     if world > 1:

@@ -299,10 +299,18 @@ NET_ERR  NetUtil_MI355X_StreamSum32        (const NETCSUM_SPAN *spans,
                                             uint32_t            n_spans,
                                             uint32_t           *p_sum32);
 
+/* Frees the calling thread's per-device contexts (stream, pinned staging, device buffers) used by
+ * the four drop-in functions, NetUtil_MI355X_StreamSum32 and ..._ChkSumBatchStridedHost. They are
+ * also freed automatically when the thread exits; the next call re-creates them. */
+NET_ERR  NetUtil_MI355X_ThreadRelease      (void);
+
 /* NET_BUF chain walk of NetUtil_16BitOnesCplSumDataCalc (net_util.c:1589-1687) as pure host
  * logic: emits the spans whose concatenation is the checksummed stream (pseudo-header first).
+ * Chains of any length are walked. spans == NULL counts only (*p_n_spans = spans needed).
  * Returns NET_UTIL_ERR_NONE, NET_UTIL_ERR_INVALID_PROTOCOL, NET_UTIL_ERR_BUF_TOO_SMALL (more
- * than max_spans pieces) or — with dbg_chk != 0 — the NET_ERR_CFG_ARG_CHK_DBG_EN errors. */
+ * than max_spans pieces: the first max_spans are written and *p_n_spans is the count needed,
+ * so the caller can size an array and walk again) or — with dbg_chk != 0 — the
+ * NET_ERR_CFG_ARG_CHK_DBG_EN errors. On any other error *p_n_spans is 0. */
 NET_ERR  NetUtil_MI355X_ChainToSpans       (const void   *pdata_buf,
                                             const void   *ppseudo_hdr,
                                             CPU_INT16U    pseudo_hdr_size,

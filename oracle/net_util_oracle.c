@@ -403,6 +403,21 @@ void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const ui
     }
 }
 
+uint32_t Oracle_C1Loop(const void *pdata_buf, const void *ppseudo_hdr, uint16_t pseudo_hdr_size,
+                       const void *ip_hdr, uint64_t iters)
+{
+    uint32_t acc = 0u, err = 0u;
+    uint64_t k;
+    for (k = 0; k < iters; ++k) {
+        acc ^= Oracle_DataCalc(pdata_buf, ppseudo_hdr, pseudo_hdr_size, &err, 0);
+        acc ^= (uint32_t)Oracle_HdrCalc(ip_hdr, 20u, &err, 0) << 16;
+        acc += Oracle_HdrVerify(ip_hdr, 20u, &err, 0);
+        acc += Oracle_DataVerify(pdata_buf, ppseudo_hdr, pseudo_hdr_size, &err, 0);
+        __asm__ __volatile__("" : "+r"(acc) : : "memory");   /* one full sequence per iteration */
+    }
+    return acc ^ err;
+}
+
 int Oracle_MaxThreads(void)
 {
 #ifdef _OPENMP

@@ -64,6 +64,14 @@ void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const ui
                         uint16_t pseudo_len, uint32_t n_chains, void *out, int op, int n_threads);
 void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern);
 
+/* Config C1 (BASELINE configs[0]) per-datagram checksum sequence of the loopback UDP echo
+ * (SURVEY §3.1/§3.2), `iters` times on the same NET_BUF: Tx DataCalc(pbuf, pseudo, plen)
+ * (net_udp.c:2891) -> HdrCalc(ip_hdr, 20) (net_ipv4.c:9578) -> Rx HdrVerify(ip_hdr, 20)
+ * (net_ipv4.c:5247) -> DataVerify(pbuf, pseudo, plen) (net_udp.c:1934). Returns an XOR of the
+ * results (so no call is elided); bench.py times it for the C1 CPU per-call figure. */
+uint32_t Oracle_C1Loop(const void *pdata_buf, const void *ppseudo_hdr, uint16_t pseudo_hdr_size,
+                       const void *ip_hdr, uint64_t iters);
+
 /* Number of OpenMP threads the batch drivers would use with n_threads = 0. */
 int  Oracle_MaxThreads(void);
 

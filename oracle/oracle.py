@@ -77,6 +77,8 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.Oracle_BatchChains.restype = None
     L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
     L.Oracle_Fill.restype = None
+    L.Oracle_C1Loop.argtypes = [vp, vp, u16, vp, u64]
+    L.Oracle_C1Loop.restype = u32
     L.Oracle_MaxThreads.argtypes = []
     L.Oracle_MaxThreads.restype = i32
     return L
@@ -168,6 +170,11 @@ def fill(first_byte: int, n_bytes: int, seed: int, pattern: int = 0) -> np.ndarr
     buf = np.empty(n_bytes, dtype=np.uint8)
     lib().Oracle_Fill(buf.ctypes.data, first_byte, n_bytes, seed, pattern)
     return buf
+
+
+def c1_loop(pbuf, pseudo, pseudo_size, ip_hdr, iters: int) -> int:
+    """The C1 per-datagram sequence (DataCalc, HdrCalc, HdrVerify, DataVerify) `iters` times in C."""
+    return int(lib().Oracle_C1Loop(_ptr(pbuf), _ptr(pseudo), pseudo_size, _ptr(ip_hdr), iters))
 
 
 def max_threads() -> int:

@@ -1,0 +1,12 @@
+/* In-stack compile check: the stack configuration the drop-in reads (template values,
+ * Cfg/Template/net_cfg.h:184; the DBG build of the check sets NETCSUM_TEST_DBG). */
+#ifndef NET_CFG_MODULE_PRESENT
+#define NET_CFG_MODULE_PRESENT
+#include "lib_def.h"
+#ifdef NETCSUM_TEST_DBG
+#define NET_ERR_CFG_ARG_CHK_DBG_EN   DEF_ENABLED
+#else
+#define NET_ERR_CFG_ARG_CHK_DBG_EN   DEF_DISABLED
+#endif
+#define NET_TCP_MODULE_EN                        /* net_cfg_net.h: TCP configured in */
+#endif

@@ -72,7 +72,31 @@ def test_chain_to_spans_quirks_and_errors():
     ix = netcsum.Chain([{"data": b"abcd", "proto": 71, "transport_ix": 0xFFFF, "data_len": 0}])
     assert netcsum.chain_to_spans(ix.ptr, None, 0, dbg=True)[1] == 622
     many = netcsum.Chain([{"data": b"ab", "proto": 71}] * 10)
-    assert netcsum.chain_to_spans(many.ptr, None, 0, max_spans=4)[1] == netcsum.NET_UTIL_ERR_BUF_TOO_SMALL
+    spans, err = netcsum.chain_to_spans(many.ptr, None, 0, max_spans=4)      # caller's array too small:
+    assert err == netcsum.NET_UTIL_ERR_BUF_TOO_SMALL and len(spans) == 4      # first 4 + the count needed
+    spans, err = netcsum.chain_to_spans(many.ptr, None, 0)                   # auto-sized: all 10
+    assert err == 200 and [ln for _, ln in spans] == [2] * 10
+
+
+@pytest.mark.parametrize("nbuf", [63, 64, 65, 200, 1000])
+def test_chain_to_spans_long_chains_no_cap(nbuf):
+    """net_util.c:1611-1687 walks chains of any length (e.g. a 64 KiB datagram reassembled from
+    576-B-MTU fragments, net_ipv4.c:6523, is ~120 buffers): the walk has no span cap."""
+    rng = random.Random(nbuf)
+    chain = []
+    for i in range(nbuf):
+        ln = 0 if i % 17 == 5 else rng.randint(1, 97)                # odd splits, empty middles
+        chain.append({"data": rand_bytes(rng, ln), "proto": 70 if i == 0 else 71, "offset": rng.randint(0, 3)})
+    pseudo = rand_bytes(rng, 11)
+    ch = netcsum.Chain(chain)
+    ph = netcsum.HostBytes(pseudo, 1)
+    spans, err = netcsum.chain_to_spans(ch.ptr, ph.ptr, 11)
+    want, werr = onp.chain_stream([to_np_buf(b) for b in chain], pseudo)
+    assert err == werr == 200
+    assert _stream_bytes(spans) == want
+    n = ctypes.c_uint32(7)
+    assert netcsum.lib().NetUtil_MI355X_ChainToSpans(ch.ptr, ph.ptr, 11, None, 0, ctypes.byref(n), 0) == 200
+    assert n.value == len(spans)
 
 
 def test_batch_argument_validation_before_device_work():

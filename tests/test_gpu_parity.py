@@ -13,7 +13,7 @@ import pytest
 
 import netcsum
 import oracle
-from helpers import rand_bytes, rand_chain
+from helpers import rand_buf, rand_bytes, rand_chain
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -216,6 +216,30 @@ def test_reference_signatures_on_gpu_vs_oracle():
     assert netcsum.DataCalc(bad.ptr, None, 0) == (0, 211)
     ph12 = netcsum.HostBytes(b"\x0a\x00\x00\x01\x0a\x00\x00\x02\x00\x06\x00\x14")
     assert netcsum.DataCalc(None, ph12.ptr, 12) == oracle.data_calc(None, ph12.ptr, 12)
+
+
+@pytest.mark.parametrize("nbuf", [63, 64, 65, 120, 200, 1000])
+def test_reference_signatures_long_chains_vs_oracle(nbuf):
+    """DataCalc / DataVerify through the drop-in on NET_BUF chains longer than any fixed span
+    array (net_util.c:1611-1687 has no bound; a 64 KiB datagram reassembled from 576-B-MTU
+    fragments is ~120 buffers, net_ipv4.c:6523): odd splits, zero-length middles, odd and even
+    pseudo-headers, and a self-verifying chain, all against the C oracle."""
+    rng = random.Random(7000 + nbuf)
+    for it in range(4):
+        pat = ["random", "ff", "carry", "random"][it]
+        chain = []
+        for i in range(nbuf):
+            ln = 0 if i % 13 == 6 else rng.choice([1, 2, 3, rng.randint(1, 576)])
+            chain.append(rand_buf(rng, ln, pattern=pat) | {"offset": rng.randint(0, 3)})
+        plen = [12, 11, 40, 1][it]
+        ph = netcsum.HostBytes(rand_bytes(rng, plen, pat), rng.randint(0, 3))
+        ch = netcsum.Chain(chain)
+        args = (ch.ptr, ph.ptr, plen)
+        c = netcsum.DataCalc(*args)
+        assert c == oracle.data_calc(*args), (nbuf, it)
+        assert c[1] == 200
+        assert netcsum.DataVerify(*args) == oracle.data_verify(*args), (nbuf, it)
+        assert netcsum.DataCalc(ch.ptr, None, 0) == oracle.data_calc(ch.ptr, None, 0), (nbuf, it)
 
 
 def test_stream_sum32_reproduces_u32_wrap():

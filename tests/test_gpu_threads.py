@@ -1,0 +1,118 @@
+"""Host threading of the drop-in on the GPU (the reference is reentrant — no statics in
+net_util.c:159-449 — and serialised by the stack's global lock, Source/net.c:550; the GPU C ABI must
+be safe from one host thread per device):
+
+* the plain C caller (tests/c/dropin_caller.c, standalone build) with NETCSUM_EXPECT_GPU=1: every
+  device call succeeds and matches its own RFC 1071 sum, incl. two pthreads on one device and
+  chains of up to 1000 buffers;
+* two Python threads on one device (ctypes drops the GIL during the call) against the oracle;
+* one thread per device when the box has more than one GPU;
+* per-thread contexts are released at thread exit and by NetUtil_MI355X_ThreadRelease: 48 threads
+  that each stage a > 16 KiB packet leave no device memory behind.
+"""
+import os
+import random
+import subprocess
+import threading
+
+import pytest
+
+import netcsum
+import oracle
+from helpers import rand_buf, rand_chain
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_c_caller_on_gpu():
+    exe = os.path.join(REPO, "tests", "c", "build", "standalone")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "c"), "build/standalone"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, NETCSUM_EXPECT_GPU="1"))
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert r.stdout.startswith("ok ") and "device_missing=0" in r.stdout, r.stdout
+
+
+def _cases(seed, n):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        ch = netcsum.Chain(rand_chain(rng, rng.choice([20, 72, 1480, rng.randint(0, 20000)]), rng.randint(1, 5)))
+        ph = netcsum.HostBytes(bytes(rng.randrange(256) for _ in range(12)), rng.randint(0, 3))
+        out.append((ch, ph, oracle.data_calc(ch.ptr, ph.ptr, 12), oracle.data_verify(ch.ptr, ph.ptr, 12)))
+    return out
+
+
+def _worker(cases, dev, errors):
+    try:
+        torch.cuda.set_device(dev)
+        for k, (ch, ph, want_c, want_v) in enumerate(cases):
+            got = netcsum.DataCalc(ch.ptr, ph.ptr, 12)
+            if got != want_c:
+                errors.append((dev, k, got, want_c))
+            if netcsum.DataVerify(ch.ptr, ph.ptr, 12) != want_v:
+                errors.append((dev, k, "verify"))
+    except Exception as e:  # noqa: BLE001 — reported through the list
+        errors.append(repr(e))
+    finally:
+        netcsum.thread_release()
+
+
+def _run_threads(devs, per_thread=150):
+    errors = []
+    ths = [threading.Thread(target=_worker, args=(_cases(11 + i, per_thread), d, errors)) for i, d in enumerate(devs)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ths), "a drop-in thread did not finish"
+    assert errors == []
+
+
+def test_two_threads_one_device():
+    _run_threads([0, 0])
+
+
+def test_one_thread_per_device():
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("one GPU on this box")
+    _run_threads(list(range(min(n, 8))), per_thread=60)
+
+
+def test_thread_contexts_released():
+    """Each thread stages a 1.2 MB reassembled datagram (20 x 60000-B buffers: a 1.2 MB device
+    staging buffer, streams, pinned memory). After 48 such threads have exited (58 MB if leaked),
+    device memory is back where it was: contexts do not leak."""
+    rng = random.Random(3)
+    ch = netcsum.Chain([rand_buf(rng, 60000) for _ in range(20)])
+    want = oracle.data_calc(ch.ptr, None, 0)
+
+    def one(errors):
+        try:
+            if netcsum.DataCalc(ch.ptr, None, 0) != want:
+                errors.append("mismatch")
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    errors = []
+    t = threading.Thread(target=one, args=(errors,))
+    t.start()
+    t.join()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(48):
+        t = threading.Thread(target=one, args=(errors,))
+        t.start()
+        t.join(timeout=30)
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert errors == []
+    assert free0 - free1 < 32 << 20, f"{(free0 - free1) >> 20} MiB of device memory not released"
+    # explicit release on this thread, then the drop-in re-creates its context on the next call
+    assert netcsum.thread_release() == 200
+    assert netcsum.DataCalc(ch.ptr, None, 0) == want
+    assert netcsum.thread_release() == 200

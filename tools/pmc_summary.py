@@ -21,9 +21,16 @@ def kernel_rows(path, prefix):
     return d
 
 
-def main(tag, trace_dir, fetch_dir, write_dir, n_seg, seg_len=1500, plen=12):
+def main(tag, trace_dir, fetch_dir, write_dir, n_seg, bench_json=None, out_dir="profiles", seg_len=1500, plen=12):
     out = {"tag": tag, "n_seg": n_seg, "seg_len": seg_len, "pseudo_len": plen,
            "algorithmic_bytes_per_launch": n_seg * (seg_len + plen + 2)}
+    if bench_json:                    # the launched kernel form + the hash of its sources (bench.py checks both)
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        kd = json.loads(open(bench_json).read().strip().splitlines()[-1])["roofline"]["kernel"]
+        out["kernel_desc"] = kd
+        out["kernel_src_sha"] = bench.kernel_src_sha(kd.split("::")[-1].split("<")[0])
     tr = kernel_rows(f"{trace_dir}/trace_kernel_trace.csv", "netcsum::")
     kern = {}
     for name, rows in tr.items():
@@ -56,9 +63,10 @@ def main(tag, trace_dir, fetch_dir, write_dir, n_seg, seg_len=1500, plen=12):
         if tk:
             out["rocprof_avg_us"] = tk[0]["avg_us"]
             out["achieved_GBps_from_rocprof_avg"] = round(out["algorithmic_bytes_per_launch"] / (tk[0]["avg_us"] * 1e3), 1)
-    json.dump(out, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
+    json.dump(out, open(f"{out_dir}/{tag}_pmc.json", "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]),
+         sys.argv[6] if len(sys.argv) > 6 else None, sys.argv[7] if len(sys.argv) > 7 else "profiles")

@@ -264,8 +264,13 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a, uint32_t len_hint, hipStrea
 }
 
 // ----------------------------------------------------------- per-thread host-path contexts
+// One context per (host thread, device): its own stream, pinned staging, completion word and
+// device buffers, so one host thread per device needs no lock (SURVEY §8(b) threading). The
+// context is released when its thread exits (thread_local destructor) or on request
+// (NetUtil_MI355X_ThreadRelease); a partially failed initialisation is rolled back.
 struct HostCtx {
     bool                 ready = false;
+    int                  dev = -1;
     hipStream_t          stream = nullptr;
     uint8_t*             h_stage = nullptr;   // pinned
     uint8_t*             d_stage = nullptr;
@@ -279,6 +284,40 @@ struct HostCtx {
     hipStream_t          pstream[3] = {nullptr, nullptr, nullptr};
     uint8_t*             d_pipe[3] = {nullptr, nullptr, nullptr};
     size_t               pipe_cap = 0;
+
+    bool empty() const {
+        if (stream || h_stage || d_stage || d_sum || h_sum) return false;
+        for (int j = 0; j < 3; ++j) {
+            if (pstream[j] || d_pipe[j]) return false;
+        }
+        return true;
+    }
+    // Frees everything this context holds (on its own device), leaving it reusable.
+    void release() {
+        if (empty()) {
+            ready = false;
+            return;
+        }
+        int cur = -1;
+        const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+        if (dev >= 0) (void)hipSetDevice(dev);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (int j = 0; j < 3; ++j) {
+            if (pstream[j]) (void)hipStreamSynchronize(pstream[j]);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+        if (h_stage) (void)hipHostFree(h_stage);
+        if (d_stage) (void)hipFree(d_stage);
+        if (d_sum) (void)hipFree(d_sum);
+        if (h_sum) (void)hipHostFree(h_sum);
+        for (int j = 0; j < 3; ++j) {
+            if (pstream[j]) (void)hipStreamDestroy(pstream[j]);
+            if (d_pipe[j]) (void)hipFree(d_pipe[j]);
+        }
+        if (have_cur && cur != dev && cur >= 0) (void)hipSetDevice(cur);
+        *this = HostCtx{};
+    }
+    ~HostCtx() { release(); }
 };
 
 thread_local HostCtx tls_ctx[kMaxDev];
@@ -289,11 +328,17 @@ NET_ERR host_ctx(HostCtx** out) {
     if (dev < 0 || dev >= kMaxDev) return dev_fail("device index", hipErrorInvalidDevice);
     HostCtx& c = tls_ctx[dev];
     if (!c.ready) {
-        NC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-        NC_HIP(hipMalloc(&c.d_sum, 16));
+        c.release();                               // roll back a previous partial initialisation
+        c.dev = dev;
+        hipError_t e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc(&c.d_sum, 16);
         // coherent: the single-block kernel's system-scope completion store is visible while it runs
-        NC_HIP(hipHostMalloc(&c.h_sum, 16, hipHostMallocMapped | hipHostMallocCoherent));
-        NC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.h_sum_dev), c.h_sum, 0));
+        if (e == hipSuccess) e = hipHostMalloc(&c.h_sum, 16, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c.h_sum_dev), c.h_sum, 0);
+        if (e != hipSuccess) {
+            c.release();
+            return dev_fail("host context init", e);
+        }
         c.ready = true;
     }
     *out = &c;
@@ -434,6 +479,13 @@ NET_ERR NetUtil_MI355X_ChkSumBatchStridedHost(const void* h_seg, uint64_t seg_st
     }
     for (int j = 0; j < 3; ++j) {
         NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    }
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_ThreadRelease(void) {
+    for (int d = 0; d < kMaxDev; ++d) {
+        tls_ctx[d].release();
     }
     return NET_UTIL_ERR_NONE;
 }

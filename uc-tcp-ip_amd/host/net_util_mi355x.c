@@ -40,9 +40,10 @@
 
 #include <stddef.h>
 #include <stdio.h>
+#include <stdlib.h>
 
-#define NC_NEG_ZERO   0xFFFFu              /* NET_UTIL_16_BIT_ONES_CPL_NEG_ZERO (net_util.c:56) */
-#define NC_MAX_SPANS  64u                  /* pseudo-header + up to 63 chained buffers per call */
+#define NC_NEG_ZERO     0xFFFFu            /* NET_UTIL_16_BIT_ONES_CPL_NEG_ZERO (net_util.c:56) */
+#define NC_STACK_SPANS  64u                /* spans on the stack; longer chains use the heap */
 
 static CPU_INT16U nc_fold(uint32_t sum)
 {
@@ -60,11 +61,14 @@ NET_ERR NetUtil_MI355X_ChainToSpans(const void *pdata_buf, const void *ppseudo_h
                                     uint32_t max_spans, uint32_t *p_n_spans, int dbg_chk)
 {
     const NET_BUF *pbuf = (const NET_BUF *)pdata_buf;
-    uint32_t n = 0u;
+    uint32_t n = 0u;                                          /* spans the chain needs */
     int first = 1;
 
-    if (p_n_spans == NULL || (spans == NULL && max_spans != 0u)) {
+    if (p_n_spans == NULL) {
         return NET_ERR_FAULT_NULL_PTR;
+    }
+    if (spans == NULL) {                                      /* count-only walk */
+        max_spans = 0u;
     }
     *p_n_spans = 0u;
     if (dbg_chk && pdata_buf == NULL) {                       /* :1566-1570 */
@@ -79,15 +83,16 @@ NET_ERR NetUtil_MI355X_ChainToSpans(const void *pdata_buf, const void *ppseudo_h
             len = (CPU_INT16U)(len - 1u);
         }
         if (len != 0u) {
-            if (n >= max_spans) return NET_UTIL_ERR_BUF_TOO_SMALL;
-            spans[n].p = ppseudo_hdr;
-            spans[n].len = len;
-            spans[n].rsvd = 0u;
+            if (n < max_spans) {
+                spans[n].p = ppseudo_hdr;
+                spans[n].len = len;
+                spans[n].rsvd = 0u;
+            }
             ++n;
         }
     }
 
-    while (pbuf != NULL) {                                    /* :1611-1687 */
+    while (pbuf != NULL) {                                    /* :1611-1687, any chain length */
         const NET_BUF_HDR *h = &pbuf->Hdr;
         CPU_INT16U ix, len;
 
@@ -111,48 +116,62 @@ NET_ERR NetUtil_MI355X_ChainToSpans(const void *pdata_buf, const void *ppseudo_h
             len = (CPU_INT16U)h->DataLen;
             break;
         default:
-            *p_n_spans = 0u;
             return NET_UTIL_ERR_INVALID_PROTOCOL;            /* :1637-1639 */
         }
         if (dbg_chk && ix == NET_BUF_IX_NONE) {               /* :1642-1647 */
-            *p_n_spans = 0u;
             return NET_BUF_ERR_INVALID_IX;
         }
         if (dbg_chk && first) {                               /* :1660-1672 */
             first = 0;
             if (h->NextBufPtr == NULL && len == 0u) {
-                *p_n_spans = 0u;
                 return NET_UTIL_ERR_NULL_SIZE;
             }
         }
         if (len != 0u) {                                      /* zero-length buffers only pass */
-            if (n >= max_spans) {                             /* the carried octet through     */
-                *p_n_spans = 0u;
-                return NET_UTIL_ERR_BUF_TOO_SMALL;
+            if (n < max_spans) {                              /* the carried octet through     */
+                spans[n].p = pbuf->DataPtr + ix;
+                spans[n].len = len;
+                spans[n].rsvd = 0u;
             }
-            spans[n].p = pbuf->DataPtr + ix;
-            spans[n].len = len;
-            spans[n].rsvd = 0u;
             ++n;
         }
         pbuf = (const NET_BUF *)h->NextBufPtr;
     }
     *p_n_spans = n;
+    if (spans != NULL && n > max_spans) {
+        return NET_UTIL_ERR_BUF_TOO_SMALL;                    /* *p_n_spans = the count needed */
+    }
     return NET_UTIL_ERR_NONE;
 }
 
 /* The reference's u32 accumulator for one packet, summed on the GPU. */
+/* The chain may be any length (net_util.c:1611-1687 has no bound; e.g. a 64 KiB datagram
+ * reassembled from 576-B-MTU fragments is ~120 buffers, net_ipv4.c:6523): short chains use a
+ * stack array, longer ones a heap array sized by the walk's own count. */
 static NET_ERR nc_data_sum32(void *pdata_buf, void *ppseudo_hdr, CPU_INT16U pseudo_hdr_size,
                              uint32_t *p_sum32)
 {
-    NETCSUM_SPAN spans[NC_MAX_SPANS];
+    NETCSUM_SPAN stack_spans[NC_STACK_SPANS];
+    NETCSUM_SPAN *spans = stack_spans;
     uint32_t n = 0u;
     NET_ERR err = NetUtil_MI355X_ChainToSpans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, spans,
-                                              NC_MAX_SPANS, &n, NETCSUM_ARG_CHK_DBG_EN);
-    if (err != NET_UTIL_ERR_NONE) {
-        return err;
+                                              NC_STACK_SPANS, &n, NETCSUM_ARG_CHK_DBG_EN);
+    if (err == NET_UTIL_ERR_BUF_TOO_SMALL) {
+        spans = (NETCSUM_SPAN *)malloc((size_t)n * sizeof(NETCSUM_SPAN));
+        if (spans == NULL) {
+            fprintf(stderr, "[netcsum-mi355x] out of host memory for a %u-buffer chain\n", (unsigned)n);
+            return (NET_ERR)NET_UTIL_ERR_MI355X_DEV;
+        }
+        err = NetUtil_MI355X_ChainToSpans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, spans, n, &n,
+                                          NETCSUM_ARG_CHK_DBG_EN);
     }
-    return NetUtil_MI355X_StreamSum32(spans, n, p_sum32);
+    if (err == NET_UTIL_ERR_NONE) {
+        err = NetUtil_MI355X_StreamSum32(spans, n, p_sum32);
+    }
+    if (spans != stack_spans) {
+        free(spans);
+    }
+    return err;
 }
 
 static NET_ERR nc_hdr_sum32(void *phdr, CPU_INT16U hdr_size, uint32_t *p_sum32)

@@ -185,6 +185,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_16BitSumDataCalcAlign_32.restype = u32
     L.NetUtil_MI355X_StreamSum32.argtypes = [ctypes.POINTER(Span), u32, ctypes.POINTER(ctypes.c_uint32)]
     L.NetUtil_MI355X_StreamSum32.restype = i32
+    L.NetUtil_MI355X_ThreadRelease.argtypes = []
+    L.NetUtil_MI355X_ThreadRelease.restype = i32
     L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
                                               ctypes.POINTER(ctypes.c_uint32), i32]
     L.NetUtil_MI355X_ChainToSpans.restype = i32
@@ -288,13 +290,27 @@ def SumDataCalcAlign_32(pdata_32, size):
     return int(lib().NetUtil_16BitSumDataCalcAlign_32(_p(pdata_32), size))
 
 
-def chain_to_spans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, dbg=False, max_spans=64):
-    spans = (Span * max_spans)()
+def chain_to_spans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, dbg=False, max_spans=None):
+    """Spans of the chain's checksummed stream. max_spans=None sizes the array by a count-only
+    walk first (chains of any length); a fixed max_spans returns BUF_TOO_SMALL past it, with the
+    first max_spans spans and n = the count needed."""
     n = ctypes.c_uint32(0)
+    if max_spans is None:
+        err = lib().NetUtil_MI355X_ChainToSpans(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size, None, 0,
+                                                ctypes.byref(n), int(dbg))
+        if err != NET_UTIL_ERR_NONE:
+            return [], int(err)
+        max_spans = n.value
+    spans = (Span * max(1, max_spans))()
     err = lib().NetUtil_MI355X_ChainToSpans(_p(pdata_buf), _p(ppseudo_hdr), pseudo_hdr_size, spans,
                                             max_spans, ctypes.byref(n), int(dbg))
-    out = [(spans[i].p, spans[i].len) for i in range(n.value)]
+    out = [(spans[i].p, spans[i].len) for i in range(min(n.value, max_spans))]
     return out, int(err)
+
+
+def thread_release():
+    """Free the calling thread's per-device drop-in contexts (also done at thread exit)."""
+    return int(lib().NetUtil_MI355X_ThreadRelease())
 
 
 def stream_sum32(spans):
