@@ -142,7 +142,9 @@ NET_ERR  NetUtil_MI355X_ChkSumBatchStridedHost(const void  *h_seg,
 /* ============================================================================================
  * (2b) IPv4 packet batches. Packet i = one IPv4 datagram starting at
  * its IP header: d_base + d_off[i] with d_len[i] bytes present (d_off/d_len non-NULL), or
- * d_base + i*stride with pkt_len bytes present (d_off = d_len = NULL). Any alignment.
+ * d_base + i*stride with pkt_len bytes present (d_off = d_len = NULL). Any alignment. Strided
+ * batches need 7 * stride + 65536 < 2^32 (packets at most ~613 MB apart), else
+ * NET_UTIL_ERR_MI355X_INVALID_ARG; offset/length batches have no such bound.
  *
  * RxValidateIPv4 — one HBM pass per packet, d_flags[i] = NETCSUM_PKT_* bits:
  *   IP_OK       NetUtil_16BitOnesCplChkSumHdrVerify(ip_hdr, IHL*4) == DEF_OK      (net_ipv4.c:5247)

@@ -113,6 +113,10 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(10, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Fill(3, 10, 0, 0, 0, None) == 219                   # not 8-B aligned
     assert L.NetUtil_MI355X_ReadStream(16, 17, 8, None) == 219                # not a multiple of 16
+    # strided packet batches: a stride whose 32-bit store offsets would wrap is refused (G = 8 for
+    # 1500-B packets -> 7 strides + 64 KiB must stay below 2^32), checked before any device work
+    big = (1 << 32) // 7
+    assert L.NetUtil_MI355X_TxFinalizeIPv4(16, None, None, big, 1500, 4, None, 1, None) in (219, 218)
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU behaviour")

@@ -575,6 +575,12 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     }
     c.group_lanes = pow2_group((uint32_t)g);
     c.chunks_per_pass = (int)std::min<uint32_t>(8u, std::max<uint32_t>(1u, (chunks + c.group_lanes - 1u) / c.group_lanes));
+    // Strided batches store through a buffer resource based at each wave's first packet of a stage,
+    // reaching the stage's other 64/G - 1 packets by 32-bit offsets (netcsum_packets.hip pkt_store):
+    // a stride that would wrap them is refused, never silently mis-addressed.
+    if (d_off == nullptr && (uint64_t)(64u / (uint32_t)c.group_lanes - 1u) * stride + 65536u >= 0xFFFFFFFFull) {
+        return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    }
     // Rx streams with nt loads; Tx re-writes header lines it has just read and is faster with plain
     // loads (profiles/r1tc_tx_sweep.jsonl: 0.323 vs 0.356 ms at tile 2).
     const int nt = g_tune_nt.load();
