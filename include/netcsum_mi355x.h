@@ -301,6 +301,17 @@ NET_ERR  NetUtil_MI355X_StreamSum32        (const NETCSUM_SPAN *spans,
                                             uint32_t            n_spans,
                                             uint32_t           *p_sum32);
 
+/* Multi-GPU partition of a variable-length batch by bytes: rank r of `world`
+ * checksums segments [first[r], first[r+1]) — contiguous ranges whose len + pseudo_len byte totals
+ * are equal to within one segment (prefix sum; first[0] = 0, first[world] = n_seg; `first` holds
+ * world + 1 entries). Host logic, no device work; per-segment results are independent, so the
+ * union of the ranks' outputs is the single-GPU result. */
+NET_ERR  NetUtil_MI355X_ShardVarLen        (const uint16_t *seg_len,
+                                            uint32_t        n_seg,
+                                            CPU_INT16U      pseudo_len,
+                                            uint32_t        world,
+                                            uint32_t       *first);
+
 /* Frees the calling thread's per-device contexts (stream, pinned staging, device buffers) used by
  * the four drop-in functions, NetUtil_MI355X_StreamSum32 and ..._ChkSumBatchStridedHost. They are
  * also freed automatically when the thread exits; the next call re-creates them. */

@@ -76,3 +76,70 @@ def test_pseudo_headers_shape_and_fields():
     assert (ph[:, 9] == 6).all() and (ph[:, 8] == 0).all()
     assert ph[0, 10] == 1500 >> 8 and ph[0, 11] == 1500 & 0xFF
     assert bytes(ph[0, 0:4]) == bytes([0x0A, 0, 0, 5])
+
+
+def _varlen_worker(rank, world, port, lens, q):
+    """Rank r checksums ITS byte-balanced range of one global C4-shaped batch (contiguous, packed)."""
+    import netcsum
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first = netcsum.shard_varlen(lens, 12, world)
+    base, off, ph = _c4_host(lens)
+    a, b = int(first[rank]), int(first[rank + 1])
+    out = oracle.batch_varlen(base, off[a:b], lens[a:b], ph[12 * a:12 * b], 12, 12, oracle.OP_DATA_CALC)
+    mine = torch.from_numpy(out.astype(np.int32))
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([b - a]))
+    m = max(int(s.item()) for s in sizes)
+    parts = [torch.zeros(m, dtype=torch.int32) for _ in sizes]
+    dist.all_gather(parts, torch.nn.functional.pad(mine, (0, m - mine.numel())))   # test-only gather
+    parts = [p[: int(s.item())] for p, s in zip(parts, sizes)]
+    byte_tot = torch.tensor([int(lens[a:b].astype(np.int64).sum()) + 12 * (b - a)])
+    allb = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allb, byte_tot)
+    if rank == 0:
+        q.put((torch.cat(parts).numpy().astype(np.uint16), [int(x.item()) for x in allb]))
+    dist.destroy_process_group()
+
+
+def _c4_host(lens):
+    off = np.zeros(len(lens), np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    base = oracle.fill(0, int(off[-1]) + int(lens[-1]) + 16, bench.SEED, 0)
+    ph = np.random.default_rng(11).integers(0, 256, size=12 * len(lens), dtype=np.uint8)
+    return base, off, ph
+
+
+def test_varlen_byte_balanced_shards_union_equals_single_run():
+    """C4 split for N GPUs: NetUtil_MI355X_ShardVarLen's prefix-sum ranges carry equal
+    bytes to within one datagram and their union is the single-GPU result."""
+    world = 2
+    lens = np.random.default_rng(7).integers(40, 9001, size=3000).astype(np.uint16)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_varlen_worker, args=(r, world, port, lens, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, byte_tot = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    base, off, ph = _c4_host(lens)
+    want = oracle.batch_varlen(base, off, lens, ph, 12, 12, oracle.OP_DATA_CALC)
+    assert np.array_equal(got, want)
+    assert max(byte_tot) - min(byte_tot) <= 2 * (9000 + 12)
+
+
+def test_varlen_shard_boundaries():
+    import netcsum
+    rng = np.random.default_rng(7)
+    lens = rng.integers(40, 9001, size=1 << 20).astype(np.uint16)
+    for world in (1, 2, 3, 4, 8):
+        f = netcsum.shard_varlen(lens, 12, world)
+        assert f[0] == 0 and f[-1] == len(lens) and (np.diff(f.astype(np.int64)) >= 0).all()
+        b = [int(lens[f[r]:f[r + 1]].astype(np.int64).sum()) + 12 * int(f[r + 1] - f[r]) for r in range(world)]
+        assert max(b) - min(b) <= 2 * (9000 + 12), (world, b)
+    assert list(netcsum.shard_varlen(np.zeros(0, np.uint16), 12, 4)) == [0, 0, 0, 0, 0]
+    assert list(netcsum.shard_varlen(np.array([100], np.uint16), 0, 3)) == [0, 1, 1, 1]

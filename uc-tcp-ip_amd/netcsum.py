@@ -185,6 +185,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_16BitSumDataCalcAlign_32.restype = u32
     L.NetUtil_MI355X_StreamSum32.argtypes = [ctypes.POINTER(Span), u32, ctypes.POINTER(ctypes.c_uint32)]
     L.NetUtil_MI355X_StreamSum32.restype = i32
+    L.NetUtil_MI355X_ShardVarLen.argtypes = [vp, u32, u16, u32, vp]
+    L.NetUtil_MI355X_ShardVarLen.restype = i32
     L.NetUtil_MI355X_ThreadRelease.argtypes = []
     L.NetUtil_MI355X_ThreadRelease.restype = i32
     L.NetUtil_MI355X_ChainToSpans.argtypes = [vp, vp, u16, ctypes.POINTER(Span), u32,
@@ -306,6 +308,19 @@ def chain_to_spans(pdata_buf, ppseudo_hdr, pseudo_hdr_size, dbg=False, max_spans
                                             max_spans, ctypes.byref(n), int(dbg))
     out = [(spans[i].p, spans[i].len) for i in range(min(n.value, max_spans))]
     return out, int(err)
+
+
+def shard_varlen(seg_len, pseudo_len: int, world: int):
+    """Byte-balanced contiguous ranks of a varlen batch (NetUtil_MI355X_ShardVarLen): returns the
+    world + 1 boundaries, rank r owning segments [first[r], first[r+1])."""
+    import numpy as np
+    lens = np.ascontiguousarray(seg_len, dtype=np.uint16)
+    first = np.zeros(world + 1, np.uint32)
+    err = lib().NetUtil_MI355X_ShardVarLen(lens.ctypes.data if lens.size else None, lens.size, pseudo_len,
+                                            world, first.ctypes.data)
+    if err != NET_UTIL_ERR_NONE:
+        raise ValueError(f"NetUtil_MI355X_ShardVarLen: NET_ERR {err}")
+    return first
 
 
 def thread_release():
