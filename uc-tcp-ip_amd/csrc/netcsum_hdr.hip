@@ -83,7 +83,10 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
     const bool verify = A.verify != 0u;
     const __amdgpu_buffer_rsrc_t ro = rsrc(A.out, verify ? n : 2u * n);
 
-    // Issue tile i (< cnt) into ring slot i % S.
+    // Issue tile i (< cnt) into ring slot i % S: always exactly P LDS-DMA loads, every one with at
+    // least one in-range lane. A piece wholly past a short (last) tile re-reads piece 0's bytes into
+    // its own LDS slot (never read back) instead of issuing an all-out-of-range load, whose return
+    // order relative to the other loads is the one thing the hand-counted waits cannot rely on.
     auto issue = [&](uint32_t i) {
         const uint32_t slot = i % (uint32_t)S;
         const uint32_t h0 = (t0 + i * W) * TH;
@@ -94,8 +97,9 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
         const __amdgpu_buffer_rsrc_t r = rsrc(reinterpret_cast<const void*>(i0), (bytes + 15u) & ~15u);
 #pragma unroll
         for (int p = 0; p < P; ++p) {
+            const uint32_t pb = (1024u * (uint32_t)p < bytes) ? 1024u * (uint32_t)p : 0u;   // wave-uniform
             __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t*)&img[w][slot][p * 256], 16,
-                                                     (int)(1024u * (uint32_t)p + 16u * lane), 0, 0, 2);
+                                                     (int)(pb + 16u * lane), 0, 0, 2);
         }
     };
 
@@ -106,6 +110,19 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
             issue((uint32_t)j);
         }
     }
+    // Wait counts. Issue order of a wave with cnt tiles: tiles 0..S-2 in the prologue, then tile i+S-1
+    // at the top of iteration i (if it exists), P loads each; loads retire in issue order, stores
+    // are not counted. When iteration i waits for tile i, the loads issued after tile i's are those of
+    // tiles i+1 .. min(i+S-1, cnt-1): m = min(S-1, cnt-1-i) tiles = m*P loads, so vmcnt(m*P) returns
+    // exactly when tile i has landed:
+    //
+    //   S | cnt-1-i >= S-1 (steady) | cnt-1-i = 2   | cnt-1-i = 1 | cnt-1-i = 0 (last tile)
+    //   2 | m = 1: vmcnt(P)         |  (steady)     |  (steady)   | m = 0: vmcnt(0)
+    //   3 | m = 2: vmcnt(2P)        |  (steady)     | vmcnt(P)    | vmcnt(0)
+    //   4 | m = 3: vmcnt(3P)        | vmcnt(2P)     | vmcnt(P)    | vmcnt(0)
+    //
+    // (a wave with cnt < S tiles starts in the tail columns). tests/test_gpu_hdr_waits.py runs every
+    // instance with waves owning exactly 1 .. S+1 tiles, full and short last tiles, against the oracle.
     for (uint32_t i = 0; i < cnt; ++i) {
         if (i + (uint32_t)S - 1u < cnt) {
             issue(i + (uint32_t)S - 1u);

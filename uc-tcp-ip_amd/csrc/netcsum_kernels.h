@@ -78,6 +78,7 @@ bool small_supported(const SegBatchArgs& a);  // strided, no pseudo, 1..64 B, ba
 hipError_t launch_small_batch(const SegBatchArgs& a, int grid, hipStream_t s);
 bool hdr_supported(const SegBatchArgs& a);     // small_supported and stride <= 64: LDS-image header tiles
 int hdr_lanes_h(const SegBatchArgs& a, int h);  // headers per lane kernel 7 uses for a request (auto: h <= 0)
+uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per tile of 64*h headers
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256

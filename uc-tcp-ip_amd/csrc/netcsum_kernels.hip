@@ -970,9 +970,12 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     const int kid = (c.kernel >= 1 && c.kernel <= 7) ? c.kernel : 0;
     if (kid == 7) {
         const int h = hdr_lanes_h(a, c.tile);
-        const int smax = h == 4 ? 3 : 4;                          // stages the H instantiations exist for
-        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<S=%d,H=%d> block=256 grid=%d",
-                 c.chunks_per_pass < smax ? c.chunks_per_pass : smax, h, c.grid);
+        const int st = c.chunks_per_pass;                         // as launch_hdr_batch resolves it
+        const int S = std::min(st == 3 ? 3 : (st == 4 ? 4 : 2), h == 4 ? 3 : 4);
+        const uint32_t tiles = (a.n_seg + 64u * h - 1u) / (64u * h);
+        const uint32_t g = c.grid > 0 ? (uint32_t)c.grid : (tiles + 15u) / 16u;
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdr_kernel<P=%u,S=%d,H=%d> block=256 grid=%u",
+                 hdr_pieces(a, h), S, h, std::max<uint32_t>(1u, std::min<uint32_t>(g, (tiles + 3u) / 4u)));
         return;
     }
     if (kid == 6) {
