@@ -216,7 +216,7 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
 # Sources that define each dominant kernel: a PMC summary is valid only for the exact sources it was
 # collected from (tools/pmc_summary.py records their hash; bench.py recomputes it here).
 KERNEL_SOURCES = {
-    "seg_stream_kernel": ["netcsum_stream.hip", "netcsum_device.h", "netcsum_kernels.h"],
+    "seg_stream_kernel": ["netcsum_stream.hip", "netcsum_stream.h", "netcsum_device.h", "netcsum_kernels.h"],
 }
 
 

@@ -374,10 +374,16 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
-    NETCSUM_TUNE_TILE          = 9    /* J > 0: each block owns a contiguous tile of J segments per
+    NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).
                                          Kernel 6: J > 0 = segments per wave run (<= 128; auto 16).
-                                         Kernel 7: headers per lane, 1, 2 or 4 (auto 2)              */
+                                         Kernel 7: headers per lane, 1, 2 or 4 (auto 2).
+                                         IPv4 packet batches: packets per wave run of the run-stream
+                                         form (<= 64; auto 16); TUNE_KERNEL 2 forces the lane-group
+                                         packet kernel                                              */
+    NETCSUM_TUNE_TX_PASSES     = 10   /* run-stream Tx finalize: 0 auto (1), 1 checksum fields written
+                                         by the checksum pass, 2 checksum pass writes 8-B records,
+                                         a scatter pass writes the fields                            */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -110,7 +110,8 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(10, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(11, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_PASSES, 3) == 219
     assert L.NetUtil_MI355X_Fill(3, 10, 0, 0, 0, None) == 219                   # not 8-B aligned
     assert L.NetUtil_MI355X_ReadStream(16, 17, 8, None) == 219                # not a multiple of 16
     # strided packet batches: a stride whose 32-bit store offsets would wrap is refused (G = 8 for

@@ -8,6 +8,8 @@ a 16-B-aligned and a 4-B-offset base, HdrCalc and HdrVerify, against the oracle 
 of net_util.c:159-284). One run per case; no repeat-run probes.
 
 (P, H) = (1, 4) is unreachable: a 256-header tile of >= 1-B headers at a stride >= 4 is > 1 KiB.
+P is exact for the base's offset in its 16-B line (hdr_pieces), so each case picks its shape for
+the lead it runs at.
 """
 import numpy as np
 import pytest
@@ -24,17 +26,17 @@ INSTANCES = [(p, s, 1) for p in range(1, 6) for s in (2, 3, 4)] + \
             [(p, s, 4) for p in range(2, 7) for s in (2, 3)]
 
 
-def _pieces(L, st, h):
-    return (12 + (64 * h - 1) * st + L + 1023) // 1024
+def _pieces(L, st, h, lead):
+    return (lead + (64 * h - 1) * st + L + 1023) // 1024
 
 
-def _shape(P, H):
-    """The longest header (len <= stride <= 64, both multiples of 4 for the stride) whose 64H-header
-    tile takes P pieces and that the kernel accepts (hdr_supported, hdr_lanes_h keeps H)."""
+def _shape(P, H, lead):
+    """The longest header (len <= stride <= 64, stride a multiple of 4) whose 64H-header tile takes P
+    pieces at this lead and that the kernel accepts (hdr_supported, hdr_lanes_h keeps H)."""
     best = None
     for st in range(4, 65, 4):
         for L in range(1, st + 1):
-            if _pieces(L, st, 1) > 5 or _pieces(L, st, H) > 6 or _pieces(L, st, H) != P:
+            if _pieces(L, st, 1, lead) > 5 or _pieces(L, st, H, lead) > 6 or _pieces(L, st, H, lead) != P:
                 continue
             if best is None or (L, -st) > (best[0], -best[1]):
                 best = (L, st)
@@ -55,7 +57,6 @@ def _tuning():
 
 @pytest.mark.parametrize("P,S,H", INSTANCES)
 def test_hdr_kernel_every_tail_branch(P, S, H):
-    L, st = _shape(P, H)
     netcsum.tune(netcsum.TUNE_KERNEL, 7)
     netcsum.tune(netcsum.TUNE_CHUNKS, S)
     netcsum.tune(netcsum.TUNE_TILE, H)
@@ -66,8 +67,13 @@ def test_hdr_kernel_every_tail_branch(P, S, H):
         for short in (0, 5):
             n = 4 * cnt * TH - short
             for lead in (0, 4):
+                shape = _shape(P, H, lead)
+                if shape is None:
+                    continue
+                L, st = shape
                 host = rng.integers(0, 256, size=lead + n * st + 64, dtype=np.uint8)
                 dev = torch.from_numpy(host).to(DEV)
+                assert (dev.data_ptr() + lead) % 16 == lead
                 for op in (2, 3):
                     out = torch.zeros(n, dtype=torch.int16 if op == 2 else torch.uint8, device=DEV)
                     netcsum.batch_strided(dev[lead:], st, L, None, 0, 0, n, out, op)

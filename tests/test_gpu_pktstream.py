@@ -1,0 +1,152 @@
+"""GPU parity of the run-stream packet kernel (netcsum_pktstream.hip: strided IPv4 batches, fused Rx
+validation and Tx finalize) against the packet oracle (oracle/oracle_packets.py, which composes the
+C restatement's HdrVerify / DataVerify / HdrCalc / DataCalc the way net_ipv4.c, net_tcp.c,
+net_udp.c, net_icmpv4.c and net_igmp.c call them), and against the lane-group kernel it replaces
+for these batches (TUNE_KERNEL 2): every packet kind incl. malformed ones, IP options, stale
+checksum fields, odd and even base addresses, dense and gapped strides, run lengths 1..64, plain
+and non-temporal loads, UDP Tx checksums on and off. Every byte outside the written fields must be
+left as it was (gaps between packets, the bytes past the last one)."""
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle_packets as op
+from packets import KINDS, make_packet
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _defaults():
+    def reset():
+        netcsum.tune(netcsum.TUNE_KERNEL, 0)
+        netcsum.tune(netcsum.TUNE_TILE, -1)
+        netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+        netcsum.tune(netcsum.TUNE_CHUNKS, 0)
+        netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
+    reset()
+    yield
+    reset()
+
+
+def _batch(rng, n, stride, pkt_len, lead):
+    buf = np.frombuffer(rng.randbytes(lead + n * stride + 96), np.uint8).copy()
+    for i in range(n):
+        kind = rng.choice(KINDS + ["udp", "tcp", "icmp", "igmp"])
+        p = bytearray(make_packet(rng, kind, payload=rng.randint(0, max(0, pkt_len - 80))))
+        if rng.random() < 0.1:                                    # longer than the slot: truncated
+            p = bytearray(make_packet(rng, kind, payload=pkt_len))
+        p = p[:pkt_len]
+        if len(p) >= 12 and rng.random() < 0.5:
+            p[10:12] = rng.randbytes(2)                           # stale IP checksum field
+        o = lead + i * stride
+        buf[o:o + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    return buf
+
+
+def _want(buf, n, stride, pkt_len, lead, udp_tx_csum):
+    rx = np.zeros(n, np.uint8)
+    tx_buf = buf.copy()
+    tx_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        o = lead + i * stride
+        pkt = bytes(buf[o:o + pkt_len])
+        rx[i] = op.rx_validate(pkt)
+        q, tx_f[i] = op.tx_finalize(pkt, udp_tx_csum)
+        tx_buf[o:o + pkt_len] = np.frombuffer(q, np.uint8)
+    return rx, tx_buf, tx_f
+
+
+def _run(buf, n, stride, pkt_len, lead, udp_tx_csum):
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv4(b[lead:], n, f, stride=stride, pkt_len=pkt_len)
+    torch.cuda.synchronize()
+    rx_desc = netcsum.last_launch()
+    rx = f.cpu().numpy()
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b[lead:], n, ft, stride=stride, pkt_len=pkt_len, udp_tx_csum=udp_tx_csum)
+    torch.cuda.synchronize()
+    return rx, b.cpu().numpy(), ft.cpu().numpy(), rx_desc, netcsum.last_launch()
+
+
+SHAPES = [(1500, 1500), (1514, 1514), (1540, 1514), (1501, 1500), (64, 64), (100, 64), (577, 577), (9000, 9000),
+          (4096, 4040)]
+
+
+@pytest.mark.parametrize("stride,pkt_len", SHAPES)
+@pytest.mark.parametrize("lead", [0, 1, 6])
+@pytest.mark.parametrize("passes", [1, 2])
+def test_pkt_stream_vs_oracle(stride, pkt_len, lead, passes):
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    rng = random.Random(stride * 131 + pkt_len * 7 + lead)
+    n = 700 if stride < 5000 else 200
+    udp_tx_csum = lead != 6
+    buf = _batch(rng, n, stride, pkt_len, lead)
+    rx_w, tx_w, txf_w = _want(buf, n, stride, pkt_len, lead, udp_tx_csum)
+    rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, lead, udp_tx_csum)
+    assert d_rx.startswith("pkt_stream_kernel") and d_tx.startswith("pkt_stream_kernel"), (d_rx, d_tx)
+    bad = np.nonzero(rx != rx_w)[0]
+    assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
+    bad = np.nonzero(tx != tx_w)[0]
+    assert bad.size == 0, [(int(j), (int(j) - lead) // stride, (int(j) - lead) % stride, int(tx[j]), int(tx_w[j]))
+                           for j in bad[:8]]
+    assert np.array_equal(txf, txf_w)
+
+
+@pytest.mark.parametrize("spw", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("nt,depth", [(0, 4), (1, 8)])
+def test_pkt_stream_run_lengths_and_loads_equal_lane_group_kernel(spw, nt, depth):
+    rng = random.Random(spw * 3 + nt)
+    stride, pkt_len, lead, n = 1518, 1514, 3, 1000
+    buf = _batch(rng, n, stride, pkt_len, lead)
+    netcsum.tune(netcsum.TUNE_KERNEL, 2)                         # the lane-group kernel: reference run
+    rx_ref, tx_ref, txf_ref, d_rx, _ = _run(buf, n, stride, pkt_len, lead, True)
+    assert d_rx.startswith("pkt_batch_kernel"), d_rx
+    netcsum.tune(netcsum.TUNE_KERNEL, 0)
+    netcsum.tune(netcsum.TUNE_TILE, spw)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+    netcsum.tune(netcsum.TUNE_CHUNKS, depth)
+    rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, lead, True)
+    assert f"pkts_per_wave={spw}" in d_rx and f"D={depth}" in d_tx, (d_rx, d_tx)
+    assert np.array_equal(rx, rx_ref)
+    assert np.array_equal(tx, tx_ref)
+    assert np.array_equal(txf, txf_ref)
+    rx_w, tx_w, _ = _want(buf, n, stride, pkt_len, lead, True)
+    assert np.array_equal(rx, rx_w) and np.array_equal(tx, tx_w)
+
+
+def test_pkt_stream_c2_shape_round_trip_1M():
+    """1 M x 1500-B TCP datagrams (the Tx / Rx config of DESIGN §9): Tx finalize, then Rx accepts
+    every packet; one flipped byte per 1000 packets is caught exactly; 4096 sampled packets equal
+    the oracle's Tx bytes."""
+    n, L = 1 << 20, 1500
+    pk = torch.empty(n * L + 256, dtype=torch.uint8, device=DEV)
+    netcsum.fill(pk, n * L, 0x5EED0001, 0)
+    v = pk[: n * L].view(n, L)
+    v[:, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8,
+                              device=DEV)
+    smp = np.sort(np.random.default_rng(5).choice(n, size=4096, replace=False))
+    sidx = torch.from_numpy(smp).to(DEV)
+    before = v[sidx].cpu().numpy()
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith("pkt_stream_kernel")
+    after = v[sidx].cpu().numpy()
+    for j in range(len(smp)):
+        assert bytes(after[j]) == op.tx_finalize(bytes(before[j]), True)[0], int(smp[j])
+    netcsum.rx_validate_ipv4(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    ok = op.IP_OK | op.L4_OK | op.L4_CHECKED
+    assert bool(((f & ok) == ok).all())
+    bad = torch.arange(0, n, 1000, device=DEV)
+    v[bad, 777] ^= 0x04
+    netcsum.rx_validate_ipv4(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    failed = torch.nonzero((f & op.L4_OK) == 0).flatten()
+    assert torch.equal(failed, bad)

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Rx / Tx packet-batch timing on 1 M x 1500-B IPv4/TCP datagrams (strided, in place):
+the lane-group kernel (TUNE_KERNEL 2, tile 2) against the run-stream kernel over packets per wave
+(TUNE_TILE), load policy (TUNE_NT_LOADS) and pieces in flight (TUNE_CHUNKS 4 / 8). Tx restores
+nothing between launches: its written fields are the same every time. Prints JSON lines."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("uc-tcp-ip_amd", "oracle", "tests", "tools", ""):
+    sys.path.insert(0, os.path.join(REPO, sub))
+import torch  # noqa: E402
+
+import netcsum  # noqa: E402
+from bench import SEED  # noqa: E402
+from bench_configs import events_ms  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n, L = 1 << 20, 1500
+    pk = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(pk, n * L, SEED, 0)
+    v = pk[: n * L].view(n, L)
+    v[:, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8, device=dev)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    netcsum.tx_finalize_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)
+    torch.cuda.synchronize()
+    variants = [dict(kernel=2, tile=2, nt=-1, chunks=0, passes=0)]
+    for spw in [int(x) for x in os.environ.get("PS_SPW", "8,16,32").split(",")]:
+        for nt in (1, 0):
+            for d in (4, 8):
+                for passes in (1, 2):
+                    variants.append(dict(kernel=0, tile=spw, nt=nt, chunks=d, passes=passes))
+    for var in variants:
+        netcsum.tune(netcsum.TUNE_TX_PASSES, var["passes"])
+        netcsum.tune(netcsum.TUNE_KERNEL, var["kernel"])
+        netcsum.tune(netcsum.TUNE_TILE, var["tile"])
+        netcsum.tune(netcsum.TUNE_NT_LOADS, var["nt"])
+        netcsum.tune(netcsum.TUNE_CHUNKS, var["chunks"])
+        res = {}
+        for name, fn in (("rx", lambda: netcsum.rx_validate_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)),
+                         ("tx", lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st))):
+            ms = events_ms(fn, st, reps=60, warm_s=0.3)
+            res[name] = {"ms": round(ms, 4), "GBps": round(n * (L + 1) / ms / 1e6, 1), "kernel": netcsum.last_launch()}
+        ok = bool(((flags & 0x07) == 0x07).all())
+        print(json.dumps({"variant": var, **res, "all_valid_after_tx": ok}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

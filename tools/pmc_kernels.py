@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise tools/gpu_pmc.sh output for one config: per netcsum kernel the rocprofv3 kernel-trace
+average duration and the FETCH_SIZE / WRITE_SIZE PMC per launch (median), HBM bytes per launch
+= FETCH_SIZE x 1024 x 2 (gfx950 correction for 16-B/lane streaming reads, MI355X_MICROARCH.md §HBM)
++ WRITE_SIZE x 1024, and the ratio to the algorithmic bytes tools/run_config.py printed."""
+import csv
+import glob
+import json
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+
+def rows(pattern):
+    f = glob.glob(pattern, recursive=True)
+    if not f:
+        return []
+    return list(csv.DictReader(open(f[0])))
+
+
+def main(tag, cfg, out):
+    log = open(f"{out}/{tag}_{cfg}_run.log").read()
+    m = re.search(r"algo_bytes=(\d+)", log)
+    algo = int(m.group(1)) if m else None
+    trace = defaultdict(list)
+    for r in rows(f"{out}/{tag}_{cfg}_trace/**/trace_kernel_trace.csv"):
+        if "netcsum" in r["Kernel_Name"]:
+            trace[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    pmc = defaultdict(dict)
+    for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        vals = defaultdict(list)
+        for r in rows(f"{out}/{tag}_{cfg}_{kind}/**/{kind}_counter_collection.csv"):
+            if "netcsum" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        for k, v in vals.items():
+            pmc[k][ctr + "_KB"] = statistics.median(v)
+    res = {"tag": tag, "config": cfg, "launch": log.strip().splitlines()[-1] if log.strip() else None,
+           "algorithmic_bytes_per_launch": algo, "kernels": {}}
+    for k in sorted(set(trace) | set(pmc)):
+        d = {"launches": len(trace.get(k, [])),
+             "avg_us": round(statistics.mean(trace[k]), 2) if trace.get(k) else None,
+             "min_us": round(min(trace[k]), 2) if trace.get(k) else None, **pmc.get(k, {})}
+        if "FETCH_SIZE_KB" in d and "WRITE_SIZE_KB" in d:
+            d["hbm_read_bytes"] = d["FETCH_SIZE_KB"] * 1024 * 2
+            d["hbm_write_bytes"] = d["WRITE_SIZE_KB"] * 1024
+            if algo:
+                d["traffic_over_algorithmic"] = round((d["hbm_read_bytes"] + d["hbm_write_bytes"]) / algo, 4)
+        if algo and d["avg_us"]:
+            d["algorithmic_GBps_at_avg"] = round(algo / (d["avg_us"] * 1e3), 1)
+        res["kernels"][k] = d
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])

@@ -9,5 +9,7 @@ for v in ${VARIANTS:-default wb1 wb2 wb3 default}; do
   NETCSUM_LIB=$lib timeout -k 10 120 python bench.py $BENCH_ARGS --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/${T}_$v.json 2> gpurun_out/${T}_$v.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/${T}_$v.json'));r=d['roofline'];print('$v', r['kernel_ms'], r['kernel_ms_median'], d['ms_per_step'], d['parity_sample_ok'])"
 done
-[ -n "$NO_TX" ] || timeout -k 10 120 python tools/tx_sweep.py > gpurun_out/${T}_tx_sweep.jsonl 2> gpurun_out/${T}_tx_sweep.err || exit 1
-cat gpurun_out/${T}_tx_sweep.jsonl
+if [ -z "$NO_TX" ]; then
+  timeout -k 10 120 python tools/tx_sweep.py > gpurun_out/${T}_tx_sweep.jsonl 2> gpurun_out/${T}_tx_sweep.err || exit 1
+  cat gpurun_out/${T}_tx_sweep.jsonl
+fi

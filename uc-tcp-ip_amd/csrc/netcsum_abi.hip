@@ -31,6 +31,7 @@ std::atomic<int> g_tune_chunks{0};
 std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
 std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
+std::atomic<int> g_tune_tx_passes{0};             // run-stream Tx: 0 auto (1 pass), 1, 2
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -587,7 +588,36 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     c.nt = nt >= 0 ? (nt != 0) : !tx;
     c.grid = g_tune_grid.load();
     const int tile = g_tune_tile.load();
+    // Run-stream form (netcsum_pktstream.hip) for dense strided IPv4 batches unless the lane-group
+    // kernel is forced (TUNE_KERNEL 2); TILE > 0 sets its packets per wave run (default 16).
+    const int kern = g_tune_kernel.load();
+    if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
+        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : 16u;
+        const int d = g_tune_chunks.load() == 8 ? 8 : 4;
+        const bool snt = nt >= 0 ? (nt != 0) : true;
+        const bool two = tx && g_tune_tx_passes.load() == 2;
+        char desc[112];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
+                 tx ? "tx" : "rx", spw, two ? " +pkt_scatter_kernel" : "");
+        netcsum::set_last_launch(desc);
+        hipStream_t hs = static_cast<hipStream_t>(hip_stream);
+        if (two) {
+            // stream-ordered scratch for the records: allocated and freed on the caller's stream
+            netcsum::PktTxRecord* rec = nullptr;
+            NC_HIP(hipMallocAsync(reinterpret_cast<void**>(&rec), (size_t)n_pkt * sizeof(netcsum::PktTxRecord), hs));
+            const hipError_t e = netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs, rec);
+            NC_HIP(hipFreeAsync(rec, hs));
+            NC_HIP(e);
+            return NET_UTIL_ERR_NONE;
+        }
+        NC_HIP(netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs));
+        return NET_UTIL_ERR_NONE;
+    }
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
+    char desc[96];
+    snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u", c.group_lanes,
+             c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile);
+    netcsum::set_last_launch(desc);
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, static_cast<hipStream_t>(hip_stream)));
     return NET_UTIL_ERR_NONE;
 }
@@ -729,6 +759,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_PROBE:
         if (value != 0 && value != 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_probe.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_TX_PASSES:
+        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_tx_passes.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:
         if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)

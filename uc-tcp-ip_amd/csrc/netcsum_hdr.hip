@@ -181,9 +181,13 @@ hipError_t launch_hdr_t(const SegBatchArgs& a, int grid, hipStream_t s) {
 
 }  // namespace
 
-// Pieces per tile of 64*H headers: the image starts at the 16-B boundary below the tile (lead <= 12).
+// Pieces per tile of 64*H headers: the image starts at the 16-B boundary below the tile. Base and
+// stride are multiples of 4 (small_supported), so a tile spans 64*H*stride = a multiple of 256 bytes
+// and EVERY tile starts at the base's offset in its 16-B line (lead = base & 15, 0..12): the exact
+// piece count for that lead (C3's 256-header tiles of 20 B are 5 whole KiB at lead 0, not 6).
 uint32_t hdr_pieces(const SegBatchArgs& a, int h) {
-    return (uint32_t)((12u + (64u * (uint32_t)h - 1u) * a.seg_stride + a.seg_len + 1023u) / 1024u);
+    const uint64_t lead = (uintptr_t)a.base & 15u;
+    return (uint32_t)((lead + (64u * (uint64_t)h - 1u) * a.seg_stride + a.seg_len + 1023u) / 1024u);
 }
 
 bool hdr_supported(const SegBatchArgs& a) {

@@ -52,6 +52,14 @@ struct PktBatchArgs {
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
 };
 
+// Two-pass Tx (run-stream form): one record per packet between the checksum pass and the scatter pass.
+struct PktTxRecord {
+    uint32_t vals;         // IP checksum | transport checksum << 16 (host order)
+    uint16_t l4_off;       // packet offset of the transport checksum field
+    uint8_t  flags;        // NETCSUM_PKT_* verdict
+    uint8_t  store;        // bit 0: write the IP field, bit 1: write the transport field
+};
+
 struct ChainBatchArgs {
     const uint8_t*  base;          // piece j starts at base + off[j]
     const uint64_t* off;
@@ -80,6 +88,10 @@ bool hdr_supported(const SegBatchArgs& a);     // small_supported and stride <= 
 int hdr_lanes_h(const SegBatchArgs& a, int h);  // headers per lane kernel 7 uses for a request (auto: h <= 0)
 uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per tile of 64*h headers
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
+bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
+                             PktTxRecord* rec = nullptr);     // rec: two-pass Tx (records + scatter pass)
+void set_last_launch(const char* desc);
 hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256
 bool stream_dense(const SegBatchArgs& a);      // strided, stride == len >= 1024: the default for kernel 6

@@ -964,6 +964,10 @@ const char* last_launch() {
     return g_last_launch;
 }
 
+void set_last_launch(const char* desc) {
+    snprintf(g_last_launch, sizeof(g_last_launch), "%s", desc);
+}
+
 static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel",
                                   "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel"};

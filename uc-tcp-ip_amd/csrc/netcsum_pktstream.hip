@@ -1,0 +1,424 @@
+// netcsum_pktstream.hip — gfx950 "run stream" kernel for strided IPv4 packet batches (SURVEY §8(f)
+// rows 1 and 4): fused Rx validation and Tx finalize, the same per-packet semantics as
+// pkt_batch_kernel (netcsum_packets.hip, whose header lists the reference call sites), in the form
+// of seg_stream_kernel (netcsum_stream.hip): a WAVE owns a run of consecutive packets and reads
+// their bytes exactly once as 1-KiB pieces (every wave-instruction 8 whole aligned lines).
+//
+// Per run:
+//  1. prologue, lane k = packet k of the run: the 96 bytes from the 16-B boundary below the
+//     packet (6 x 16-B loads; the IPv4 header with options <= 60 B plus the transport fields at
+//     <= hlen + 17) are parsed IN THE LANE — version / IHL / total length / fragment / protocol,
+//     UDP length, the pseudo-header {src, dst, 0, proto, len} (net_tcp.c:7851-7857,
+//     net_udp.c:1918-1934) — and the IP header's exact half-word sum [0, hlen) is taken from the
+//     same registers. This overlaps the run's first D pieces in flight.
+//  2. stream: per packet ONE scalar event at its transport end (`end` = total length, or hlen
+//     when no transport verdict): the exact sum of [start, end) over the wave (prefix masks + DPP
+//     wave_total), parked in lane k of a VGPR. The transport sum is that total minus the IP header
+//     sum — exact integers, so zero iff all its bytes are zero (the reference's 0 / 0xFFFF rule).
+//  3. vector epilogue, lane k = packet k: Tx subtracts the checksum fields (treated as zero,
+//     net_ipv4.c:9573), folds, rotates odd packets, adds the pseudo-header, and derives the same
+//     verdict flags / checksum values as pkt_consume; results are stored once per run: Rx flags as
+//     one coalesced byte store, Tx checksum fields in place (host-order value memcpy'd,
+//     net_ipv4.c:9586, net_tcp.c:29862, net_udp.c:2937).
+//
+// Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64, gap <= 64 B), IPv4.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/netcsum_mi355x.h"
+#include "netcsum_device.h"
+#include "netcsum_kernels.h"
+#include "netcsum_stream.h"
+
+namespace netcsum {
+
+namespace {
+
+using namespace sv;
+
+constexpr uint32_t kMaxRunPkts = 64u;     // packets per wave run: lane k = packet k
+
+__device__ __forceinline__ uint32_t be16(uint32_t dw, int byte) {   // bytes byte, byte+1 of dw, BE
+    return (((dw >> (8 * byte)) & 0xFFu) << 8) | ((dw >> (8 * byte + 8)) & 0xFFu);
+}
+
+// A window element as an opaque register value. Every select below picks between such values:
+// a select between two LOADS of one array is folded by the optimiser into a load with a computed
+// index, which moves the whole window to scratch memory (112 B per lane, per packet run).
+__device__ __forceinline__ uint32_t ov(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// Dword t of the lane's 24-dword window (t wave-divergent): a select chain in registers.
+__device__ __forceinline__ uint32_t win_dword(const uint32_t (&wd)[24], uint32_t t) {
+    uint32_t r = 0u;
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+        r = (t == (uint32_t)i) ? ov(wd[i]) : r;
+    }
+    return r;
+}
+
+// Little-endian dword at packet offset x (lead + x + 3 < 96).
+__device__ __forceinline__ uint32_t pkt_dword_at(const uint32_t (&wd)[24], uint32_t lead, uint32_t x) {
+    const uint32_t r = lead + x;
+    const uint32_t lo = win_dword(wd, r >> 2), hi = win_dword(wd, (r >> 2) + 1u);
+    const uint32_t b = r & 3u;
+    return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+}
+
+// The same for a fixed offset X (a multiple of 4): only lead >> 2 varies, a 4-way select.
+template <int X>
+__device__ __forceinline__ uint32_t pkt_dword_fixed(const uint32_t (&wd)[24], uint32_t lead) {
+    constexpr int B = X / 4;
+    const uint32_t j = lead >> 2;
+    const uint32_t w0 = ov(wd[B]), w1 = ov(wd[B + 1]), w2 = ov(wd[B + 2]), w3 = ov(wd[B + 3]), w4 = ov(wd[B + 4]);
+    const uint32_t lo = j == 0u ? w0 : j == 1u ? w1 : j == 2u ? w2 : w3;
+    const uint32_t hi = j == 0u ? w1 : j == 1u ? w2 : j == 2u ? w3 : w4;
+    const uint32_t b = lead & 3u;
+    return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+}
+
+// What the 2 bytes of a checksum field (even packet offset; b0 first) add to an exact sum in the
+// absolute little-endian frame of a packet starting at an odd / even address.
+__device__ __forceinline__ uint32_t field_le(uint32_t b0, uint32_t b1, bool odd) {
+    return odd ? ((b0 << 8) + b1) : (b0 + (b1 << 8));
+}
+
+struct LanePkt {          // lane k's packet after the prologue
+    uint32_t flags;
+    uint32_t end;         // packet offset one past the bytes the stream sums (0: none)
+    uint32_t ip_sum;      // exact half-word sum of the IP header [0, hlen) (absolute LE frame)
+    uint32_t fields;      // Tx: exact contribution of the checksum fields to be zeroed (IP | L4 sum)
+    uint32_t l4_field;    // Tx: contribution of the transport field alone
+    uint32_t pseudo_le;
+    uint32_t l4_csum_off; // ~0u: none
+    uint32_t proto;
+    bool     check_l4;
+    bool     malformed;
+};
+
+// IPv4 parse of pkt_parse (netcsum_packets.hip) from the lane's own window; `avail` bytes present.
+template <bool TX>
+__device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
+                                              uint32_t avail, bool odd, bool udp_tx_csum) {
+    LanePkt p{};
+    p.l4_csum_off = ~0u;
+    const uint32_t d0 = pkt_dword_fixed<0>(wd, lead);
+    const uint32_t d1 = pkt_dword_fixed<4>(wd, lead);
+    const uint32_t d2 = pkt_dword_fixed<8>(wd, lead);
+    const uint32_t d3 = pkt_dword_fixed<12>(wd, lead);
+    const uint32_t d4 = pkt_dword_fixed<16>(wd, lead);
+    const uint32_t ver = (d0 >> 4) & 0xFu;
+    uint32_t hlen = (d0 & 0xFu) * 4u;
+    const uint32_t tot = be16(d0, 2);
+    const uint32_t frag = be16(d1, 2) & 0x3FFFu;                 // MF | fragment offset
+    p.proto = (d2 >> 8) & 0xFFu;
+    if (avail < 20u || ver != 4u || hlen < 20u || tot < hlen || tot > avail) {
+        p.flags = NETCSUM_PKT_MALFORMED;
+        p.malformed = true;
+        return p;                                                // end 0: nothing summed
+    }
+    // exact sum of the IP header [0, hlen) from the window (lead + hlen <= 75 < 96)
+    uint32_t s = 0u - low_bytes(h[0], (int)lead);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        s += low_bytes(h[c], min(max((int)(lead + hlen) - 16 * c, 0), 16));
+    }
+    p.ip_sum = s;
+    p.fields = TX ? field_le((d2 >> 16) & 0xFFu, d2 >> 24, odd) : 0u;   // IP checksum field, offset 10
+    p.end = hlen;
+    if (frag != 0u) {
+        p.flags = NETCSUM_PKT_FRAGMENT;
+        return p;
+    }
+    const uint32_t l4len = tot - hlen;
+    const uint32_t src_dst = __builtin_amdgcn_sad_u16(d3, 0u, __builtin_amdgcn_sad_u16(d4, 0u, 0u));
+    const uint32_t fo = p.proto == 17u ? hlen + 4u : (p.proto == 6u ? hlen + 16u : hlen + 2u);
+    const uint32_t fd = pkt_dword_at(wd, lead, fo);              // UDP: len | csum; TCP / ICMP / IGMP: csum
+    switch (p.proto) {
+    case 6u:
+        if (l4len < 20u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = hlen + 16u;
+        p.pseudo_le = src_dst + (6u << 8) + (((l4len & 0xFFu) << 8) | (l4len >> 8));
+        p.l4_field = TX ? field_le(fd & 0xFFu, (fd >> 8) & 0xFFu, odd) : 0u;
+        break;
+    case 17u: {
+        if (l4len < 8u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        const uint32_t udp_len = be16(fd, 0);
+        if (udp_len != l4len) {                                  // net_udp.c:1903-1907
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = hlen + 6u;
+        if (!TX && (fd >> 16) == 0u) {                           // no checksum transmitted
+            p.flags = NETCSUM_PKT_UDP_NO_CSUM | NETCSUM_PKT_L4_OK;
+            return p;
+        }
+        if (TX && !udp_tx_csum) {
+            p.flags = NETCSUM_PKT_UDP_NO_CSUM;                   // write 0 (NET_UDP_HDR_CHK_SUM_NONE)
+            return p;
+        }
+        p.check_l4 = true;
+        p.pseudo_le = src_dst + (17u << 8) + (((udp_len & 0xFFu) << 8) | (udp_len >> 8));
+        p.l4_field = TX ? field_le((fd >> 16) & 0xFFu, fd >> 24, odd) : 0u;
+        break;
+    }
+    case 1u:                                                     // ICMPv4 / IGMP: no pseudo-header
+    case 2u:
+        if (l4len < 4u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = hlen + 2u;
+        p.l4_field = TX ? field_le(fd & 0xFFu, (fd >> 8) & 0xFFu, odd) : 0u;
+        break;
+    default:
+        break;
+    }
+    if (p.check_l4) {
+        p.end = tot;
+    }
+    return p;
+}
+
+__device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memcpy of a host-order u16
+    __attribute__((address_space(1))) uint8_t* q = (__attribute__((address_space(1))) uint8_t*)p;
+    q[0] = (uint8_t)(v & 0xFFu);
+    q[1] = (uint8_t)(v >> 8);
+}
+
+// REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
+// coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
+template <int D, bool NT, bool TX, bool REC>
+__global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    if (sb64 >= A.n) {
+        return;
+    }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(A.n - s_begin, spw);
+    const uint32_t s_end = s_begin + nres;
+    const uint32_t L = A.len_u;
+    const uint32_t st = (uint32_t)A.stride;
+    const uintptr_t a_first = (uintptr_t)A.base + (uint64_t)s_begin * A.stride;
+    const uintptr_t O = a_first & ~(uintptr_t)127;
+    const uint32_t lead0 = (uint32_t)(a_first - O);
+    const uint32_t span = lead0 + (nres - 1u) * st + L;
+    const uint32_t npieces = (span + 1023u) >> 10;
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
+    const uint32_t lane16 = 16u * lane;
+
+    u32x4 dv[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {                              // first D pieces in flight ...
+        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+    }
+
+    // ... while lane k parses packet k from its own 96-B window.
+    const bool mine = lane < nres;
+    const uint32_t prel = lead0 + lane * st;                   // run-relative start of packet `lane`
+    const uint32_t plead = prel & 15u;
+    const uint32_t pq = prel - plead;
+    u32x4 h[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        h[c] = buf_load16<false>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
+    }
+    uint32_t wd[24];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        wd[4 * c] = h[c].x;
+        wd[4 * c + 1] = h[c].y;
+        wd[4 * c + 2] = h[c].z;
+        wd[4 * c + 3] = h[c].w;
+    }
+    const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
+    const LanePkt pk = lane_parse<TX>(wd, h, plead, L, odd, A.udp_tx_csum != 0u);
+    const uint32_t end_v = mine ? pk.end : 0u;
+
+    uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k
+    uint32_t cur = s_begin;                                    // next packet to finish
+    uint32_t cs = lead0;                                       // its start / end, run-relative
+    uint32_t ce = lead0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)end_v);
+    uint32_t acc = 0u;
+
+    // General walk of seg_stream_kernel with per-packet ends (state written back unconditionally).
+    auto consume = [&](uint32_t q, u32x4 v) {
+        const uint32_t qb = q << 10;
+        const uint32_t pend = qb + 1024u;
+        const uint32_t full = sum4(v, 0u);
+        uint32_t u = cur, c = cs, e = ce, a = acc, t = tot_v;
+        if (!(u < s_end && e <= pend)) {                       // no packet ends in this piece
+            if (u < s_end) {
+                a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+            }
+        } else {
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+#pragma clang loop vectorize(disable) unroll(disable)
+            do {
+                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                const uint32_t T = wave_total(a + (Pe - Ps));
+                t = (lane == u - s_begin) ? T : t;
+                a = 0u;
+                ++u;
+                c += st;
+                const bool adj = c == e;                       // dense: the next packet starts at this end
+                if (u < s_end) {
+                    e = c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin));
+                }
+                Ps = adj ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+            } while (u < s_end && e <= pend);
+            if (u < s_end) {
+                a = full - Ps;
+            }
+        }
+        cur = u;
+        cs = c;
+        ce = e;
+        acc = a;
+        tot_v = t;
+    };
+
+    const uint32_t rounds = (npieces + (uint32_t)D - 1u) / (uint32_t)D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const uint32_t q = r * (uint32_t)D + (uint32_t)j;
+            consume(q, opaque_tuple(dv[j]));
+            dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
+            asm volatile("" ::: "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (!mine) {
+        return;
+    }
+    // vector epilogue: lane k = packet s_begin + k (pkt_consume's verdicts / values)
+    uint32_t acc_ip = pk.ip_sum, acc_l4 = tot_v - pk.ip_sum;
+    if (TX && !pk.malformed) {
+        acc_ip -= pk.fields;
+        if (pk.check_l4) {
+            acc_l4 -= pk.l4_field;
+        }
+    }
+    uint32_t sip = fold16(acc_ip), sl4 = fold16(acc_l4);
+    if (odd) {
+        sip = rot8(sip);
+        sl4 = rot8(sl4);
+    }
+    sl4 = fold16(sl4 + pk.pseudo_le);
+    uint32_t f = pk.flags;
+    uint32_t cip = ~0u, cl4 = ~0u;
+    if (!pk.malformed) {
+        if constexpr (!TX) {
+            f |= (sip == 0xFFFFu) ? NETCSUM_PKT_IP_OK : 0u;
+            if (pk.check_l4) {
+                f |= NETCSUM_PKT_L4_CHECKED | ((sl4 == 0xFFFFu) ? NETCSUM_PKT_L4_OK : 0u);
+            }
+        } else {
+            cip = (~sip) & 0xFFFFu;                              // net_ipv4.c:9578-9586
+            f |= NETCSUM_PKT_IP_OK;
+            if (pk.check_l4) {
+                cl4 = (~sl4) & 0xFFFFu;
+                if (pk.proto == 17u && cl4 == 0u) {
+                    cl4 = 0xFFFFu;                               // RFC 768 (net_udp.c:2929-2931)
+                }
+                f |= NETCSUM_PKT_L4_CHECKED | NETCSUM_PKT_L4_OK;
+            } else if ((f & NETCSUM_PKT_UDP_NO_CSUM) && pk.l4_csum_off != ~0u) {
+                cl4 = 0u;                                        // no UDP checksum (net_udp.c:2935)
+            }
+        }
+    }
+    const uint32_t idx = s_begin + lane;
+    if constexpr (REC) {
+        PktTxRecord r;
+        r.vals = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
+        r.l4_off = (uint16_t)pk.l4_csum_off;
+        r.flags = (uint8_t)f;
+        r.store = (uint8_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u));
+        rec[idx] = r;
+        return;
+    }
+    if (A.flags_out) {
+        A.flags_out[idx] = (uint8_t)f;
+    }
+    if constexpr (TX) {
+        uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)idx * A.stride;
+        if (cip != ~0u) {
+            store_field(p + 10, cip);
+        }
+        if (cl4 != ~0u) {
+            store_field(p + pk.l4_csum_off, cl4);
+        }
+    }
+}
+
+// Second pass of the two-pass Tx: one thread per packet writes its fields (and flags) from its record.
+__global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const PktTxRecord* rec) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.n) {
+        return;
+    }
+    const PktTxRecord r = rec[i];
+    if (A.flags_out) {
+        A.flags_out[i] = r.flags;
+    }
+    uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
+    if (r.store & 1u) {
+        store_field(p + 10, r.vals & 0xFFFFu);
+    }
+    if (r.store & 2u) {
+        store_field(p + r.l4_off, r.vals >> 16);
+    }
+}
+
+template <int D, bool NT, bool TX>
+hipError_t launch_pkt_stream_t(const PktBatchArgs& a, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
+    const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
+    const int grid = (int)((waves + 3u) / 4u);
+    if (TX && rec != nullptr) {
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX>), dim3(grid), dim3(256), 0, s, a, spw, rec);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(pkt_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a, (const PktTxRecord*)rec);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false>), dim3(grid), dim3(256), 0, s, a, spw, rec);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Strided IPv4 batches of >= 64-B packets, dense (gap <= 64 B), whose runs span < 2^31 bytes.
+bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver) {
+    return ip_ver == 4 && a.off == nullptr && a.len_u >= 64u && a.stride >= a.len_u && a.stride <= a.len_u + 64u &&
+           (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
+}
+
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
+                             PktTxRecord* rec) {
+    if (spw == 0u || spw > kMaxRunPkts) return hipErrorInvalidValue;
+#define NETCSUM_P(D_, NT_, TX_) \
+    if (depth == D_ && nt == NT_ && tx == TX_) return launch_pkt_stream_t<D_, NT_, TX_>(a, spw, s, rec);
+    NETCSUM_P(4, true, false) NETCSUM_P(4, false, false) NETCSUM_P(4, true, true) NETCSUM_P(4, false, true)
+    NETCSUM_P(8, true, false) NETCSUM_P(8, false, false) NETCSUM_P(8, true, true) NETCSUM_P(8, false, true)
+#undef NETCSUM_P
+    return hipErrorInvalidValue;
+}
+
+}  // namespace netcsum

@@ -35,47 +35,13 @@
 
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
+#include "netcsum_stream.h"
 
 namespace netcsum {
 
 namespace {
 
-constexpr int kRsrcWord3 = 0x00020000;     // gfx9-family raw buffer V# word 3 (32-bit data format)
-constexpr uint32_t kOOB = 0x80000000u;     // voffset past every run's num_records: reads zeros
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t run_rsrc(uintptr_t base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
-}
-
-template <bool NT>
-__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, NT ? 2 : 0);
-}
-
-// `opaque` over the whole 128-bit register tuple (one "+v" operand): the value stays in the tuple the
-// load wrote, so the refill of the same ring slot needs no copy (a copy would force a vmcnt wait).
-__device__ __forceinline__ u32x4 opaque_tuple(u32x4 v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-
-// This lane's share of the bytes of a 1-KiB piece that lie below piece offset x (wave-uniform,
-// 0..1024): its whole chunk if the chunk ends at or below x, the low (x - 16*lane) bytes if x falls
-// inside it, nothing above. A span [xs, xe) of the piece is prefix(xe) - prefix(xs), exactly.
-__device__ __forceinline__ uint32_t piece_prefix(u32x4 v, uint32_t lane16, uint32_t x) {
-    return low_bytes(v, min(max((int)x - (int)lane16, 0), 16));
-}
-
-// Sum over the 64 lanes (every lane active): inclusive row scans by DPP row_shr 1/2/4/8 (lanes with
-// no source add the 0 `old` operand), then the four row totals from lanes 15/31/47/63 (scalar).
-__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) + (uint32_t)__builtin_amdgcn_readlane((int)v, 31) +
-           (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
+using namespace sv;
 
 constexpr uint32_t kMaxRun = 128u;     // segments per wave run: results live in two VGPRs (lane = k % 64)
 constexpr uint64_t kMaxGap = 64u;      // varlen runs stream across gaps of up to this many bytes
