@@ -370,7 +370,11 @@ typedef enum netcsum_tune_key {
                                          of segments, streamed when packed; else falls back to 2;
                                          CHUNKS = pieces in flight per wave: 4, 6 or 8), 7 header
                                          tiles through LDS (kernel 5's domain with stride <= 64 B;
-                                         CHUNKS = tiles in flight per wave: 2, 3 or 4)              */
+                                         CHUNKS = tiles in flight per wave: 2, 3 or 4), 8 packed
+                                         16 / 20-B headers streamed by one wave per run (stride ==
+                                         len, base a multiple of 4, no pseudo-header; else 7;
+                                         CHUNKS 4 / 8 = pieces in flight; TILE = headers per run,
+                                         auto 1024)                                                 */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
@@ -379,9 +383,9 @@ typedef enum netcsum_tune_key {
                                          Kernel 6: J > 0 = segments per wave run (<= 128; auto 16).
                                          Kernel 7: headers per lane, 1, 2 or 4 (auto 2).
                                          IPv4 packet batches: packets per wave run of the run-stream
-                                         form (<= 64; auto 16); TUNE_KERNEL 2 forces the lane-group
+                                         form (<= 64; auto 8); TUNE_KERNEL 2 forces the lane-group
                                          packet kernel                                              */
-    NETCSUM_TUNE_TX_PASSES     = 10   /* run-stream Tx finalize: 0 auto (1), 1 checksum fields written
+    NETCSUM_TUNE_TX_PASSES     = 10   /* run-stream Tx finalize: 0 auto (2), 1 checksum fields written
                                          by the checksum pass, 2 checksum pass writes 8-B records,
                                          a scatter pass writes the fields                            */
 } NETCSUM_TUNE_KEY;

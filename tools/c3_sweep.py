@@ -30,11 +30,26 @@ def main():
     print(json.dumps({"variant": "read_probe", "ms": round(ms, 4), "GBps": round(n * L / ms / 1e6, 1)}), flush=True)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
     ref = None
-    for h in (2, 4, 1):
+    for spw in (384, 512, 768, 1024):                      # kernel 8: headers per wave run
+        for d in (4, 8):
+            for nt in (1,):
+                netcsum.tune(netcsum.TUNE_KERNEL, 8)
+                netcsum.tune(netcsum.TUNE_TILE, spw)
+                netcsum.tune(netcsum.TUNE_CHUNKS, d)
+                netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
+                fn = lambda: netcsum.batch_strided(hdr, L, L, None, 0, 0, n, out, 2, stream=st)  # noqa: E731
+                ms = events_ms(fn, st, reps=40, warm_s=0.2)
+                r = out.clone()
+                same = True if ref is None else bool(torch.equal(r, ref))
+                ref = r if ref is None else ref
+                print(json.dumps({"variant": dict(kernel=8, spw=spw, d=d, nt=nt), "kernel": netcsum.last_launch(),
+                                  "ms": round(ms, 4), "GBps_algo": round(algo / ms / 1e6, 1), "same": same}), flush=True)
+    netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+    for h in (2, 4):
         for s in (2, 3, 4):
             if h == 4 and s == 4:
                 continue
-            for div in (0, 8, 32, 64):
+            for div in (0, 8):
                 tiles = n // (64 * h)
                 grid = 0 if div == 0 else tiles // div
                 netcsum.tune(netcsum.TUNE_KERNEL, 7)

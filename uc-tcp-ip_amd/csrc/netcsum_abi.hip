@@ -31,7 +31,7 @@ std::atomic<int> g_tune_chunks{0};
 std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
 std::atomic<int> g_tune_grid_mult{1};
 std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
-std::atomic<int> g_tune_tx_passes{0};             // run-stream Tx: 0 auto (1 pass), 1, 2
+std::atomic<int> g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -147,13 +147,29 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
                  : netcsum::small_supported(a) ? 5
                  : (netcsum::stream_dense(a) || (varlen && netcsum::stream_supported(a))) ? 6 : 2;
     }
+    if (c.kernel == 8) {
+        if (netcsum::hdrstream_supported(a)) {
+            // Run-stream header form: TILE > 0 = headers per wave run (auto 1024), CHUNKS 4 / 8 =
+            // pieces in flight (auto 4), non-temporal loads unless NT_LOADS 0.
+            int d = g_tune_chunks.load();
+            c.chunks_per_pass = (d == 8) ? 8 : 4;
+            c.stream_spw = tile > 0 ? (uint32_t)tile : 1024u;
+            c.nt = nt != 0;
+            c.group_lanes = 64;
+            c.blocks_needed = 0;
+            return c;
+        }
+        c.kernel = 7;                                  // outside its domain: the LDS-tile header form
+    }
     if (c.kernel == 7) {
         if (netcsum::hdr_supported(a)) {
-            // Defaults from the r1h2 sweep (C3, 16 M x 20 B): 2 headers per lane (128-header
-            // tiles), 3 tiles in flight per wave, 4 tiles per wave (grid = tiles / 16): 5.77 TB/s vs
-            // 5.55 for one header per lane and 5.44 for kernel 5; GRID_MULT > 1 instead sizes the
-            // grid as resident blocks x CUs x mult.
-            c.tile = netcsum::hdr_lanes_h(a, tile);           // TILE = headers per lane (1, 2, 4; auto 2)
+            // Defaults from the r2 sweeps (C3, 16 M x 20 B, tools/c3_sweep.py): 4 headers per lane
+            // (256-header tiles = 5 whole KiB now that the piece count is exact), 2 tiles in flight,
+            // 2 tiles per wave (grid = tiles / 8): 0.0615 ms = 6.0 TB/s vs 0.063 for round 1's 2
+            // headers x 3 tiles x 4 tiles per wave; GRID_MULT > 1 instead sizes the grid as resident
+            // blocks x CUs x mult.
+            const bool auto_h = !(tile == 1 || tile == 2 || tile == 4);
+            c.tile = netcsum::hdr_lanes_h(a, auto_h ? 4 : tile);   // TILE = headers per lane (1, 2, 4)
             int st = g_tune_chunks.load();
             if (!(st == 2 || st == 3 || st == 4)) st = (c.tile == 2) ? 3 : 2;
             c.chunks_per_pass = st;
@@ -162,8 +178,9 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
             c.blocks_needed = 0;
             if (c.grid <= 0) {
                 const uint64_t tiles = ((uint64_t)a.n_seg + 64u * c.tile - 1u) / (64u * c.tile);
+                const uint64_t per_wave = (auto_h && c.tile == 4) ? 2u : 4u;
                 c.grid = c.grid_mult > 1 ? netcsum::hdr_occupancy(a, st, c.tile) * c.cus * c.grid_mult
-                                         : (int)std::max<uint64_t>(1u, (tiles + 15u) / 16u);
+                                         : (int)std::max<uint64_t>(1u, (tiles + 4u * per_wave - 1u) / (4u * per_wave));
             }
             return c;
         }
@@ -254,6 +271,68 @@ NET_ERR check_op(NETCSUM_OP op, const void* d_pseudo, CPU_INT16U pseudo_len) {
         return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;     // header checksums take no pseudo-header
     }
     return NET_UTIL_ERR_NONE;
+}
+
+// Scratch of the two-pass Tx (8-B records between its two kernels): plain hipMalloc device memory,
+// one buffer per (device, stream) — launches on one stream are ordered, so a stream's buffer is never
+// in use by two launches at once. Memory from the stream-ordered allocator measured ~70 us slower
+// for the record stores on 1 M packets (profiles/r2tx_*), so it is not used. Up to kScratchSlots
+// buffers are kept; the least recently used is freed (after a device synchronisation) beyond that.
+constexpr int kScratchSlots = 16;
+struct ScratchSlot {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    void* p = nullptr;
+    size_t cap = 0;
+    uint64_t used = 0;
+};
+
+hipError_t stream_scratch(int dev, hipStream_t st, size_t bytes, void** out) {
+    static std::mutex mu;
+    static ScratchSlot slots[kScratchSlots];
+    static uint64_t tick = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    ScratchSlot* hit = nullptr;
+    ScratchSlot* lru = &slots[0];
+    for (ScratchSlot& sl : slots) {
+        if (sl.dev == dev && sl.stream == st && sl.p != nullptr) {
+            hit = &sl;
+            break;
+        }
+        if (sl.p == nullptr || sl.used < lru->used) lru = &sl;
+    }
+    if (hit == nullptr) {
+        hit = lru;
+        if (hit->p != nullptr) {                       // evict: nothing may still use it
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return e;
+            (void)hipSetDevice(hit->dev);
+            (void)hipFree(hit->p);
+            (void)hipSetDevice(dev);
+            *hit = ScratchSlot{};
+        }
+        hit->dev = dev;
+        hit->stream = st;
+    }
+    if (hit->cap < bytes) {                            // grow: the stream's earlier work may use it
+        if (hit->p != nullptr) {
+            hipError_t e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            (void)hipFree(hit->p);
+            hit->p = nullptr;
+            hit->cap = 0;
+        }
+        const size_t cap = std::max<size_t>(bytes, (size_t)1 << 20);
+        hipError_t e = hipMalloc(&hit->p, cap);
+        if (e != hipSuccess) {
+            hit->p = nullptr;
+            return e;
+        }
+        hit->cap = cap;
+    }
+    hit->used = ++tick;
+    *out = hit->p;
+    return hipSuccess;
 }
 
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a, uint32_t len_hint, hipStream_t s) {
@@ -591,23 +670,24 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // Run-stream form (netcsum_pktstream.hip) for dense strided IPv4 batches unless the lane-group
     // kernel is forced (TUNE_KERNEL 2); TILE > 0 sets its packets per wave run (default 16).
     const int kern = g_tune_kernel.load();
+    // Defaults from the r2tx sweep (tools/pkt_stream_probe.py, 1 M x 1500-B IPv4/TCP): runs of 8
+    // packets, 4 pieces in flight, nt loads (Rx 0.215 ms); Tx in two passes (checksum pass writing
+    // 8-B records + scatter pass: 0.288 ms against 0.296 for in-pass field writes).
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
-        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : 16u;
+        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : 8u;
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
-        const bool two = tx && g_tune_tx_passes.load() == 2;
+        const bool two = tx && g_tune_tx_passes.load() != 1;
         char desc[112];
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
                  tx ? "tx" : "rx", spw, two ? " +pkt_scatter_kernel" : "");
         netcsum::set_last_launch(desc);
         hipStream_t hs = static_cast<hipStream_t>(hip_stream);
         if (two) {
-            // stream-ordered scratch for the records: allocated and freed on the caller's stream
-            netcsum::PktTxRecord* rec = nullptr;
-            NC_HIP(hipMallocAsync(reinterpret_cast<void**>(&rec), (size_t)n_pkt * sizeof(netcsum::PktTxRecord), hs));
-            const hipError_t e = netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs, rec);
-            NC_HIP(hipFreeAsync(rec, hs));
-            NC_HIP(e);
+            // the records live in this stream's scratch buffer (stream_scratch)
+            void* rec = nullptr;
+            NC_HIP(stream_scratch(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord), &rec));
+            NC_HIP(netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs, static_cast<netcsum::PktTxRecord*>(rec)));
             return NET_UTIL_ERR_NONE;
         }
         NC_HIP(netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs));
@@ -739,7 +819,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_nt.store(value < 0 ? -1 : (value != 0));
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_KERNEL:
-        if (value < 0 || value > 7) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 8) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_kernel.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CHUNKS:
@@ -753,7 +833,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_grid_mult.store(value == 0 ? 1 : value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_TILE:
-        if (value < -1 || value > 1024) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > (1 << 20)) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tile.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:

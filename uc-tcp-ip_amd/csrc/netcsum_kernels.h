@@ -35,6 +35,7 @@ struct LaunchCfg {
                            // 5: seg_small_kernel (small 4-B-aligned strided segments, no pseudo),
                            // 6: seg_stream_kernel (dense strided runs, one wave per run),
                            // 7: seg_hdr_kernel (small headers through LDS-image tiles)
+                           // 8: seg_hdrstream_kernel (packed 16 / 20-B headers, one wave per run)
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
     uint32_t stream_spw;   // kernel 6: segments per wave (one contiguous run each)
@@ -52,7 +53,8 @@ struct PktBatchArgs {
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
 };
 
-// Two-pass Tx (run-stream form): one record per packet between the checksum pass and the scatter pass.
+// Two-pass Tx (run-stream form): one record per packet between the checksum pass and the scatter pass,
+// written and read as ONE little-endian uint64 (vals | l4_off << 32 | flags << 48 | store << 56).
 struct PktTxRecord {
     uint32_t vals;         // IP checksum | transport checksum << 16 (host order)
     uint16_t l4_off;       // packet offset of the transport checksum field
@@ -88,6 +90,8 @@ bool hdr_supported(const SegBatchArgs& a);     // small_supported and stride <= 
 int hdr_lanes_h(const SegBatchArgs& a, int h);  // headers per lane kernel 7 uses for a request (auto: h <= 0)
 uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per tile of 64*h headers
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
+bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
+hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
                              PktTxRecord* rec = nullptr);     // rec: two-pass Tx (records + scatter pass)

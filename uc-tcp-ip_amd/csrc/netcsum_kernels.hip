@@ -970,8 +970,13 @@ void set_last_launch(const char* desc) {
 
 static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
     static const char* names[] = {"?", "seg_batch_kernel", "seg_pipe_kernel", "seg_lds_kernel", "seg_tile_kernel",
-                                  "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel"};
-    const int kid = (c.kernel >= 1 && c.kernel <= 7) ? c.kernel : 0;
+                                  "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel", "seg_hdrstream_kernel"};
+    const int kid = (c.kernel >= 1 && c.kernel <= 8) ? c.kernel : 0;
+    if (kid == 8) {
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdrstream_kernel<M=%u,D=%d%s> block=256 hdrs_per_wave=%u",
+                 a.seg_len / 4u, c.chunks_per_pass, c.nt ? ",nt" : "", c.stream_spw);
+        return;
+    }
     if (kid == 7) {
         const int h = hdr_lanes_h(a, c.tile);
         const int st = c.chunks_per_pass;                         // as launch_hdr_batch resolves it
@@ -1005,6 +1010,9 @@ hipError_t launch_seg_batch(const SegBatchArgs& args, const LaunchCfg& c, hipStr
     }
     if (c.kernel == 7) {
         return launch_hdr_batch(a, c.chunks_per_pass, c.tile, c.grid, s);                 // K = tiles in flight
+    }
+    if (c.kernel == 8) {
+        return launch_hdrstream(a, c.chunks_per_pass, c.stream_spw, c.nt, s);            // K = pieces in flight
     }
     if (c.kernel == 4) {
         return launch_tile_dispatch(a, c, s);

@@ -345,13 +345,26 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         }
     }
     const uint32_t idx = s_begin + lane;
+#if defined(NETCSUM_PKTSTREAM_PROBE)
+    // EXPERIMENT builds (tools/pkt_write_probe.sh): 1 = Rx stores nothing, 2 = Rx stores 8 B per
+    // packet (flags_out must hold 8 B per packet), 4 = the Tx record pass stores nothing
+    if (!TX && NETCSUM_PKTSTREAM_PROBE == 1) return;
+    if (!TX && NETCSUM_PKTSTREAM_PROBE == 2) {
+        reinterpret_cast<uint64_t*>(A.flags_out)[idx] = ((uint64_t)tot_v << 32) | f;
+        return;
+    }
+    if (REC && NETCSUM_PKTSTREAM_PROBE == 4) {
+        if (tot_v == 0x12345678u) rec[0].vals = f;            // keeps the work live, never taken
+        return;
+    }
+#endif
     if constexpr (REC) {
-        PktTxRecord r;
-        r.vals = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
-        r.l4_off = (uint16_t)pk.l4_csum_off;
-        r.flags = (uint8_t)f;
-        r.store = (uint8_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u));
-        rec[idx] = r;
+        // one 8-B store per packet (a struct assignment compiles to four partial stores, which
+        // made this pass ~70 us slower on 1 M packets)
+        const uint64_t r = (uint64_t)((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16)) |
+                           ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) | ((uint64_t)(f & 0xFFu) << 48) |
+                           ((uint64_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u)) << 56);
+        reinterpret_cast<uint64_t*>(rec)[idx] = r;
         return;
     }
     if (A.flags_out) {
@@ -374,16 +387,18 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
     if (i >= A.n) {
         return;
     }
-    const PktTxRecord r = rec[i];
+    const uint64_t r = reinterpret_cast<const uint64_t*>(rec)[i];      // PktTxRecord, one 8-B load
+    const uint32_t vals = (uint32_t)r, l4_off = (uint32_t)(r >> 32) & 0xFFFFu;
+    const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
     if (A.flags_out) {
-        A.flags_out[i] = r.flags;
+        A.flags_out[i] = (uint8_t)flags;
     }
     uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
-    if (r.store & 1u) {
-        store_field(p + 10, r.vals & 0xFFFFu);
+    if (store & 1u) {
+        store_field(p + 10, vals & 0xFFFFu);
     }
-    if (r.store & 2u) {
-        store_field(p + r.l4_off, r.vals >> 16);
+    if (store & 2u) {
+        store_field(p + l4_off, vals >> 16);
     }
 }
 
