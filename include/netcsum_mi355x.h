@@ -385,9 +385,17 @@ typedef enum netcsum_tune_key {
                                          IPv4 packet batches: packets per wave run of the run-stream
                                          form (<= 64; auto 8); TUNE_KERNEL 2 forces the lane-group
                                          packet kernel                                              */
-    NETCSUM_TUNE_TX_PASSES     = 10   /* run-stream Tx finalize: 0 auto (2), 1 checksum fields written
+    NETCSUM_TUNE_TX_PASSES     = 10,  /* run-stream Tx finalize: 0 auto (2), 1 checksum fields written
                                          by the checksum pass, 2 checksum pass writes 8-B records,
                                          a scatter pass writes the fields                            */
+    NETCSUM_TUNE_STREAM_WAVES  = 11,  /* run-stream kernels (segments, packets): resident waves per
+                                         SIMD, 3..8, enforced by reserving LDS per workgroup; 0 = as
+                                         many as registers allow; -1 = each kernel's default (dense
+                                         segment batches 5, others 0)                               */
+    NETCSUM_TUNE_STREAM_TOUCH  = 12   /* run-stream kernels: row-touch prologue (the first dword of
+                                         every 1-KiB piece of a wave's run loaded up front): 1 on,
+                                         0 off, -1 each kernel's default (segment batches on, packet
+                                         batches off)                                               */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -27,6 +27,8 @@ def _reset_tuning():
         netcsum.tune(k, 0)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_TILE, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
 
 
 @pytest.fixture(autouse=True)
@@ -442,6 +444,46 @@ def test_stream_kernel_full_c2_equals_pipe_kernel():
     netcsum.batch_strided(seg, L, L, ph, 12, 12, n, ok, 1)
     torch.cuda.synchronize()
     assert bool(ok.all())
+
+
+@pytest.mark.parametrize("touch", [0, 1])
+@pytest.mark.parametrize("waves", [0, 3, 5, 8])
+def test_stream_touch_and_residency_do_not_change_results(touch, waves):
+    """The row-touch prologue and the residency cap (NETCSUM_TUNE_STREAM_TOUCH / _WAVES) are launch
+    options only: dense, gapped and varlen stream batches — runs short and long enough that the touch
+    covers only their first 128 pieces — give the oracle's results under every combination."""
+    rng = np.random.default_rng(100 * waves + touch)
+    netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
+    netcsum.tune(netcsum.TUNE_STREAM_WAVES, waves)
+    netcsum.tune(netcsum.TUNE_KERNEL, 6)
+    for L, stride, n, run in ((1500, 1500, 4099, -1), (1500, 1500, 700, 128), (9000, 9000, 300, 128),
+                              (1499, 1503, 1000, -1), (65535, 65535, 5, 4)):
+        data = _host_bytes(rng, n * stride + 64, "random")
+        data_d = torch.from_numpy(data).to(DEV)
+        ph = _host_bytes(rng, n * 12 + 64, "random")
+        ph_d = torch.from_numpy(ph).to(DEV)
+        netcsum.tune(netcsum.TUNE_TILE, run)
+        for base_off in (0, 1):
+            got = _gpu_strided(data_d, base_off, stride, L, ph_d, 12, 12, n, 0)
+            assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
+            want = oracle.batch_strided(data, stride, L, ph, 12, 12, n, 0, seg_offset=base_off)
+            assert np.array_equal(got, want), (L, stride, n, run, base_off)
+    lens, off, base = None, None, None
+    n = 2000
+    lens = rng.integers(40, 9001, size=n).astype(np.uint16)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    base = _host_bytes(rng, int(off[-1]) + int(lens[-1]) + 64, "random")
+    ph = _host_bytes(rng, n * 12 + 64, "random")
+    base_d, ph_d = torch.from_numpy(base).to(DEV), torch.from_numpy(ph).to(DEV)
+    off_d, len_d = torch.from_numpy(off.view(np.int64)).to(DEV), torch.from_numpy(lens.view(np.int16)).to(DEV)
+    for run in (-1, 128):
+        netcsum.tune(netcsum.TUNE_TILE, run)
+        out = _out(n, 1)
+        netcsum.batch_varlen(base_d, off_d, len_d, ph_d, 12, 12, n, out, 1)
+        torch.cuda.synchronize()
+        assert netcsum.last_launch().startswith("seg_stream_varlen_kernel"), netcsum.last_launch()
+        assert np.array_equal(_np_out(out), oracle.batch_varlen(base, off, lens, ph, 12, 12, 1)), run
 
 
 @pytest.mark.parametrize("layout", ["packed", "packed_zero_len", "gaps", "reversed", "overlap", "mixed", "nic_ring",

@@ -28,6 +28,8 @@ def _defaults():
         netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
         netcsum.tune(netcsum.TUNE_CHUNKS, 0)
         netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
+        netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
+        netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     reset()
     yield
     reset()
@@ -99,9 +101,9 @@ def test_pkt_stream_vs_oracle(stride, pkt_len, lead, passes):
 
 
 @pytest.mark.parametrize("spw", [1, 5, 16, 33, 64])
-@pytest.mark.parametrize("nt,depth", [(0, 4), (1, 8)])
-def test_pkt_stream_run_lengths_and_loads_equal_lane_group_kernel(spw, nt, depth):
-    rng = random.Random(spw * 3 + nt)
+@pytest.mark.parametrize("nt,depth,touch,waves", [(0, 4, -1, -1), (1, 8, -1, -1), (1, 4, 1, 3), (0, 8, 1, 8)])
+def test_pkt_stream_run_lengths_and_loads_equal_lane_group_kernel(spw, nt, depth, touch, waves):
+    rng = random.Random(spw * 3 + nt + 10 * touch)
     stride, pkt_len, lead, n = 1518, 1514, 3, 1000
     buf = _batch(rng, n, stride, pkt_len, lead)
     netcsum.tune(netcsum.TUNE_KERNEL, 2)                         # the lane-group kernel: reference run
@@ -111,6 +113,8 @@ def test_pkt_stream_run_lengths_and_loads_equal_lane_group_kernel(spw, nt, depth
     netcsum.tune(netcsum.TUNE_TILE, spw)
     netcsum.tune(netcsum.TUNE_NT_LOADS, nt)
     netcsum.tune(netcsum.TUNE_CHUNKS, depth)
+    netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)               # row touch / residency cap: launch options
+    netcsum.tune(netcsum.TUNE_STREAM_WAVES, waves)
     rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, lead, True)
     assert f"pkts_per_wave={spw}" in d_rx and f"D={depth}" in d_tx, (d_rx, d_tx)
     assert np.array_equal(rx, rx_ref)

@@ -27,6 +27,7 @@ def main():
     v[:, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8, device=dev)
     flags8 = torch.zeros(8 * n, dtype=torch.uint8, device=dev)     # 8 B per packet: write-probe builds
     flags = flags8[:n]
+    tx_flags = flags if os.environ.get("PS_TX_FLAGS") else None   # write-probe build 5 stores 8 B here
     netcsum.tx_finalize_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)
     torch.cuda.synchronize()
     variants = [dict(kernel=2, tile=2, nt=-1, chunks=0, passes=0)]
@@ -43,7 +44,7 @@ def main():
         netcsum.tune(netcsum.TUNE_CHUNKS, var["chunks"])
         res = {}
         for name, fn in (("rx", lambda: netcsum.rx_validate_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)),
-                         ("tx", lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st))):
+                         ("tx", lambda: netcsum.tx_finalize_ipv4(pk, n, tx_flags, stride=L, pkt_len=L, stream=st))):
             ms = events_ms(fn, st, reps=60, warm_s=0.3)
             res[name] = {"ms": round(ms, 4), "GBps": round(n * (L + 1) / ms / 1e6, 1), "kernel": netcsum.last_launch()}
         ok = bool(((flags & 0x07) == 0x07).all()) if not os.environ.get("NETCSUM_LIB") else None

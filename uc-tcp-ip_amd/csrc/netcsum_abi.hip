@@ -204,7 +204,9 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
             } else if (c.grid_mult > 1) {
                 waves = (uint64_t)netcsum::stream_occupancy(d, a, c.nt) * 4u * (uint64_t)c.cus * (uint64_t)c.grid_mult;
             } else {
-                waves = ((uint64_t)a.n_seg + 15u) / 16u;
+                // runs of 16 segments for dense batches (C2), 8 for varlen ones (C4, r2ct)
+                const uint64_t run = varlen ? 8u : 16u;
+                waves = ((uint64_t)a.n_seg + run - 1u) / run;
             }
             c.stream_spw = netcsum::stream_spw(a, waves);
             c.group_lanes = 64;
@@ -843,6 +845,14 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_TX_PASSES:
         if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tx_passes.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_STREAM_WAVES:
+        if (value != -1 && value != 0 && (value < 3 || value > 8)) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_stream_waves(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_STREAM_TOUCH:
+        if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_stream_touch(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:
         if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)

@@ -19,6 +19,7 @@ struct SegBatchArgs {
     uint32_t        verify;        // 0: u16 checksum out, 1: u8 DEF_OK/DEF_FAIL out
     uint32_t        tile;          // 0: grid-stride; J > 0: block b owns segments [b*gpb*J, (b+1)*gpb*J)
     void*           out;
+    uint32_t        touch;         // run-stream kernels: row-touch prologue (set by the launcher)
 };
 
 struct LaunchCfg {
@@ -51,6 +52,7 @@ struct PktBatchArgs {
     uint8_t*        flags_out;     // NETCSUM_PKT_* per packet (optional for Tx)
     uint32_t        tile;          // segments (packets) per group per block tile (0 = grid-stride)
     uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
+    uint32_t        touch;         // run-stream form: row-touch prologue (set by the launcher)
 };
 
 // Two-pass Tx (run-stream form): one record per packet between the checksum pass and the scatter pass,
@@ -102,6 +104,15 @@ bool stream_dense(const SegBatchArgs& a);      // strided, stride == len >= 1024
 uint32_t stream_spw(const SegBatchArgs& a, uint64_t waves);
 int stream_occupancy(int depth, const SegBatchArgs& a, bool nt);   // resident 256-thread blocks per CU
 hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
+// Residency cap of the run-stream kernels (NETCSUM_TUNE_STREAM_WAVES, -1 = each kernel's default):
+// LDS bytes each 256-thread workgroup reserves so that at most w of them (w waves per SIMD) fit a
+// CU's 160 KiB; 0 = no cap.
+void set_stream_waves(int w);
+uint32_t stream_lds_bytes(int auto_waves);
+// Row-touch prologue of the run-stream kernels (NETCSUM_TUNE_STREAM_TOUCH: -1 each kernel's
+// default `auto_on`, 0 off, 1 on).
+void set_stream_touch(int t);
+bool stream_touch(bool auto_on);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s, uint32_t tag = 0u);   // tag != 0 (grid 1): completion word
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,

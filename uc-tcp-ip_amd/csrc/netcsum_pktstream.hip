@@ -228,6 +228,8 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
 
+    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);    // row touch (netcsum_stream.h)
+
     // ... while lane k parses packet k from its own 96-B window.
     const bool mine = lane < nres;
     const uint32_t prel = lead0 + lane * st;                   // run-relative start of packet `lane`
@@ -304,6 +306,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    touch_retire(touch);
 
     if (!mine) {
         return;
@@ -357,6 +360,20 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         if (tot_v == 0x12345678u) rec[0].vals = f;            // keeps the work live, never taken
         return;
     }
+    // 5 = the Tx record pass stores its 8-B records into flags_out (the probe's 8-B-per-packet
+    // torch buffer) instead of the scratch buffer; 6 = 4-B records (values only) into the scratch
+    // (run with PS_TX_FLAGS=1 so that Tx gets the 8-B-per-packet flags buffer)
+    if (REC && NETCSUM_PKTSTREAM_PROBE == 5) {
+        if (A.flags_out == nullptr) return;
+        reinterpret_cast<uint64_t*>(A.flags_out)[idx] =
+            (uint64_t)((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16)) | ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) |
+            ((uint64_t)(f & 0xFFu) << 48);
+        return;
+    }
+    if (REC && NETCSUM_PKTSTREAM_PROBE == 6) {
+        reinterpret_cast<uint32_t*>(rec)[idx] = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
+        return;
+    }
 #endif
     if constexpr (REC) {
         // one 8-B store per packet (a struct assignment compiles to four partial stores, which
@@ -403,17 +420,21 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
 }
 
 template <int D, bool NT, bool TX>
-hipError_t launch_pkt_stream_t(const PktBatchArgs& a, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
+hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
+    PktBatchArgs a = a0;
+    // no piece touch by default: the header prologue already loads each packet's first bytes with
+    // the plain policy, and touching every piece on top is slower (r2ct: Rx 0.2174 -> 0.2315 ms)
+    a.touch = stream_touch(false) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     if (TX && rec != nullptr) {
-        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX>), dim3(grid), dim3(256), 0, s, a, spw, rec);
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(pkt_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a, (const PktTxRecord*)rec);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false>), dim3(grid), dim3(256), 0, s, a, spw, rec);
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
     return hipGetLastError();
 }
 

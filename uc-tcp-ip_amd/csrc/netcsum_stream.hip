@@ -32,6 +32,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
@@ -167,6 +168,7 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     for (int j = 0; j < D; ++j) {                              // first D pieces in flight ...
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
+    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);    // row touch (netcsum_stream.h)
 
     // ... while the run's pseudo-header sums are computed.
     uint32_t ps0 = 0u, ps1 = 0u;
@@ -290,6 +292,7 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     }
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
+    touch_retire(touch);
 
     store_run_results(A, s_begin, nres, lane, res0, res1);
 #if defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE == 1
@@ -403,6 +406,7 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
     for (int j = 0; j < D; ++j) {
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
+    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     // run-relative segment starts and ends (a packed run may have gaps of <= kMaxGap bytes)
     const uint32_t rs0 = lead + (uint32_t)(off0 - first), re0 = rs0 + len0;
     const uint32_t rs1 = lead + (uint32_t)(off1 - first), re1 = rs1 + len1;
@@ -462,22 +466,32 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    touch_retire(touch);
     store_run_results(A, s_begin, nres, lane, res0, res1);
 }
 
 template <int D, int PH, bool NT>
-hipError_t launch_stream_varlen_t(const SegBatchArgs& a, uint32_t spw, hipStream_t s) {
+hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
+    SegBatchArgs a = a0;
+    // defaults from r2ct (C4, 1 M packed 40-9000 B): runs of 8, touch, 5 waves per SIMD: 0.680 ms
+    // against 0.696 ms for runs of 16 at full residency without the touch
+    a.touch = stream_touch(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
-    hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256), 0, s, a, spw);
+    hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256), stream_lds_bytes(5), s, a, spw);
     return hipGetLastError();
 }
 
 template <int D, int PH, bool NT, bool ONE>
-hipError_t launch_stream_t(const SegBatchArgs& a, uint32_t spw, hipStream_t s) {
+hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
+    SegBatchArgs a = a0;
+    a.touch = stream_touch(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
-    hipLaunchKernelGGL((seg_stream_kernel<D, PH, NT, ONE>), dim3(grid), dim3(256), 0, s, a, spw);
+    // dense batches default to 5 waves per SIMD with the row touch: C2 0.2188 ms against 0.2346 ms
+    // without either (r2ct; 0.2268 touch only, 0.2300 cap only)
+    hipLaunchKernelGGL((seg_stream_kernel<D, PH, NT, ONE>), dim3(grid), dim3(256), stream_lds_bytes(ONE ? 5 : 0), s, a,
+                       spw);
     return hipGetLastError();
 }
 
@@ -491,6 +505,32 @@ bool stream_one(const SegBatchArgs& a) {
 }
 
 }  // namespace
+
+namespace {
+std::atomic<int> g_stream_waves{-1};
+std::atomic<int> g_stream_touch{-1};
+}
+
+void set_stream_waves(int w) {
+    g_stream_waves.store(w);
+}
+
+uint32_t stream_lds_bytes(int auto_waves) {
+    const int g = g_stream_waves.load(std::memory_order_relaxed);
+    const int w = g >= 0 ? g : auto_waves;
+    // w workgroups of 4 waves per CU = w waves per SIMD: the largest 512-B multiple of which w fit
+    // the 160 KiB of LDS and w + 1 do not
+    return (w >= 3 && w <= 8) ? ((163840u / (uint32_t)w) & ~511u) : 0u;
+}
+
+void set_stream_touch(int t) {
+    g_stream_touch.store(t);
+}
+
+bool stream_touch(bool auto_on) {
+    const int t = g_stream_touch.load(std::memory_order_relaxed);
+    return t < 0 ? auto_on : t != 0;
+}
 
 // Packed segments of >= 1 KiB (stride == len): the form the library picks by default (C2, C5).
 bool stream_dense(const SegBatchArgs& a) {

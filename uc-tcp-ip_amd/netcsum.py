@@ -52,6 +52,8 @@ PKT_MALFORMED, PKT_FRAGMENT, PKT_L4_MALFORMED = 0x10, 0x20, 0x40
 TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
 TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
 TUNE_TX_PASSES = 10
+TUNE_STREAM_WAVES = 11
+TUNE_STREAM_TOUCH = 12
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
