@@ -358,7 +358,7 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */
     NETCSUM_TUNE_NT_LOADS      = 3,   /* -1 auto (default), 0 plain, 1 non-temporal segment loads */
     NETCSUM_TUNE_BLOCK_THREADS = 4,   /* threads per workgroup: 64, 128 or 256 (0 = 256)         */
-    NETCSUM_TUNE_KERNEL        = 5,   /* 0 auto (default: 7 where it applies, else 5 where it
+    NETCSUM_TUNE_KERNEL        = 5,   /* 0 auto (default: 8 where it applies, else 7, else 5 where it
                                          applies, 6 for packed strided segments of >= 1 KiB and for
                                          offset/length batches, else 2), 1 simple,
                                          2 pipelined register loads, 3 pipelined LDS-DMA, 4 wave-tile
@@ -374,7 +374,8 @@ typedef enum netcsum_tune_key {
                                          16 / 20-B headers streamed by one wave per run (stride ==
                                          len, base a multiple of 4, no pseudo-header; else 7;
                                          CHUNKS 4 / 8 = pieces in flight; TILE = headers per run,
-                                         auto 1024)                                                 */
+                                         auto: the most that fit 4 KiB from any 128-B lead, 192 for
+                                         20-B headers)                                              */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """C3 (16 M x 20-B IPv4 headers, HdrCalc) sweep of seg_hdr_kernel<P,S,H>: headers per lane H (TILE),
-tiles in flight S (CHUNKS), grid (GRID_BLOCKS; 0 = tiles / 16 = 4 tiles per wave), against the
-LDS-DMA read probe over the same 335 MB. Results checked equal across variants. JSON lines."""
+tiles in flight S (CHUNKS), grid (GRID_BLOCKS; 0 = tiles / 16 = 4 tiles per wave), and of the
+run-stream header kernel 8 over headers per run (C3_SPW), residency cap (C3_WAVES) and row touch
+(C3_TOUCH), against the LDS-DMA read probe over the same 335 MB. Results checked equal across
+variants. JSON lines."""
 import json
 import os
 import sys
@@ -30,9 +32,13 @@ def main():
     print(json.dumps({"variant": "read_probe", "ms": round(ms, 4), "GBps": round(n * L / ms / 1e6, 1)}), flush=True)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
     ref = None
-    for spw in (384, 512, 768, 1024):                      # kernel 8: headers per wave run
-        for d in (4, 8):
-            for nt in (1,):
+    spws = [int(x) for x in os.environ.get("C3_SPW", "384,512,768,1024").split(",")]
+    waves_l = [int(x) for x in os.environ.get("C3_WAVES", "-1").split(",")]
+    touch_l = [int(x) for x in os.environ.get("C3_TOUCH", "-1").split(",")]
+    for spw, d, nt, w, tch in [(spw, d, nt, w, t) for spw in spws for d in (4, 8) for nt in (1,) for w in waves_l
+                               for t in touch_l]:
+                netcsum.tune(netcsum.TUNE_STREAM_WAVES, w)
+                netcsum.tune(netcsum.TUNE_STREAM_TOUCH, tch)
                 netcsum.tune(netcsum.TUNE_KERNEL, 8)
                 netcsum.tune(netcsum.TUNE_TILE, spw)
                 netcsum.tune(netcsum.TUNE_CHUNKS, d)
@@ -42,9 +48,14 @@ def main():
                 r = out.clone()
                 same = True if ref is None else bool(torch.equal(r, ref))
                 ref = r if ref is None else ref
-                print(json.dumps({"variant": dict(kernel=8, spw=spw, d=d, nt=nt), "kernel": netcsum.last_launch(),
+                print(json.dumps({"variant": dict(kernel=8, spw=spw, d=d, nt=nt, waves=w, touch=tch),
+                                  "kernel": netcsum.last_launch(),
                                   "ms": round(ms, 4), "GBps_algo": round(algo / ms / 1e6, 1), "same": same}), flush=True)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
+    if os.environ.get("C3_NO_K7"):
+        return
     for h in (2, 4):
         for s in (2, 3, 4):
             if h == 4 and s == 4:

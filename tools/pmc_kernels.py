@@ -35,7 +35,7 @@ def main(tag, cfg, out):
                 vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in vals.items():
             pmc[k][ctr + "_KB"] = statistics.median(v)
-    res = {"tag": tag, "config": cfg, "launch": log.strip().splitlines()[-1] if log.strip() else None,
+    res = {"tag": tag, "config": cfg, "launch": next((ln for ln in log.splitlines() if ln.startswith(cfg + " ")), None),
            "algorithmic_bytes_per_launch": algo, "kernels": {}}
     for k in sorted(set(trace) | set(pmc)):
         d = {"launches": len(trace.get(k, [])),

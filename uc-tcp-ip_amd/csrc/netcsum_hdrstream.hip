@@ -54,8 +54,14 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
     const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);   // whole 16-B loads; bytes past
                                                                            // rend are masked below
     const bool verify = A.verify != 0u;
-    const __amdgpu_buffer_rsrc_t ro = run_rsrc((uintptr_t)A.out + (uintptr_t)s_begin * (verify ? 1u : 2u),
-                                               nres * (verify ? 1u : 2u));
+    // The output V# must be provably wave-uniform: built from plain arithmetic the compiler kept it
+    // in VGPRs and wrapped every store in a readfirstlane "waterfall" loop; readfirstlane on its
+    // parts puts it in SGPRs (one store instruction per piece).
+    const uint64_t ob = (uint64_t)(uintptr_t)A.out + (uint64_t)s_begin * (verify ? 1u : 2u);
+    const uint32_t ob_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ob);
+    const uint32_t ob_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ob >> 32));
+    const __amdgpu_buffer_rsrc_t ro = run_rsrc((uintptr_t)(((uint64_t)ob_hi << 32) | ob_lo),
+                                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(nres * (verify ? 1u : 2u))));
     const uint32_t lane16 = 16u * lane;
 
     u32x4 dv[D];
@@ -63,6 +69,7 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
     for (int j = 0; j < D; ++j) {
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
+    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);    // row touch (netcsum_stream.h)
 
     // First header start at or after run-relative dword r (r may be below r0), as an offset from r.
     auto first_start = [&](int r) -> int {
@@ -112,17 +119,24 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
         for (int j = 0; j < D; ++j) {
             const uint32_t q = r * (uint32_t)D + (uint32_t)j;
             consume(q, opaque_tuple(dv[j]));                   // pieces past `total`: zeros, no stores
+            // Refills past the run read zeros without memory traffic. Branching around them (or peeling
+            // the last round) was measured: the uniform branch makes the compiler drain vmcnt(0) at
+            // every piece, the peeled round was 2-3 % slower (profiles/r2c3p_*).
             dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
             asm volatile("" ::: "memory");
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    touch_retire(touch);
 }
 
 template <int M, int D, bool NT>
-hipError_t launch_hs_t(const SegBatchArgs& a, uint32_t spw, hipStream_t s) {
+hipError_t launch_hs_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
+    SegBatchArgs a = a0;
+    a.touch = stream_touch(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
-    hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT>), dim3((unsigned)((waves + 3u) / 4u)), dim3(256), 0, s, a, spw);
+    hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT>), dim3((unsigned)((waves + 3u) / 4u)), dim3(256),
+                       stream_lds_bytes(0), s, a, spw);
     return hipGetLastError();
 }
 
