@@ -102,7 +102,7 @@ def main():
     netcsum.tx_finalize_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)      # valid checksums
     torch.cuda.synchronize()
     ms_fused = events_ms(lambda: netcsum.rx_validate_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st), st)
-    fused_kernel = "netcsum::pkt_batch_kernel<G=16,K=6,strided,nt,rx>"
+    fused_kernel = netcsum.last_launch()
     ok_all = bool(((flags & 0x07) == 0x07).all().item())
     o_ip = torch.zeros(n, dtype=torch.uint8, device=dev)
     o_l4 = torch.zeros(n, dtype=torch.uint8, device=dev)
@@ -118,13 +118,15 @@ def main():
                                  "GiB_per_s_two_pass": round(n * L / ms_two / 1e6 / 1.073741824, 1),
                                  "all_valid_fused": ok_all, "all_valid_two_pass": two_ok, "kernel": fused_kernel}
     ms_tx = events_ms(lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st), st)
-    out["tx_finalize_1500B_tcp"] = {"ms": round(ms_tx, 4), "GiB_per_s": round(n * L / ms_tx / 1e6 / 1.073741824, 1)}
+    out["tx_finalize_1500B_tcp"] = {"ms": round(ms_tx, 4), "GiB_per_s": round(n * L / ms_tx / 1e6 / 1.073741824, 1),
+                                    "kernel": netcsum.last_launch()}
     # ---- the same 1 M x 1500-B datagrams as IPv6/TCP (40-B header, 40-B pseudo-header)
     hdr6 = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8, device=dev)
     v[:, 0:8] = hdr6
     netcsum.tx_finalize_ipv6(pk, n, flags, stride=L, pkt_len=L, stream=st)
     torch.cuda.synchronize()
     ms6 = events_ms(lambda: netcsum.rx_validate_ipv6(pk, n, flags, stride=L, pkt_len=L, stream=st), st)
+    k6 = netcsum.last_launch()
     ok6 = bool(((flags & 0x07) == 0x07).all().item())
     ms6_tx = events_ms(lambda: netcsum.tx_finalize_ipv6(pk, n, None, stride=L, pkt_len=L, stream=st), st)
     # every other datagram back to IPv4 (its header restored, checksums rewritten): a mixed ring
@@ -138,7 +140,8 @@ def main():
                                     "GiB_per_s_rx": round(n * L / msmx / 1e6 / 1.073741824, 1)}
     out["ipv6_1500B_tcp"] = {"packets": n, "ms_rx": round(ms6, 4), "ms_tx": round(ms6_tx, 4),
                              "GiB_per_s_rx": round(n * L / ms6 / 1e6 / 1.073741824, 1),
-                             "GiB_per_s_tx": round(n * L / ms6_tx / 1e6 / 1.073741824, 1), "all_valid_rx": ok6}
+                             "GiB_per_s_tx": round(n * L / ms6_tx / 1e6 / 1.073741824, 1), "all_valid_rx": ok6,
+                             "kernel_rx": k6}
     del pk, v, tcp_ph, flags, o_ip, o_l4
     torch.cuda.empty_cache()
     # ---- batched NET_BUF chains: 16 Ki reassembled 64 KiB UDP datagrams, 45 fragments each, every
