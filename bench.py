@@ -15,8 +15,10 @@ the W counted warm-up steps the step is repeated untimed for --ramp-seconds (def
 value     = Σ_ranks n_seg*(1500+12) bytes * steps / max_rank(wall time of the K timed steps) / 2^30
 roofline  = dominant kernel (the form the library picks for C2: seg_stream_kernel) algorithmic bytes
             per launch n_seg*(1500+12+2) / mean HIP-event duration of that launch on its stream, vs the
-            8.0 TB/s HBM3E spec peak; `traffic` = HBM bytes per launch from rocprofv3 PMC
-            (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) or null.
+            8.0 TB/s HBM3E spec peak; `traffic` = HBM bytes per launch from rocprofv3 PMC,
+            FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE: measured live at N=1 (--pmc live: two
+            rocprofv3 --pmc passes over a short child run of this bench at the same size), else
+            from the committed profiles/*pmc*.json whose kernel form and source hash match, or null.
 cpu_baseline = the oracle's restatement of the reference C path (gcc -O2, same per-segment
             NetUtil_16BitOnesCplChkSumDataCalc call on a one-buffer NET_BUF) timed on this host's
             cores on a bounded sample of the same workload (rank 0, N=1 only).
@@ -55,6 +57,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of the CPU sample")
     ap.add_argument("--traffic-json", default=None, help="PMC summary (default: newest profiles/*pmc*.json)")
+    ap.add_argument("--pmc", choices=["live", "file", "off"], default="live",
+                    help="roofline.traffic source: live rocprofv3 --pmc passes over a child run (rank 0, N=1; "
+                         "falls back to the committed summaries), committed file only, or none")
     ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block)")
     return ap.parse_args()
 
@@ -231,6 +236,44 @@ def kernel_src_sha(kernel_fn):
     return h.hexdigest()[:16]
 
 
+def live_traffic(args, n, kernel_desc):
+    """HBM bytes per launch of the dominant kernel measured NOW: two rocprofv3 passes (--pmc FETCH_SIZE,
+    --pmc WRITE_SIZE; one counter group per pass, MI355X_MICROARCH.md §HBM) over a child run of this
+    bench (3 launches, same size and tuning). The child is a separate process started after this one's
+    timing; rocprofv3 runs the Python interpreter directly after `--`. Returns (bytes, source, problem)."""
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, None, "rocprofv3 not on PATH"
+    kfn = kernel_desc.split("::")[-1].split("<")[0] + "<"
+    tmp = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1", "--ramp-seconds", "0",
+             "--no-cpu-baseline", "--pmc", "off", "--segments", str(n), "--seg-len", str(args.seg_len),
+             "--pseudo-len", str(args.pseudo_len)] + [x for kv in args.tune for x in ("--tune", kv)]
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", counter, "-d", os.path.join(tmp, counter), "-o", counter,
+               "--output-format", "csv", "--"] + child
+        r = subprocess.run(cmd, cwd="/tmp", env={**os.environ, "TMPDIR": "/tmp"}, capture_output=True, text=True)
+        if r.returncode != 0:
+            return None, None, f"rocprofv3 --pmc {counter} exited {r.returncode}: {r.stderr.strip()[-300:]}"
+        rows = []
+        for f in glob.glob(os.path.join(tmp, counter, "**", f"{counter}_counter_collection.csv"), recursive=True):
+            import csv
+            rows += [float(x["Counter_Value"]) for x in csv.DictReader(open(f))
+                     if kfn in x["Kernel_Name"] and x["Counter_Name"] == counter]
+        if not rows:
+            return None, None, f"no {counter} rows for {kfn} in the rocprofv3 output"
+        vals[counter] = statistics.median(rows)
+    shutil.rmtree(tmp, ignore_errors=True)
+    b = vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024
+    return b, (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 3-launch child run "
+               f"(median per launch: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KB x2, WRITE_SIZE {vals['WRITE_SIZE']:.0f} KB)"), None
+
+
 def load_traffic(path, n_seg, kernel_desc):
     """HBM bytes per launch of THIS kernel (name, template form, launch geometry and source hash)
     at this size, from a rocprofv3 PMC summary under profiles/. Returns (bytes, source, problem):
@@ -372,7 +415,15 @@ def main():
         value = total_bytes / wall / 2 ** 30
         algo_bytes = n * (L + plen + 2)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src, traffic_err = load_traffic(args.traffic_json, n, kernel_desc)
+        traffic, traffic_src = None, None
+        traffic_err = "--pmc off" if args.pmc == "off" else None
+        live_err = None
+        if args.pmc == "live" and world == 1:
+            traffic, traffic_src, live_err = live_traffic(args, n, kernel_desc)
+        if traffic is None and args.pmc != "off":
+            traffic, traffic_src, traffic_err = load_traffic(args.traffic_json, n, kernel_desc)
+            if live_err:
+                traffic_err = f"live PMC failed ({live_err}); " + (traffic_err or "committed summary used")
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -396,7 +447,8 @@ def main():
                        "global_batch": n * world, "parallelism": f"shard{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         "traffic": round(traffic) if traffic is not None else None,
+                         "traffic_over_algorithmic": round(traffic / algo_bytes, 4) if traffic else None,
                          "kernel": kernel_desc,
                          "kernel_ms": round(kern_ms, 5), "kernel_ms_median": round(kern_med_ms, 5),
                          "algorithmic_bytes_per_launch": algo_bytes,

@@ -24,6 +24,7 @@ def _defaults():
             netcsum.tune(k, 0)
         netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
         netcsum.tune(netcsum.TUNE_TILE, -1)
+        netcsum.tune(netcsum.TUNE_KERNEL, 0)
     reset()
     yield
     reset()
@@ -126,7 +127,10 @@ def test_tx_finalize_v6_varlen_then_rx_accepts(udp_tx_csum, group):
 @pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (200, 184), (96, 72)])
 @pytest.mark.parametrize("group", [0, 16, 32])
 def test_tx_finalize_v6_strided_vs_oracle(stride, pkt_len, group):
-    """Strided IPv6 Tx: packets finalized exactly as the oracle does, bytes between packets untouched."""
+    """Strided IPv6 Tx through the lane-group kernel (TUNE_KERNEL 2; the run-stream form has its own
+    tests in test_gpu_pktstream.py): packets finalized exactly as the oracle does with the group's
+    window, bytes between packets untouched."""
+    netcsum.tune(netcsum.TUNE_KERNEL, 2)
     rng = random.Random(stride * 5 + pkt_len + group)
     n = 600
     kinds = ["tcp", "tcp", "udp", "udp0", "icmp_echo", "icmp_err", "ext", "other", "tcp_short", "bad_ver",

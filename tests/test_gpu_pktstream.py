@@ -1,4 +1,4 @@
-"""GPU parity of the run-stream packet kernel (netcsum_pktstream.hip: strided IPv4 batches, fused Rx
+"""GPU parity of the run-stream packet kernel (netcsum_pktstream.hip: strided IPv4, IPv6 and mixed batches, fused Rx
 validation and Tx finalize) against the packet oracle (oracle/oracle_packets.py, which composes the
 C restatement's HdrVerify / DataVerify / HdrCalc / DataCalc the way net_ipv4.c, net_tcp.c,
 net_udp.c, net_icmpv4.c and net_igmp.c call them), and against the lane-group kernel it replaces
@@ -7,6 +7,7 @@ checksum fields, odd and even base addresses, dense and gapped strides, run leng
 and non-temporal loads, UDP Tx checksums on and off. Every byte outside the written fields must be
 left as it was (gaps between packets, the bytes past the last one)."""
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -151,6 +152,152 @@ def test_pkt_stream_c2_shape_round_trip_1M():
     bad = torch.arange(0, n, 1000, device=DEV)
     v[bad, 777] ^= 0x04
     netcsum.rx_validate_ipv4(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    failed = torch.nonzero((f & op.L4_OK) == 0).flatten()
+    assert torch.equal(failed, bad)
+
+
+# ---- IPv6 and mixed IPv4 / IPv6 batches in the run-stream form (VER 6 / VER 0) -----------------
+
+def _stream_window(lead, i, stride):
+    """Bytes of datagram i the lane's 96-B window holds: 96 - (its address mod 16); the batch buffer
+    is 256-B aligned (torch), the datagrams start at lead + i * stride."""
+    return 96 - ((lead + i * stride) & 15)
+
+
+def _batch_ip(rng, n, stride, pkt_len, lead, v6_share):
+    from packets import KINDS6, make_packet_v6
+    buf = np.frombuffer(rng.randbytes(lead + n * stride + 96), np.uint8).copy()
+    for i in range(n):
+        if rng.random() < v6_share:
+            p = bytearray(make_packet_v6(rng, rng.choice(KINDS6), payload=rng.randint(0, max(0, pkt_len - 100))))
+        else:
+            p = bytearray(make_packet(rng, rng.choice(KINDS + ["udp", "tcp"]), payload=rng.randint(0, max(0, pkt_len - 80))))
+        if rng.random() < 0.1:                                    # longer than the slot: truncated
+            p = bytearray(make_packet_v6(rng, "tcp", payload=pkt_len))
+        p = p[:pkt_len]
+        o = lead + i * stride
+        buf[o:o + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    return buf
+
+
+def _want_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver):
+    rx = np.zeros(n, np.uint8)
+    tx_buf = buf.copy()
+    tx_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        o = lead + i * stride
+        pkt = bytes(buf[o:o + pkt_len])
+        w = _stream_window(lead, i, stride)
+        if ver == 6:
+            rx[i] = op.rx_validate_v6(pkt, w)
+            q, tx_f[i] = op.tx_finalize_v6(pkt, udp_tx_csum, w)
+        else:
+            rx[i] = op.rx_validate_ip(pkt, w)
+            q, tx_f[i] = op.tx_finalize_ip(pkt, udp_tx_csum, w)
+        tx_buf[o:o + pkt_len] = np.frombuffer(q, np.uint8)
+    return rx, tx_buf, tx_f
+
+
+def _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver):
+    rxf, txf = ((netcsum.rx_validate_ipv6, netcsum.tx_finalize_ipv6) if ver == 6
+                else (netcsum.rx_validate_ip, netcsum.tx_finalize_ip))
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    rxf(b[lead:], n, f, stride=stride, pkt_len=pkt_len)
+    torch.cuda.synchronize()
+    rx_desc = netcsum.last_launch()
+    rx = f.cpu().numpy()
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    txf(b[lead:], n, ft, stride=stride, pkt_len=pkt_len, udp_tx_csum=udp_tx_csum)
+    torch.cuda.synchronize()
+    return rx, b.cpu().numpy(), ft.cpu().numpy(), rx_desc, netcsum.last_launch()
+
+
+@pytest.mark.parametrize("ver", [6, 0])
+@pytest.mark.parametrize("stride,pkt_len", [(1500, 1500), (1540, 1514), (1501, 1500), (64, 64), (100, 64),
+                                            (577, 577), (9000, 9000)])
+@pytest.mark.parametrize("lead", [0, 1, 6, 13])
+@pytest.mark.parametrize("passes", [1, 2])
+def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
+    """Every IPv6 kind (TCP / UDP / UDP without checksum, ICMPv6 echo / error / NDP / other types,
+    extension-header chains inside and beyond the lane's window, Hop-by-Hop after the first, Fragment,
+    opaque extension headers, malformed versions / lengths, corrupted bytes), alone (VER 6) or mixed
+    with every IPv4 kind (VER 0), Rx verdicts and Tx bytes + verdicts against the oracle with the
+    window of the lane's 96-B prologue (96 - address mod 16)."""
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    rng = random.Random(ver * 1000 + stride * 7 + pkt_len + lead * 131 + passes)
+    n = 600 if stride < 5000 else 150
+    udp_tx_csum = lead != 6
+    buf = _batch_ip(rng, n, stride, pkt_len, lead, 1.0 if ver == 6 else 0.5)
+    rx_w, tx_w, txf_w = _want_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
+    rx, tx, txf, d_rx, d_tx = _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
+    tag = "v6" if ver == 6 else "mixed"
+    assert d_rx.startswith("pkt_stream_kernel") and f",rx,{tag}>" in d_rx and f",tx,{tag}>" in d_tx, (d_rx, d_tx)
+    bad = np.nonzero(rx != rx_w)[0]
+    assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
+    bad = np.nonzero(tx != tx_w)[0]
+    assert bad.size == 0, [(int(j), (int(j) - lead) // stride, (int(j) - lead) % stride, int(tx[j]), int(tx_w[j]))
+                           for j in bad[:8]]
+    assert np.array_equal(txf, txf_w)
+    if pkt_len >= 577:
+        assert (rx_w & op.EXT_HDR).any() and ((rx_w & op.L4_OK) != 0).any()
+
+
+@pytest.mark.parametrize("lead", list(range(16)))
+def test_pkt_stream_v6_extension_chains_at_the_window_edge(lead):
+    """Destination Options headers of 1..10 units (8..80 B) before TCP / UDP / ICMPv6 at every lead:
+    walked while the chain and the transport fields fit the lane's 96 - lead bytes, EXT_HDR beyond —
+    the oracle's window rule — and Tx finalizes exactly the walked ones."""
+    from packets import make_packet_v6
+    rng = random.Random(900 + lead)
+    stride = pkt_len = 512
+    pkts = []
+    for units in range(1, 11):
+        for _ in range(6):
+            inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 300))
+            ext = struct.pack("!BB", inner[6], units - 1) + rng.randbytes(units * 8 - 2)
+            body = ext + inner[40:]
+            hdr = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40]
+            pkts.append(op.tx_finalize_v6(hdr + body)[0][:pkt_len])
+    rng.shuffle(pkts)
+    n = len(pkts)
+    buf = np.frombuffer(rng.randbytes(lead + n * stride + 96), np.uint8).copy()
+    for i, p in enumerate(pkts):
+        buf[lead + i * stride:lead + i * stride + len(p)] = np.frombuffer(p, np.uint8)
+    rx_w, tx_w, txf_w = _want_ip(buf, n, stride, pkt_len, lead, True, 6)
+    rx, tx, txf, d_rx, _ = _run_ip(buf, n, stride, pkt_len, lead, True, 6)
+    assert d_rx.startswith("pkt_stream_kernel"), d_rx
+    assert np.array_equal(rx, rx_w) and np.array_equal(tx, tx_w) and np.array_equal(txf, txf_w)
+    assert (rx_w & op.EXT_HDR).any() and ((rx_w & op.L4_OK) != 0).any()
+
+
+def test_pkt_stream_v6_c2_shape_round_trip_1M():
+    """1 M x 1500-B TCP/IPv6 datagrams: Tx finalize, Rx accepts every one, one flipped byte per 1000
+    (addresses included) is caught exactly, 4096 sampled datagrams equal the oracle's Tx bytes."""
+    n, L = 1 << 20, 1500
+    pk = torch.empty(n * L + 256, dtype=torch.uint8, device=DEV)
+    netcsum.fill(pk, n * L, 0x5EED0006, 0)
+    v = pk[: n * L].view(n, L)
+    v[:, 0:8] = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8, device=DEV)
+    v[:, 52] = 0x50                                                 # TCP data offset 5
+    smp = np.sort(np.random.default_rng(6).choice(n, size=4096, replace=False))
+    sidx = torch.from_numpy(smp).to(DEV)
+    before = v[sidx].cpu().numpy()
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv6(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith("pkt_stream_kernel"), netcsum.last_launch()
+    after = v[sidx].cpu().numpy()
+    for j in range(len(smp)):
+        assert bytes(after[j]) == op.tx_finalize_v6(bytes(before[j]), True)[0], int(smp[j])
+    netcsum.rx_validate_ipv6(pk, n, f, stride=L, pkt_len=L)
+    torch.cuda.synchronize()
+    ok = op.IP_OK | op.L4_OK | op.L4_CHECKED
+    assert bool(((f & ok) == ok).all())
+    bad = torch.arange(0, n, 1000, device=DEV)
+    v[bad, 21] ^= 0x10                                              # a source-address byte
+    netcsum.rx_validate_ipv6(pk, n, f, stride=L, pkt_len=L)
     torch.cuda.synchronize()
     failed = torch.nonzero((f & op.L4_OK) == 0).flatten()
     assert torch.equal(failed, bad)

@@ -4,6 +4,7 @@
 # bench   driver-shaped bench (--gpus 1 --steps 20 --warmup 5) -> gpurun_out/TAG_bench.json
 # prof    rocprofv3 --kernel-trace --stats of bench.py, then separate FETCH_SIZE / WRITE_SIZE PMC
 #         passes (MI355X_MICROARCH.md §HBM), summarised   -> gpurun_out/TAG_pmc.json + TAG_trace/
+# profc5  the same for the C5 shard (16 M segments)          -> gpurun_out/TAGc5_pmc.json
 # configs tools/bench_configs.py (C1/C3/C4/packets/chains)  -> gpurun_out/TAG_configs.json
 # Every GPU step has its own time limit; the first failure ends the session.
 set -o pipefail
@@ -30,11 +31,11 @@ for s in $STEPS; do
   prof)
     ( cd /tmp && export TMPDIR=/tmp &&
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${T}_trace -o trace --output-format csv \
-        -- python3 $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline > $O/${T}_prof_bench.json 2> $O/${T}_prof_trace.err &&
+        -- python3 $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline --pmc off > $O/${T}_prof_bench.json 2> $O/${T}_prof_trace.err &&
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/${T}_fetch -o fetch --output-format csv \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline > /dev/null 2> $O/${T}_pmc_fetch.err &&
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --pmc off > /dev/null 2> $O/${T}_pmc_fetch.err &&
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/${T}_write -o write --output-format csv \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline > /dev/null 2> $O/${T}_pmc_write.err
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --pmc off > /dev/null 2> $O/${T}_pmc_write.err
     ) || { tail -20 $O/${T}_prof_trace.err $O/${T}_pmc_*.err; exit 1; }
     cat $O/${T}_prof_bench.json
     d() { dirname "$(find $O/${T}_$1 -name "$1_$2" -print -quit)"; }
@@ -42,6 +43,21 @@ for s in $STEPS; do
       "$(d write counter_collection.csv)" 1048576 $O/${T}_prof_bench.json $O > /dev/null || exit 1
     cp "$(d trace kernel_stats.csv)/trace_kernel_stats.csv" $O/${T}_rocprof_kernel_stats.csv
     python -c "import json;d=json.load(open('$O/${T}_pmc.json'));print({k:d.get(k) for k in ('dominant_kernel','rocprof_avg_us','traffic_over_algorithmic','kernel_src_sha')})" ;;
+  profc5)   # the same evidence for the C5 shard (16 M segments per GPU): the summary bench.py --pmc file
+            # uses for roofline.traffic at N > 1
+    ( cd /tmp && export TMPDIR=/tmp && A="--segments 16777216 --no-cpu-baseline --pmc off" &&
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${T}c5_trace -o trace --output-format csv \
+        -- python3 $R/bench.py --steps 30 --warmup 5 $A > $O/${T}c5_prof_bench.json 2> $O/${T}c5_prof_trace.err &&
+      timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/${T}c5_fetch -o fetch --output-format csv \
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 $A > /dev/null 2> $O/${T}c5_pmc_fetch.err &&
+      timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/${T}c5_write -o write --output-format csv \
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 $A > /dev/null 2> $O/${T}c5_pmc_write.err
+    ) || { tail -20 $O/${T}c5_prof_trace.err $O/${T}c5_pmc_*.err; exit 1; }
+    d() { dirname "$(find $O/${T}c5_$1 -name "$1_$2" -print -quit)"; }
+    python tools/pmc_summary.py ${T}c5 "$(d trace kernel_trace.csv)" "$(d fetch counter_collection.csv)" \
+      "$(d write counter_collection.csv)" 16777216 $O/${T}c5_prof_bench.json $O > /dev/null || exit 1
+    cp "$(d trace kernel_stats.csv)/trace_kernel_stats.csv" $O/${T}c5_rocprof_kernel_stats.csv
+    python -c "import json;d=json.load(open('$O/${T}c5_pmc.json'));print({k:d.get(k) for k in ('dominant_kernel','rocprof_avg_us','traffic_over_algorithmic','kernel_src_sha')})" ;;
   configs)
     timeout -k 10 400 python tools/bench_configs.py > $O/${T}_configs.json 2> $O/${T}_configs.err || { tail -20 $O/${T}_configs.err; exit 1; }
     cat $O/${T}_configs.json ;;

@@ -685,18 +685,18 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const bool snt = nt >= 0 ? (nt != 0) : true;
         const bool two = tx && g_tune_tx_passes.load() != 1;
         char desc[112];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
-                 tx ? "tx" : "rx", spw, two ? " +pkt_scatter_kernel" : "");
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
+                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "");
         netcsum::set_last_launch(desc);
         hipStream_t hs = static_cast<hipStream_t>(hip_stream);
         if (two) {
             // the records live in this stream's scratch buffer (stream_scratch)
             void* rec = nullptr;
             NC_HIP(stream_scratch(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord), &rec));
-            NC_HIP(netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs, static_cast<netcsum::PktTxRecord*>(rec)));
+            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs, static_cast<netcsum::PktTxRecord*>(rec)));
             return NET_UTIL_ERR_NONE;
         }
-        NC_HIP(netcsum::launch_pkt_stream(a, d, spw, snt, tx, hs));
+        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs));
         return NET_UTIL_ERR_NONE;
     }
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)

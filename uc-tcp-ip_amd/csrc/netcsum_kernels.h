@@ -95,8 +95,8 @@ int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
-hipError_t launch_pkt_stream(const PktBatchArgs& a, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
-                             PktTxRecord* rec = nullptr);     // rec: two-pass Tx (records + scatter pass)
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx,
+                             hipStream_t s, PktTxRecord* rec = nullptr);   // rec: two-pass Tx (records + scatter)
 void set_last_launch(const char* desc);
 hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256

@@ -21,7 +21,17 @@
 //     one coalesced byte store, Tx checksum fields in place (host-order value memcpy'd,
 //     net_ipv4.c:9586, net_tcp.c:29862, net_udp.c:2937).
 //
-// Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64, gap <= 64 B), IPv4.
+// IPv6 (VER 6) and mixed rings (VER 0, per datagram by the version nibble) take the same form with
+// the parse of pkt_parse_v6 (netcsum_packets.hip, whose header cites net_ipv6.c / net_icmpv6.c):
+// no header checksum; the transport sum is the stream total minus the window's sum of [0, 8) and of
+// the extension headers [40, transport start) — the addresses [8, 40) stay in, the length and next
+// header words of the 40-B pseudo-header are added in registers; ICMPv6 types 1/3/4 on Rx subtract
+// all of [0, transport start) (no pseudo-header, net_icmpv6.c:2910-2920). Hop-by-Hop / Routing /
+// Destination Options headers are walked inside the lane's window: the first 96 - lead bytes of the
+// datagram (lead = its address mod 16), the window(lead) of oracle_packets._parse6; a chain beyond it
+// gets EXT_HDR, exactly as the lane-group kernel does beyond its 16 G - lead bytes.
+//
+// Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64, gap <= 64 B).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -91,7 +101,8 @@ __device__ __forceinline__ uint32_t field_le(uint32_t b0, uint32_t b1, bool odd)
 struct LanePkt {          // lane k's packet after the prologue
     uint32_t flags;
     uint32_t end;         // packet offset one past the bytes the stream sums (0: none)
-    uint32_t ip_sum;      // exact half-word sum of the IP header [0, hlen) (absolute LE frame)
+    uint32_t ip_sum;      // IPv4: exact half-word sum of the IP header [0, hlen) (absolute LE frame);
+                          // IPv6: the bytes of [0, end) outside the transport sum (see the header)
     uint32_t fields;      // Tx: exact contribution of the checksum fields to be zeroed (IP | L4 sum)
     uint32_t l4_field;    // Tx: contribution of the transport field alone
     uint32_t pseudo_le;
@@ -99,7 +110,134 @@ struct LanePkt {          // lane k's packet after the prologue
     uint32_t proto;
     bool     check_l4;
     bool     malformed;
+    bool     v6;
 };
+
+// Exact half-word sum of packet bytes [0, x) from the lane's window (lead + x <= 96).
+__device__ __forceinline__ uint32_t win_prefix(const u32x4 (&h)[6], uint32_t lead, uint32_t x) {
+    uint32_t s = 0u - low_bytes(h[0], (int)lead);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        s += low_bytes(h[c], min(max((int)(lead + x) - 16 * c, 0), 16));
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+
+// Extension-header values of pkt_parse_v6 (netcsum_packets.hip).
+__device__ __forceinline__ bool ipv6_ext(uint32_t nh) {
+    return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 59u || nh == 60u ||
+           nh == 135u || nh == 139u || nh == 140u || nh == 253u || nh == 254u;
+}
+
+// IPv6 parse of pkt_parse_v6 from the lane's own window (RFC 8200; net_ipv6.c:8290-8360, 8601,
+// 5682; net_tcp.c:7871-7879; net_udp.c:1947-1957; net_icmpv6.c:2910-2948).
+template <bool TX>
+__device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
+                                               uint32_t avail, bool odd, bool udp_tx_csum, uint32_t d0, uint32_t d1) {
+    LanePkt p{};
+    p.l4_csum_off = ~0u;
+    p.v6 = true;
+    const uint32_t tot = 40u + be16(d1, 0);
+    uint32_t nh = (d1 >> 16) & 0xFFu;
+    if (avail < 40u || ((d0 >> 4) & 0xFu) != 6u || tot > avail) {
+        p.flags = NETCSUM_PKT_MALFORMED;
+        p.malformed = true;
+        return p;
+    }
+    const uint32_t window = 96u - lead;                          // bytes of the datagram in the window
+    uint32_t off = 40u;
+    for (int e = 0; e < 4 && (nh == 0u || nh == 43u || nh == 60u); ++e) {
+        if ((nh == 0u && off != 40u) || off + 8u > window) {
+            p.flags = NETCSUM_PKT_EXT_HDR;
+            return p;
+        }
+        const uint32_t d = pkt_dword_at(wd, lead, off);
+        off += (((d >> 8) & 0xFFu) + 1u) * 8u;
+        nh = d & 0xFFu;
+        if (off > tot) {                                         // extension header past the payload
+            p.flags = NETCSUM_PKT_MALFORMED;
+            p.malformed = true;
+            return p;
+        }
+    }
+    if (nh == 44u) {
+        p.flags = NETCSUM_PKT_FRAGMENT;
+        return p;
+    }
+    if (ipv6_ext(nh) || (off != 40u && off + 24u > window)) {
+        p.flags = NETCSUM_PKT_EXT_HDR;
+        return p;
+    }
+    p.proto = nh;
+    const uint32_t ulen = tot - off;                             // upper-layer length (< 2^16)
+    const uint32_t pseudo = (nh << 8) + swap16(ulen);
+    bool nopseudo = false;
+    switch (nh) {
+    case 6u:
+        if (ulen < 20u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.check_l4 = true;
+        p.l4_csum_off = off + 16u;
+        break;
+    case 17u: {
+        if (ulen < 8u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        const uint32_t du = pkt_dword_at(wd, lead, off + 4u);
+        if (be16(du, 0) != ulen) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = off + 6u;
+        if (!TX && (du >> 16) == 0u) {
+            p.flags = NETCSUM_PKT_UDP_NO_CSUM | NETCSUM_PKT_L4_OK;
+            return p;
+        }
+        if (TX && !udp_tx_csum) {
+            p.flags = NETCSUM_PKT_UDP_NO_CSUM;
+            return p;
+        }
+        p.check_l4 = true;
+        break;
+    }
+    case 58u:
+        if (ulen < 4u) {
+            p.flags = NETCSUM_PKT_L4_MALFORMED;
+            return p;
+        }
+        p.l4_csum_off = off + 2u;
+        if constexpr (TX) {
+            p.check_l4 = true;
+        } else {
+            const uint32_t type = pkt_dword_at(wd, lead, off) & 0xFFu;
+            if (type == 1u || type == 3u || type == 4u) {
+                p.check_l4 = true;
+                nopseudo = true;                                 // message alone (net_icmpv6.c:2910-2920)
+            } else if ((type >= 128u && type <= 131u) || (type >= 134u && type <= 137u)) {
+                p.check_l4 = true;
+            }
+        }
+        break;
+    default:
+        break;
+    }
+    if (p.check_l4) {
+        p.end = tot;
+        const uint32_t s_off = win_prefix(h, lead, off);
+        p.ip_sum = nopseudo ? s_off : s_off - (win_prefix(h, lead, 40u) - win_prefix(h, lead, 8u));
+        p.pseudo_le = nopseudo ? 0u : pseudo;
+        if constexpr (TX) {
+            const uint32_t fd = pkt_dword_at(wd, lead, p.l4_csum_off);
+            p.l4_field = field_le(fd & 0xFFu, (fd >> 8) & 0xFFu, odd);
+        }
+    }
+    return p;
+}
 
 // IPv4 parse of pkt_parse (netcsum_packets.hip) from the lane's own window; `avail` bytes present.
 template <bool TX>
@@ -201,7 +339,23 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memc
 
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
-template <int D, bool NT, bool TX, bool REC>
+template <int VER, bool TX>
+__device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
+                                                  uint32_t avail, bool odd, bool udp_tx_csum) {
+    if constexpr (VER == 4) {
+        return lane_parse<TX>(wd, h, lead, avail, odd, udp_tx_csum);
+    } else {
+        const uint32_t d0 = pkt_dword_fixed<0>(wd, lead);
+        const uint32_t d1 = pkt_dword_fixed<4>(wd, lead);
+        if (VER == 6 || ((d0 >> 4) & 0xFu) == 6u) {
+            return lane_parse6<TX>(wd, h, lead, avail, odd, udp_tx_csum, d0, d1);
+        }
+        return lane_parse<TX>(wd, h, lead, avail, odd, udp_tx_csum);
+    }
+}
+
+// VER 4 / 6: one IP version per batch; VER 0: per datagram by the version nibble (a mixed ring).
+template <int D, bool NT, bool TX, bool REC, int VER>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -249,7 +403,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         wd[4 * c + 3] = h[c].w;
     }
     const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
-    const LanePkt pk = lane_parse<TX>(wd, h, plead, L, odd, A.udp_tx_csum != 0u);
+    const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, L, odd, A.udp_tx_csum != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
 
     uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k
@@ -329,12 +483,12 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     uint32_t cip = ~0u, cl4 = ~0u;
     if (!pk.malformed) {
         if constexpr (!TX) {
-            f |= (sip == 0xFFFFu) ? NETCSUM_PKT_IP_OK : 0u;
+            f |= (pk.v6 || sip == 0xFFFFu) ? NETCSUM_PKT_IP_OK : 0u;   // IPv6: well-formed (no header checksum)
             if (pk.check_l4) {
                 f |= NETCSUM_PKT_L4_CHECKED | ((sl4 == 0xFFFFu) ? NETCSUM_PKT_L4_OK : 0u);
             }
         } else {
-            cip = (~sip) & 0xFFFFu;                              // net_ipv4.c:9578-9586
+            cip = pk.v6 ? ~0u : ((~sip) & 0xFFFFu);             // net_ipv4.c:9578-9586; IPv6: none
             f |= NETCSUM_PKT_IP_OK;
             if (pk.check_l4) {
                 cl4 = (~sl4) & 0xFFFFu;
@@ -419,7 +573,7 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
     }
 }
 
-template <int D, bool NT, bool TX>
+template <int D, bool NT, bool TX, int VER>
 hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
     PktBatchArgs a = a0;
     // no piece touch by default: the header prologue already loads each packet's first bytes with
@@ -428,31 +582,36 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     if (TX && rec != nullptr) {
-        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(pkt_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a, (const PktTxRecord*)rec);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Strided IPv4 batches of >= 64-B packets, dense (gap <= 64 B), whose runs span < 2^31 bytes.
+// Strided batches of >= 64-B packets (IPv4, IPv6 or mixed), dense (gap <= 64 B), whose runs span
+// < 2^31 bytes.
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver) {
-    return ip_ver == 4 && a.off == nullptr && a.len_u >= 64u && a.stride >= a.len_u && a.stride <= a.len_u + 64u &&
-           (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
+    return (ip_ver == 4 || ip_ver == 6 || ip_ver == 0) && a.off == nullptr && a.len_u >= 64u && a.stride >= a.len_u &&
+           a.stride <= a.len_u + 64u && (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
 
-hipError_t launch_pkt_stream(const PktBatchArgs& a, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
                              PktTxRecord* rec) {
     if (spw == 0u || spw > kMaxRunPkts) return hipErrorInvalidValue;
-#define NETCSUM_P(D_, NT_, TX_) \
-    if (depth == D_ && nt == NT_ && tx == TX_) return launch_pkt_stream_t<D_, NT_, TX_>(a, spw, s, rec);
-    NETCSUM_P(4, true, false) NETCSUM_P(4, false, false) NETCSUM_P(4, true, true) NETCSUM_P(4, false, true)
-    NETCSUM_P(8, true, false) NETCSUM_P(8, false, false) NETCSUM_P(8, true, true) NETCSUM_P(8, false, true)
+#define NETCSUM_P(V_, D_, NT_, TX_) \
+    if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_) return launch_pkt_stream_t<D_, NT_, TX_, V_>(a, spw, s, rec);
+#define NETCSUM_PV(V_)                                                                                      \
+    NETCSUM_P(V_, 4, true, false) NETCSUM_P(V_, 4, false, false) NETCSUM_P(V_, 4, true, true)                \
+    NETCSUM_P(V_, 4, false, true) NETCSUM_P(V_, 8, true, false) NETCSUM_P(V_, 8, false, false)               \
+    NETCSUM_P(V_, 8, true, true) NETCSUM_P(V_, 8, false, true)
+    NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
+#undef NETCSUM_PV
 #undef NETCSUM_P
     return hipErrorInvalidValue;
 }
