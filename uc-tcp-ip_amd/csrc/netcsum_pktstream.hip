@@ -382,8 +382,6 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
 
-    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);    // row touch (netcsum_stream.h)
-
     // ... while lane k parses packet k from its own 96-B window.
     const bool mine = lane < nres;
     const uint32_t prel = lead0 + lane * st;                   // run-relative start of packet `lane`
@@ -404,6 +402,10 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     }
     const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
     const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, L, odd, A.udp_tx_csum != 0u);
+    // Row touch (off by default here: the header loads above already touch every datagram) issued
+    // after the parse, when the window's registers are free (issued before it, its two VGPRs raised
+    // the prologue's peak to 73 = 6 waves/SIMD).
+    const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
 
     uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k

@@ -66,8 +66,9 @@ __device__ __forceinline__ RunTouch touch_run(__amdgpu_buffer_rsrc_t r, uint32_t
     return t;
 }
 
-// The touched values are consumed here, after the run's final vmcnt(0), so no wait is ever placed
-// on them earlier.
+// The touched values are consumed here: either after a wait that in-order retirement already makes
+// cover the touches (loads issued after them and awaited anyway), or after the run's final vmcnt(0).
+// Never earlier: consuming them alone would wait for every piece issued before them.
 __device__ __forceinline__ void touch_retire(RunTouch t) {
     asm volatile("" ::"v"(t.a), "v"(t.b));
 }

@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     uint32_t ps0 = 0u, ps1 = 0u;
     if constexpr (PH != 0) {
         run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
+        touch_retire(touch);                                   // issued before the pseudo loads: retired
     }
 
     uint32_t res0 = 0u, res1 = 0u;                             // result of run segment k: lane k % 64
@@ -292,7 +293,9 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     }
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
-    touch_retire(touch);
+    if constexpr (PH == 0) {
+        touch_retire(touch);
+    }
 
     store_run_results(A, s_begin, nres, lane, res0, res1);
 #if defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE == 1
