@@ -76,6 +76,26 @@ CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumDataVerify(void        *pdata_buf,
 CPU_INT32U   NetUtil_16BitSumDataCalcAlign_32    (void        *pdata_32,
                                                   CPU_INT32U   size);
 
+/* CRC-32 of net_util.c:485-636 (IEEE 802.3 polynomial, reflected, register initialised to
+ * 0xFFFFFFFF): Calc returns the register, CalcCpl its complement (the Ethernet FCS value), Reflect
+ * reverses the 32 bits (net_util.c:610-636; the drivers' multicast hash, e.g.
+ * Dev/Ether/GMAC/net_dev_gmac.c:2673-2683). With NETCSUM_ARG_CHK_EXT_EN (default 1, the template's
+ * NET_ERR_CFG_ARG_CHK_EXT_EN = DEF_ENABLED, net_cfg.h:178): p_data NULL -> 0 and
+ * NET_ERR_FAULT_NULL_PTR, data_len 0 -> 0 and NET_UTIL_ERR_NULL_SIZE. The CRC is computed on the
+ * GPU (NetUtil_MI355X_CRC32Host); Reflect is a bit permutation of one register, done in host C.
+ *  NetUtil_32BitCRC_Calc     replaces Source/net_util.c:485  (decl net_util.h:442)
+ *  NetUtil_32BitCRC_CalcCpl  replaces Source/net_util.c:571  (decl net_util.h:446)
+ *  NetUtil_32BitReflect      replaces Source/net_util.c:610  (decl net_util.h:450) */
+CPU_INT32U   NetUtil_32BitCRC_Calc               (CPU_INT08U  *p_data,
+                                                  CPU_INT32U   data_len,
+                                                  NET_ERR     *p_err);
+
+CPU_INT32U   NetUtil_32BitCRC_CalcCpl            (CPU_INT08U  *p_data,
+                                                  CPU_INT32U   data_len,
+                                                  NET_ERR     *p_err);
+
+CPU_INT32U   NetUtil_32BitReflect                (CPU_INT32U   val);
+
 /* ============================================================================================
  * (2) Batch ABI — device-resident segments.
  *
@@ -311,6 +331,33 @@ NET_ERR  NetUtil_MI355X_ShardVarLen        (const uint16_t *seg_len,
                                             CPU_INT16U      pseudo_len,
                                             uint32_t        world,
                                             uint32_t       *first);
+
+/* CRC-32 batches (device memory): d_out[i] = NetUtil_32BitCRC_Calc (cpl = 0) or _CalcCpl (cpl != 0)
+ * of segment i — base + i * stride, `len` bytes (strided) or base + d_off[i], d_len[i] bytes
+ * (varlen) — any alignment and length; an empty segment gives 0 (the reference's NULL_SIZE case).
+ * Segments up to 256 B (strided) take one lane each with slicing-by-4 tables in LDS; longer ones a
+ * 16-lane group whose lanes CRC equal blocks and merge them by GF(2) shifts (netcsum_crc.hip). */
+NET_ERR  NetUtil_MI355X_CRC32BatchStrided  (const void *d_base,
+                                            uint64_t    stride,
+                                            uint32_t    len,
+                                            uint32_t    n,
+                                            uint32_t   *d_out,
+                                            int         cpl,
+                                            void       *hip_stream);
+
+NET_ERR  NetUtil_MI355X_CRC32BatchVarLen   (const void     *d_base,
+                                            const uint64_t *d_off,
+                                            const uint32_t *d_len,
+                                            uint32_t        n,
+                                            uint32_t       *d_out,
+                                            int             cpl,
+                                            void           *hip_stream);
+
+/* One CRC-32 register value (NetUtil_32BitCRC_Calc's result) of a host buffer, computed on the GPU
+ * from this thread's pinned staging (the per-call path of the drop-in CRC functions). */
+NET_ERR  NetUtil_MI355X_CRC32Host          (const void *h_data,
+                                            uint32_t    len,
+                                            uint32_t   *p_crc);
 
 /* Frees the calling thread's per-device contexts (stream, pinned staging, device buffers) used by
  * the four drop-in functions, NetUtil_MI355X_StreamSum32 and ..._ChkSumBatchStridedHost. They are

@@ -451,3 +451,68 @@ void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t s
         }
     }
 }
+
+/* ------------------------------ CRC-32 (net_util.c:485-636) ------------------------------- */
+
+/* Restates NetUtil_32BitCRC_Calc (net_util.c:485-530): register starts at
+ * NET_UTIL_32_BIT_ONES_CPL_NEG_ZERO (0xFFFFFFFF, :58), each octet is XORed into the low byte and
+ * shifted out bit by bit against the reflected IEEE 802.3 polynomial 0xEDB88320 (:77), no final
+ * complement. Argument checks of NET_ERR_CFG_ARG_CHK_EXT_EN (template default enabled,
+ * net_cfg.h:178): NULL -> NET_ERR_FAULT_NULL_PTR (23), zero length -> NET_UTIL_ERR_NULL_SIZE (210),
+ * both returning 0. */
+uint32_t Oracle_CRC32Calc(const uint8_t *p_data, uint32_t data_len, uint32_t *p_err)
+{
+    uint32_t crc = 0xFFFFFFFFu, i, j;
+    if (p_data == NULL) {
+        *p_err = 23u;
+        return 0u;
+    }
+    if (data_len < 1u) {
+        *p_err = 210u;
+        return 0u;
+    }
+    for (i = 0u; i < data_len; ++i) {
+        uint32_t v = (crc ^ p_data[i]) & 0xFFu;
+        for (j = 0u; j < 8u; ++j) {
+            v = (v & 1u) ? ((v >> 1) ^ 0xEDB88320u) : (v >> 1);
+        }
+        crc = (crc >> 8) ^ v;
+    }
+    *p_err = 200u;
+    return crc;
+}
+
+/* NetUtil_32BitCRC_CalcCpl (net_util.c:571-588): the same, complemented; 0 on error. */
+uint32_t Oracle_CRC32CalcCpl(const uint8_t *p_data, uint32_t data_len, uint32_t *p_err)
+{
+    uint32_t crc = Oracle_CRC32Calc(p_data, data_len, p_err);
+    if (*p_err != 200u) {
+        return 0u;
+    }
+    return crc ^ 0xFFFFFFFFu;
+}
+
+/* NetUtil_32BitReflect (net_util.c:610-636): bit i -> bit 31 - i. */
+uint32_t Oracle_Reflect32(uint32_t val)
+{
+    uint32_t r = 0u, i;
+    for (i = 0u; i < 32u; ++i) {
+        if (val & (1u << i)) {
+            r |= 1u << (31u - i);
+        }
+    }
+    return r;
+}
+
+/* Batch driver: out[i] = Calc (cpl 0) or CalcCpl (cpl 1) of segment i (base + off[i] or
+ * base + i*stride, len[i] or len bytes); 0 for an empty segment (the reference's NULL_SIZE). */
+void Oracle_CRC32Batch(const uint8_t *base, const uint64_t *off, const uint32_t *lens, uint64_t stride,
+                       uint32_t len, uint32_t n, uint32_t *out, int cpl)
+{
+    uint32_t i, err;
+    for (i = 0u; i < n; ++i) {
+        const uint8_t *p = base + (off ? off[i] : (uint64_t)i * stride);
+        const uint32_t l = lens ? lens[i] : len;
+        out[i] = cpl ? Oracle_CRC32CalcCpl(p, l, &err) : Oracle_CRC32Calc(p, l, &err);
+    }
+}

@@ -72,6 +72,14 @@ void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t s
 uint32_t Oracle_C1Loop(const void *pdata_buf, const void *ppseudo_hdr, uint16_t pseudo_hdr_size,
                        const void *ip_hdr, uint64_t iters);
 
+/* CRC-32 of net_util.c:485-636 (IEEE 802.3, reflected, init 0xFFFFFFFF; Calc without and CalcCpl
+ * with the final complement; NULL -> 23, zero length -> 210 with the EXT argument checks on). */
+uint32_t Oracle_CRC32Calc(const uint8_t *p_data, uint32_t data_len, uint32_t *p_err);
+uint32_t Oracle_CRC32CalcCpl(const uint8_t *p_data, uint32_t data_len, uint32_t *p_err);
+uint32_t Oracle_Reflect32(uint32_t val);
+void     Oracle_CRC32Batch(const uint8_t *base, const uint64_t *off, const uint32_t *lens, uint64_t stride,
+                           uint32_t len, uint32_t n, uint32_t *out, int cpl);
+
 /* Number of OpenMP threads the batch drivers would use with n_threads = 0. */
 int  Oracle_MaxThreads(void);
 

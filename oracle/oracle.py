@@ -79,6 +79,14 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.Oracle_Fill.restype = None
     L.Oracle_C1Loop.argtypes = [vp, vp, u16, vp, u64]
     L.Oracle_C1Loop.restype = u32
+    L.Oracle_CRC32Calc.argtypes = [vp, u32, pu32]
+    L.Oracle_CRC32Calc.restype = u32
+    L.Oracle_CRC32CalcCpl.argtypes = [vp, u32, pu32]
+    L.Oracle_CRC32CalcCpl.restype = u32
+    L.Oracle_Reflect32.argtypes = [u32]
+    L.Oracle_Reflect32.restype = u32
+    L.Oracle_CRC32Batch.argtypes = [vp, vp, vp, u64, u32, u32, vp, i32]
+    L.Oracle_CRC32Batch.restype = None
     L.Oracle_MaxThreads.argtypes = []
     L.Oracle_MaxThreads.restype = i32
     return L
@@ -179,3 +187,30 @@ def c1_loop(pbuf, pseudo, pseudo_size, ip_hdr, iters: int) -> int:
 
 def max_threads() -> int:
     return int(lib().Oracle_MaxThreads())
+
+
+# ---- CRC-32 (net_util.c:485-636) -----------------------------------------------------------
+
+def crc32_calc(data, cpl: bool = False):
+    """(crc, err) of NetUtil_32BitCRC_Calc / _CalcCpl over `data` (bytes, or None for NULL)."""
+    err = ctypes.c_uint32()
+    if data is None:
+        p, n = None, 0
+    else:
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        p, n = ctypes.addressof(buf), len(data)
+    f = lib().Oracle_CRC32CalcCpl if cpl else lib().Oracle_CRC32Calc
+    return int(f(p, n, ctypes.byref(err))), int(err.value)
+
+
+def reflect32(v: int) -> int:
+    return int(lib().Oracle_Reflect32(v))
+
+
+def crc32_batch(base: np.ndarray, n: int, cpl: bool, stride: int = 0, length: int = 0, off=None, lens=None):
+    out = np.zeros(n, np.uint32)
+    o = None if off is None else np.ascontiguousarray(off, np.uint64)
+    ln = None if lens is None else np.ascontiguousarray(lens, np.uint32)
+    lib().Oracle_CRC32Batch(base.ctypes.data, None if o is None else o.ctypes.data,
+                            None if ln is None else ln.ctypes.data, stride, length, n, out.ctypes.data, int(cpl))
+    return out

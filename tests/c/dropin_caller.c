@@ -244,6 +244,40 @@ static void check_errors(void)
 #endif
 }
 
+/* CRC-32 drop-ins (net_util.c:485-636): the EXT argument checks answered on the host, the
+ * complement relation, the CRC-32 check value through the device, and the bit reflection. */
+static uint32_t crc_bitwise(const uint8_t *p, uint32_t n)
+{
+    uint32_t c = 0xFFFFFFFFu, i, j;
+    for (i = 0; i < n; ++i) {
+        c ^= p[i];
+        for (j = 0; j < 8; ++j) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    }
+    return c;
+}
+
+static void check_crc(void)
+{
+    static uint8_t kat[] = "123456789";
+    uint8_t mac[6] = { 0x01, 0x00, 0x5E, 0x12, 0x34, 0x56 };
+    NET_ERR err;
+    CPU_INT32U v;
+    uint32_t i, r;
+    CHECK(NetUtil_32BitCRC_Calc(NULL, 6, &err) == 0u && (unsigned)err == NET_ERR_FAULT_NULL_PTR,
+          "CRC(NULL) -> %u (net_util.c:499-503)", (unsigned)err);
+    CHECK(NetUtil_32BitCRC_CalcCpl(mac, 0, &err) == 0u && (unsigned)err == NET_UTIL_ERR_NULL_SIZE,
+          "CRC(len 0) -> %u (net_util.c:504-508)", (unsigned)err);
+    v = NetUtil_32BitCRC_CalcCpl(kat, 9, &err);
+    if (dev_result(err, "CRC32 CalcCpl")) CHECK(v == 0xCBF43926u, "CRC-32 check value %08x", (unsigned)v);
+    v = NetUtil_32BitCRC_Calc(mac, 6, &err);
+    if (dev_result(err, "CRC32 Calc")) CHECK(v == crc_bitwise(mac, 6), "CRC of a MAC %08x", (unsigned)v);
+    for (i = 0; i < 32; ++i) {
+        r = NetUtil_32BitReflect(1u << i);
+        CHECK(r == (1u << (31u - i)), "Reflect(bit %u) = %08x", i, r);
+    }
+    CHECK(NetUtil_32BitReflect(0x12345678u) == 0x1E6A2C48u, "Reflect(0x12345678)");
+}
+
 static void *thread_main(void *arg)
 {
     uint32_t t = (uint32_t)(uintptr_t)arg, k;
@@ -266,6 +300,7 @@ int main(void)
     }
     check_headers();
     check_errors();
+    check_crc();
     /* two host threads on the same device, each with its own chains and context */
     for (i = 0; i < 2; ++i) pthread_create(&th[i], NULL, thread_main, (void *)(uintptr_t)i);
     for (i = 0; i < 2; ++i) pthread_join(th[i], NULL);

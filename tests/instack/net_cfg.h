@@ -8,5 +8,10 @@
 #else
 #define NET_ERR_CFG_ARG_CHK_DBG_EN   DEF_DISABLED
 #endif
+#ifdef NETCSUM_TEST_NO_EXT
+#define NET_ERR_CFG_ARG_CHK_EXT_EN   DEF_DISABLED
+#else
+#define NET_ERR_CFG_ARG_CHK_EXT_EN   DEF_ENABLED   /* template default, Cfg/Template/net_cfg.h:178 */
+#endif
 #define NET_TCP_MODULE_EN                        /* net_cfg_net.h: TCP configured in */
 #endif

@@ -1,5 +1,5 @@
-/* In-stack compile check: the declarations of Source/net_util.h the drop-in implements. The four
- * prototypes are the reference's (net_util.h:422-438; tests/test_boundary_cpu.py compares them token
+/* In-stack compile check: the declarations of Source/net_util.h the drop-in implements. The
+ * prototypes are the reference's (net_util.h:422-450; tests/test_boundary_cpu.py compares them token
  * for token with the reference header when /root/reference is present). */
 #ifndef NET_UTIL_MODULE_PRESENT
 #define NET_UTIL_MODULE_PRESENT
@@ -30,4 +30,14 @@ CPU_BOOLEAN  NetUtil_16BitOnesCplChkSumDataVerify(void        *pdata_buf,
 
 CPU_INT32U  NetUtil_16BitSumDataCalcAlign_32(void        *pdata_32,
                                              CPU_INT32U   size);
+
+CPU_INT32U   NetUtil_32BitCRC_Calc               (CPU_INT08U  *p_data,
+                                                  CPU_INT32U   data_len,
+                                                  NET_ERR     *p_err);
+
+CPU_INT32U   NetUtil_32BitCRC_CalcCpl            (CPU_INT08U  *p_data,
+                                                  CPU_INT32U   data_len,
+                                                  NET_ERR     *p_err);
+
+CPU_INT32U   NetUtil_32BitReflect                (CPU_INT32U   val);
 #endif

@@ -1,7 +1,7 @@
 """The drop-in boundary, checked by a compiler and a C caller (no GPU needed):
 
-* the four prototypes of include/netcsum_mi355x.h and of the in-stack stand-in tests/instack/net_util.h
-  equal the reference's Source/net_util.h:422-438 token for token, and every NET_BUF field the chain
+* the checksum and CRC prototypes of include/netcsum_mi355x.h and of the in-stack stand-in
+  tests/instack/net_util.h equal the reference's Source/net_util.h:422-450 token for token, and every NET_BUF field the chain
   walk reads has the reference's type in Source/net_buf.h:394-598 (skipped where the reference tree
   is absent, e.g. on the GPU box);
 * host/net_util_mi355x.c compiles -Wall -Wextra -Werror -pedantic in both modes — standalone and
@@ -23,7 +23,8 @@ REF = "/root/reference/Source"
 CDIR = os.path.join(REPO, "tests", "c")
 VARIANTS = ["standalone_asan", "dbg_asan", "instack_asan", "instack_dbg_asan"]
 FUNCS = ["NetUtil_16BitOnesCplChkSumHdrCalc", "NetUtil_16BitOnesCplChkSumHdrVerify",
-         "NetUtil_16BitOnesCplChkSumDataCalc", "NetUtil_16BitOnesCplChkSumDataVerify"]
+         "NetUtil_16BitOnesCplChkSumDataCalc", "NetUtil_16BitOnesCplChkSumDataVerify",
+         "NetUtil_32BitCRC_Calc", "NetUtil_32BitCRC_CalcCpl", "NetUtil_32BitReflect"]
 
 
 def _prototype(text, name):

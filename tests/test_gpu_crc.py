@@ -1,0 +1,133 @@
+"""GPU parity of the CRC-32 path (net_util.c:485-636): the drop-in NetUtil_32BitCRC_Calc / _CalcCpl
+on host buffers, the drivers' multicast hash built on them, and the strided / varlen batch kernels
+(one lane per short segment; 16-lane groups combining equal blocks by GF(2) shifts for long ones),
+against the C restatement (pinned to the CRC-32 check value and zlib in tests/test_crc_cpu.py).
+Full size: the Ethernet residue property — a segment followed by its little-endian CalcCpl value
+has CalcCpl 0x2144DF1C — over every segment of a 1 M x 1500-B batch."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RESIDUE = int(np.array([0x2144DF1C], np.uint32).view(np.int32)[0])   # CRC-32 residue, as the int32 out holds it
+
+
+def _host(data: bytes):
+    buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    return buf, ctypes.addressof(buf)
+
+
+@pytest.mark.parametrize("cpl", [False, True])
+def test_dropin_crc_vs_oracle(cpl):
+    rng = random.Random(11 + cpl)
+    for n in list(range(1, 80)) + [255, 256, 257, 1023, 1500, 4096, 9000, 65535, 65536, 200003]:
+        m = rng.randbytes(n)
+        keep, p = _host(m)
+        for off in [o for o in ((0, 1, 3) if n < 300 else (0, 5)) if o < n]:
+            got = netcsum.CRC32Calc(p + off, n - off, cpl)
+            want = oracle.crc32_calc(m[off:], cpl)
+            assert got == want, (n, off, hex(got[0]), hex(want[0]))
+    keep, p = _host(b"123456789")                                  # keep the buffer alive
+    assert netcsum.CRC32Calc(p, 9, True) == (0xCBF43926, netcsum.NET_UTIL_ERR_NONE)
+
+
+def test_dropin_multicast_hash_like_the_drivers():
+    """Dev/Ether/GMAC/net_dev_gmac.c:2673-2683: hash = Reflect(CalcCpl(mac, 6)) >> 26."""
+    rng = random.Random(3)
+    for _ in range(64):
+        mac = bytes([0x01, 0x00, 0x5E]) + rng.randbytes(3)
+        keep, p = _host(mac)
+        crc, err = netcsum.CRC32Calc(p, 6, True)
+        assert err == netcsum.NET_UTIL_ERR_NONE
+        want, _ = oracle.crc32_calc(mac, True)
+        assert (netcsum.Reflect32(crc) >> 26) & 0x3F == (oracle.reflect32(want) >> 26) & 0x3F
+
+
+STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (255, 256), (256, 256), (257, 300),
+           (1500, 1500), (1514, 1518), (4096, 4100), (9000, 9001)]
+
+
+@pytest.mark.parametrize("length,stride", STRIDED)
+@pytest.mark.parametrize("cpl", [0, 1])
+def test_crc_batch_strided_vs_oracle(length, stride, cpl):
+    rng = np.random.default_rng(length * 3 + stride + cpl)
+    n = 1000 if length <= 1514 else 200
+    for base_off in (0, 1, 2, 7):
+        data = rng.integers(0, 256, size=base_off + n * stride + 64, dtype=np.uint8)
+        d = torch.from_numpy(data).to(DEV)
+        out = torch.zeros(n, dtype=torch.int32, device=DEV)
+        netcsum.crc32_strided(d.data_ptr() + base_off, stride, length, n, out, cpl)
+        torch.cuda.synchronize()
+        want = oracle.crc32_batch(data[base_off:].copy(), n, bool(cpl), stride=stride, length=length)
+        got = out.cpu().numpy().view(np.uint32)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (base_off, [(int(i), hex(got[i]), hex(want[i])) for i in bad[:4]])
+        kern = netcsum.last_launch()
+        assert kern.startswith("crc_lane_kernel" if length <= 256 else "crc_group_kernel"), kern
+
+
+@pytest.mark.parametrize("cpl", [0, 1])
+def test_crc_batch_varlen_vs_oracle(cpl):
+    """Packed segments of 0..20000 B at every alignment, reversed and overlapping layouts."""
+    rng = np.random.default_rng(40 + cpl)
+    n = 3000
+    lens = rng.integers(0, 3000, size=n).astype(np.uint32)
+    lens[::97] = rng.integers(9000, 20000, size=len(lens[::97]))
+    lens[::53] = 0
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    off += 3
+    for layout in ("packed", "reversed", "overlap"):
+        o, ln = off.copy(), lens.copy()
+        if layout == "reversed":
+            o, ln = o[::-1].copy(), ln[::-1].copy()
+        elif layout == "overlap":
+            o = (o // 3).astype(np.uint64)
+        tot = int((o + ln).max()) + 64
+        data = rng.integers(0, 256, size=tot, dtype=np.uint8)
+        d = torch.from_numpy(data).to(DEV)
+        od = torch.from_numpy(o.view(np.int64)).to(DEV)
+        ld = torch.from_numpy(ln.view(np.int32)).to(DEV)
+        out = torch.zeros(n, dtype=torch.int32, device=DEV)
+        netcsum.crc32_varlen(d, od, ld, n, out, cpl)
+        torch.cuda.synchronize()
+        want = oracle.crc32_batch(data, n, bool(cpl), off=o, lens=ln)
+        got = out.cpu().numpy().view(np.uint32)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (layout, [(int(i), int(ln[i]), hex(got[i]), hex(want[i])) for i in bad[:4]])
+
+
+def test_crc_full_size_residue_1M():
+    """1 M x 1500-B frames (stride 1504): CalcCpl of each, written little-endian after it, then
+    CalcCpl over the 1504 bytes is the CRC-32 residue 0x2144DF1C for every frame; one flipped bit per
+    1000 frames breaks exactly those; 4096 sampled frames equal the oracle."""
+    n, L, S = 1 << 20, 1500, 1504
+    buf = torch.empty(n * S + 64, dtype=torch.uint8, device=DEV)
+    netcsum.fill(buf, n * S, 0x5EED00C3, 0)
+    fcs = torch.zeros(n, dtype=torch.int32, device=DEV)
+    netcsum.crc32_strided(buf, S, L, n, fcs, 1)
+    torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith("crc_group_kernel")
+    smp = np.sort(np.random.default_rng(9).choice(n, size=4096, replace=False))
+    rows = buf[: n * S].view(n, S)[torch.from_numpy(smp).to(DEV)].cpu().numpy()
+    want = oracle.crc32_batch(rows.reshape(-1).copy(), len(smp), True, stride=S, length=L)
+    assert np.array_equal(fcs.cpu().numpy().view(np.uint32)[smp], want)
+    v = buf[: n * S].view(n, S)
+    v[:, L:S] = fcs.view(torch.uint8).view(n, 4)
+    res = torch.zeros(n, dtype=torch.int32, device=DEV)
+    netcsum.crc32_strided(buf, S, S, n, res, 1)
+    torch.cuda.synchronize()
+    assert bool((res == RESIDUE).all())
+    bad = torch.arange(0, n, 1000, device=DEV)
+    v[bad, 321] ^= 0x20
+    netcsum.crc32_strided(buf, S, S, n, res, 1)
+    torch.cuda.synchronize()
+    wrong = torch.nonzero(res != RESIDUE).flatten()
+    assert torch.equal(wrong, bad)

@@ -212,6 +212,24 @@ def main():
         netcsum.DataCalc(ch.ptr, phb.ptr, 12)
     us = (time.perf_counter() - t0) / 2000 * 1e6
     out["C1_dropin_call_us"] = round(us, 2)
+    # ---- CRC-32 (net_util.c:485-636): 1 M x 1500-B frames (16-lane groups) and 16 M 6-B MAC
+    #      addresses (one lane each), CalcCpl, device-resident
+    nf, Lf = 1 << 20, 1500
+    fr = torch.empty(nf * Lf + 64, dtype=torch.uint8, device=dev)
+    netcsum.fill(fr, nf * Lf, SEED, 0)
+    fo = torch.empty(nf, dtype=torch.int32, device=dev)
+    ms_f = events_ms(lambda: netcsum.crc32_strided(fr, Lf, Lf, nf, fo, 1, stream=st), st)
+    kf = netcsum.last_launch()
+    del fr
+    nm = 1 << 24
+    macs = torch.empty(nm * 6 + 64, dtype=torch.uint8, device=dev)
+    netcsum.fill(macs, nm * 6, SEED, 0)
+    mo = torch.empty(nm, dtype=torch.int32, device=dev)
+    ms_m = events_ms(lambda: netcsum.crc32_strided(macs, 6, 6, nm, mo, 1, stream=st), st)
+    out["crc32"] = {"frames_1500B": {"n": nf, "ms": round(ms_f, 4), "GB_per_s": round(nf * (Lf + 4) / ms_f / 1e6, 1),
+                                     "kernel": kf},
+                    "macs_6B": {"n": nm, "ms": round(ms_m, 4), "G_per_s": round(nm / ms_m / 1e6, 2),
+                                "GB_per_s": round(nm * 10 / ms_m / 1e6, 1), "kernel": netcsum.last_launch()}}
     print(json.dumps(out))
 
 

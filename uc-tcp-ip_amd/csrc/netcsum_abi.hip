@@ -634,6 +634,67 @@ NET_ERR NetUtil_MI355X_StreamSum32(const NETCSUM_SPAN* spans, uint32_t n_spans, 
     return NET_UTIL_ERR_NONE;
 }
 
+NET_ERR NetUtil_MI355X_CRC32BatchStrided(const void* d_base, uint64_t stride, uint32_t len, uint32_t n,
+                                         uint32_t* d_out, int cpl, void* hip_stream) {
+    if (n == 0) return NET_UTIL_ERR_NONE;
+    if (d_out == nullptr || (d_base == nullptr && len != 0)) return NET_ERR_FAULT_NULL_PTR;
+    netcsum::CrcBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.stride = stride;
+    a.len = len;
+    a.n = n;
+    a.cpl = cpl ? 1u : 0u;
+    a.out = d_out;
+    netcsum::set_last_launch(len <= netcsum::kCrcShortMax ? "crc_lane_kernel block=256" : "crc_group_kernel G=16 block=256");
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    NC_HIP(netcsum::launch_crc_batch(a, len, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_CRC32BatchVarLen(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
+                                        uint32_t* d_out, int cpl, void* hip_stream) {
+    if (n == 0) return NET_UTIL_ERR_NONE;
+    if (d_out == nullptr || d_base == nullptr || d_off == nullptr || d_len == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    netcsum::CrcBatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.off = d_off;
+    a.lens = d_len;
+    a.n = n;
+    a.cpl = cpl ? 1u : 0u;
+    a.out = d_out;
+    netcsum::set_last_launch("crc_group_kernel G=16 block=256");
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    NC_HIP(netcsum::launch_crc_batch(a, 0xFFFFFFFFu, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
+    return NET_UTIL_ERR_NONE;
+}
+
+// One CRC-32 (the NetUtil_32BitCRC_Calc register value) of a host buffer: staged into this thread's
+// pinned buffer, read from there by the kernel (zero-copy), result copied back.
+NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_crc) {
+    if (p_crc == nullptr || (h_data == nullptr && len != 0)) return NET_ERR_FAULT_NULL_PTR;
+    HostCtx* cp = nullptr;
+    NET_ERR e = host_ctx(&cp);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    HostCtx& c = *cp;
+    *p_crc = 0u;
+    if (len == 0) return NET_UTIL_ERR_NONE;
+    e = ensure_stage(c, len);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    std::memcpy(c.h_stage, h_data, len);
+    netcsum::CrcBatchArgs a{};
+    a.base = c.h_stage_dev;
+    a.len = len;
+    a.n = 1;
+    a.out = reinterpret_cast<uint32_t*>(c.d_sum);
+    NC_HIP(netcsum::launch_crc_batch(a, len, cu_count(c.dev), c.stream));
+    NC_HIP(hipMemcpyAsync(c.h_sum, c.d_sum, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    NC_HIP(hipStreamSynchronize(c.stream));
+    *p_crc = *reinterpret_cast<volatile uint32_t*>(c.h_sum);
+    return NET_UTIL_ERR_NONE;
+}
+
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                          CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum, bool tx,
                          int ip_ver, void* hip_stream) {

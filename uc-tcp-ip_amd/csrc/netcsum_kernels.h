@@ -79,6 +79,22 @@ struct ChainBatchArgs {
 
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
 
+// CRC-32 batches (netcsum_crc.hip; net_util.c:485-636).
+struct CrcBatchArgs {
+    const uint8_t*  base;          // segment i at base + off[i] (varlen) or base + i * stride
+    const uint64_t* off;           // nullptr => strided
+    const uint32_t* lens;          // varlen lengths (nullptr => all `len`)
+    uint64_t        stride;
+    uint32_t        len;
+    uint32_t        n;
+    uint32_t        cpl;           // 0: NetUtil_32BitCRC_Calc, 1: NetUtil_32BitCRC_CalcCpl
+    uint32_t*       out;
+    uint32_t        xs[4];         // strided: x^(8 s 2^k) mod P of the 16-lane combine (set by the launcher)
+    uint32_t        xl;            // strided: x^(8 len) mod P
+};
+constexpr uint32_t kCrcShortMax = 256u;    // strided segments up to this length: one lane each
+hipError_t launch_crc_batch(const CrcBatchArgs& a, uint32_t max_len, int cus, hipStream_t s);
+
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, int ip_ver,  // 4, 6, 0 = per packet
                             hipStream_t s);
 

@@ -28,6 +28,9 @@
 #ifndef NETCSUM_ARG_CHK_DBG_EN
 #define NETCSUM_ARG_CHK_DBG_EN (NET_ERR_CFG_ARG_CHK_DBG_EN == DEF_ENABLED)
 #endif
+#ifndef NETCSUM_ARG_CHK_EXT_EN
+#define NETCSUM_ARG_CHK_EXT_EN (NET_ERR_CFG_ARG_CHK_EXT_EN == DEF_ENABLED)
+#endif
 #else
 #include "../../include/netcsum_mi355x.h"
 #include "../../include/netcsum_netbuf.h"
@@ -35,6 +38,9 @@
 #define NC_NET_TO_HOST_16(v) ((CPU_INT16U)__builtin_bswap16((uint16_t)(v)))
 #ifndef NETCSUM_ARG_CHK_DBG_EN
 #define NETCSUM_ARG_CHK_DBG_EN 0          /* template default: DEF_DISABLED (net_cfg.h:184) */
+#endif
+#ifndef NETCSUM_ARG_CHK_EXT_EN
+#define NETCSUM_ARG_CHK_EXT_EN 1          /* template default: DEF_ENABLED (net_cfg.h:178) */
 #endif
 #endif
 
@@ -269,4 +275,54 @@ CPU_INT32U NetUtil_16BitSumDataCalcAlign_32(void *pdata_32, CPU_INT32U size)
         return 0u;
     }
     return (CPU_INT32U)sum32;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * CRC-32 (net_util.c:485-636). The register is computed on the GPU; the host keeps the argument
+ * checks of NET_ERR_CFG_ARG_CHK_EXT_EN and the final complement.
+ * ---------------------------------------------------------------------------------------- */
+/* Replaces Source/net_util.c:485-530. */
+CPU_INT32U NetUtil_32BitCRC_Calc(CPU_INT08U *p_data, CPU_INT32U data_len, NET_ERR *p_err)
+{
+    uint32_t crc = 0u;
+    NET_ERR err;
+#if NETCSUM_ARG_CHK_EXT_EN
+    if (p_data == NULL) {                                     /* :499-503 */
+        *p_err = NET_ERR_FAULT_NULL_PTR;
+        return 0u;
+    }
+    if (data_len < 1u) {                                      /* :504-508 */
+        *p_err = NET_UTIL_ERR_NULL_SIZE;
+        return 0u;
+    }
+#endif
+    err = NetUtil_MI355X_CRC32Host(p_data, data_len, &crc);
+    if (err != NET_UTIL_ERR_NONE) {
+        *p_err = err;
+        return 0u;
+    }
+    /* without the EXT checks a zero length leaves the register at its initial value (:518-528) */
+    *p_err = NET_UTIL_ERR_NONE;
+    return (data_len == 0u) ? 0xFFFFFFFFu : (CPU_INT32U)crc;
+}
+
+/* Replaces Source/net_util.c:571-588. */
+CPU_INT32U NetUtil_32BitCRC_CalcCpl(CPU_INT08U *p_data, CPU_INT32U data_len, NET_ERR *p_err)
+{
+    CPU_INT32U crc = NetUtil_32BitCRC_Calc(p_data, data_len, p_err);
+    if (*p_err != NET_UTIL_ERR_NONE) {
+        return 0u;
+    }
+    return crc ^ 0xFFFFFFFFu;                                 /* :583 */
+}
+
+/* Replaces Source/net_util.c:610-636: bit i of val -> bit 31 - i. */
+CPU_INT32U NetUtil_32BitReflect(CPU_INT32U val)
+{
+    uint32_t v = (uint32_t)val;
+    v = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+    v = ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
+    v = ((v >> 4) & 0x0F0F0F0Fu) | ((v & 0x0F0F0F0Fu) << 4);
+    v = ((v >> 8) & 0x00FF00FFu) | ((v & 0x00FF00FFu) << 8);
+    return (CPU_INT32U)((v >> 16) | (v << 16));
 }

@@ -207,6 +207,18 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_RxValidateIP.restype = i32
     L.NetUtil_MI355X_TxFinalizeIP.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, vp]
     L.NetUtil_MI355X_TxFinalizeIP.restype = i32
+    L.NetUtil_32BitCRC_Calc.argtypes = [vp, u32, perr]
+    L.NetUtil_32BitCRC_Calc.restype = u32
+    L.NetUtil_32BitCRC_CalcCpl.argtypes = [vp, u32, perr]
+    L.NetUtil_32BitCRC_CalcCpl.restype = u32
+    L.NetUtil_32BitReflect.argtypes = [u32]
+    L.NetUtil_32BitReflect.restype = u32
+    L.NetUtil_MI355X_CRC32BatchStrided.argtypes = [vp, u64, u32, u32, vp, i32, vp]
+    L.NetUtil_MI355X_CRC32BatchStrided.restype = i32
+    L.NetUtil_MI355X_CRC32BatchVarLen.argtypes = [vp, vp, vp, u32, vp, i32, vp]
+    L.NetUtil_MI355X_CRC32BatchVarLen.restype = i32
+    L.NetUtil_MI355X_CRC32Host.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_uint32)]
+    L.NetUtil_MI355X_CRC32Host.restype = i32
     L.NetUtil_MI355X_Fill.argtypes = [vp, u64, u64, u64, i32, vp]
     L.NetUtil_MI355X_Fill.restype = i32
     L.NetUtil_MI355X_ReadStream.argtypes = [vp, u64, vp, vp]
@@ -339,6 +351,40 @@ def stream_sum32(spans):
     s = ctypes.c_uint32(0)
     err = lib().NetUtil_MI355X_StreamSum32(arr, len(spans), ctypes.byref(s))
     return int(s.value), int(err)
+
+
+# --------------------------------------------------------------------------- CRC-32 (net_util.c:485-636)
+def CRC32Calc(p_data, data_len, cpl=False):
+    """The drop-in NetUtil_32BitCRC_Calc / _CalcCpl on a host pointer -> (crc, err)."""
+    err = ctypes.c_int32()
+    f = lib().NetUtil_32BitCRC_CalcCpl if cpl else lib().NetUtil_32BitCRC_Calc
+    v = f(p_data, data_len, ctypes.byref(err))
+    return int(v), int(err.value)
+
+
+def Reflect32(val):
+    return int(lib().NetUtil_32BitReflect(val))
+
+
+def crc32_strided(base, stride, length, n, out, cpl=False, stream=None, check=True):
+    if n:
+        _require(base, (n - 1) * stride + length, "segments")
+        _require(out, 4 * n, "out")
+    err = lib().NetUtil_MI355X_CRC32BatchStrided(_p(base), stride, length, n, _p(out), int(cpl), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_CRC32BatchStrided")
+    return err
+
+
+def crc32_varlen(base, off, lens, n, out, cpl=False, stream=None, check=True):
+    if n:
+        _require(off, 8 * n, "offsets")
+        _require(lens, 4 * n, "lengths")
+        _require(out, 4 * n, "out")
+    err = lib().NetUtil_MI355X_CRC32BatchVarLen(_p(base), _p(off), _p(lens), n, _p(out), int(cpl), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_CRC32BatchVarLen")
+    return err
 
 
 # --------------------------------------------------------------------------- batch interface
