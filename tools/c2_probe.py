@@ -3,7 +3,8 @@
 segment kernel over the same number of bytes? Interleaves, in one process on one
 1 M x 1500-B buffer: C2 as bench.py runs it (12-B pseudo-headers from memory), C2 without
 pseudo-headers, C2 Verify (1-B results) (C2P_FORMS), each at several segments per wave (C2P_SPW) and
-residency caps (C2P_WAVES, NETCSUM_TUNE_STREAM_WAVES) and with / without the row touch (C2P_TOUCH),
+residency caps (C2P_WAVES, NETCSUM_TUNE_STREAM_WAVES), pieces in flight (C2P_D) and with / without
+the row touch (C2P_TOUCH),
 C4 (C2P_FORMS c4), the Rx packet kernel on the same bytes made
 IPv4/TCP, and the read probes. GPU box only; prints JSON lines."""
 import json
@@ -64,13 +65,14 @@ def main():
     variants = [("read_lds", dict(grid=8192, nt=1, probe=1), (-1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16),
                 ("read_reg", dict(grid=8192, nt=1, probe=0), (-1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16)]
     touches = [int(x) for x in os.environ.get("C2P_TOUCH", "-1").split(",")]
-    for w, spw, tch in [(w, spw, t) for w in [int(x) for x in os.environ.get("C2P_WAVES", "-1").split(",")]
-                        for spw in spws for t in touches]:
-            sfx = f"_spw{spw}_waves{w}_touch{tch}"
+    depths = [int(x) for x in os.environ.get("C2P_D", "0").split(",")]
+    for w, spw, tch, dd in [(w, spw, t, dd) for w in [int(x) for x in os.environ.get("C2P_WAVES", "-1").split(",")]
+                            for spw in spws for t in touches for dd in depths]:
+            sfx = f"_spw{spw}_waves{w}_touch{tch}" + (f"_D{dd}" if dd else "")
             if c4 is not None:
-                variants.append(("c4" + sfx, dict(kernel=6, tile=spw), (w, tch), c4[0], c4[1]))
+                variants.append(("c4" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch), c4[0], c4[1]))
             if "calc_pseudo" in forms:
-                variants.append(("c2_calc_pseudo" + sfx, dict(kernel=6, tile=spw), (w, tch), c2(True, 0), n * (L + 12 + 2)))
+                variants.append(("c2_calc_pseudo" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch), c2(True, 0), n * (L + 12 + 2)))
             if "calc_nopseudo" in forms:
                 variants.append(("c2_calc_nopseudo" + sfx, dict(kernel=6, tile=spw), (w, tch), c2(False, 0), n * (L + 2)))
             if "verify_pseudo" in forms:
