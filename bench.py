@@ -391,18 +391,26 @@ def main():
     except Exception as e:  # oracle missing on this host: report, never substitute
         parity_ok = f"unchecked: {e}"
 
-    # measured read-stream ceiling over the same bytes (roofline probe), same stream & events
+    # measured read-stream rates over the same bytes (roofline probes), same stream & events: the
+    # LDS-DMA grid-stride probe (TUNE_PROBE 1) and the run-stream form of the checksum kernel with no
+    # arithmetic (TUNE_PROBE 2, netcsum_stream.hip read_run_kernel)
     n16 = (n * L) // 16 * 16
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
-    for _ in range(3):
-        netcsum.read_stream(seg, n16, sink, stream=stream)
-    rs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for a, b in rs:
-        a.record(stream)
-        netcsum.read_stream(seg, n16, sink, stream=stream)
-        b.record(stream)
-    torch.cuda.synchronize()
-    rs_ms = sum(a.elapsed_time(b) for a, b in rs) / len(rs)
+    probe_ms = {}
+    for probe in (1, 2):
+        netcsum.tune(netcsum.TUNE_PROBE, probe)
+        for _ in range(20):
+            netcsum.read_stream(seg, n16, sink, stream=stream)
+        rs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for a, b in rs:
+            a.record(stream)
+            netcsum.read_stream(seg, n16, sink, stream=stream)
+            b.record(stream)
+        torch.cuda.synchronize()
+        probe_ms[probe] = sum(a.elapsed_time(b) for a, b in rs) / len(rs)
+    netcsum.tune(netcsum.TUNE_PROBE, 1)
+    rs_ms = probe_ms[1]
+    run_probe_gbps = n16 / (probe_ms[2] * 1e-3) / 1e9
 
     parity_all = parity_ok
     if world > 1:                                  # every rank's sample must match its oracle
@@ -456,7 +464,9 @@ def main():
                          "traffic_error": traffic_err,
                          "kernel_src_sha": kernel_src_sha(kernel_desc.split("::")[-1].split("<")[0]),
                          "read_stream_probe_GBps": round(n16 / (rs_ms * 1e-3) / 1e9, 1),
-                         "frac_of_read_stream_probe": round(achieved / (n16 / (rs_ms * 1e-3) / 1e9), 4)},
+                         "frac_of_read_stream_probe": round(achieved / (n16 / (rs_ms * 1e-3) / 1e9), 4),
+                         "run_stream_read_probe_GBps": round(run_probe_gbps, 1),
+                         "frac_of_run_stream_read_probe": round(achieved / run_probe_gbps, 4)},
             "parity_sample_ok": parity_all,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -424,7 +424,9 @@ typedef enum netcsum_tune_key {
                                          auto: the most that fit 4 KiB from any 128-B lead, 192 for
                                          20-B headers)                                              */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
-    NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default)  */
+    NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),
+                                         2 run-stream form of the checksum kernels (24-KiB runs per
+                                         wave, 4 nt pieces in flight, row touch, 5 waves per SIMD)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
     NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).

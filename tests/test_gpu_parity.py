@@ -265,11 +265,17 @@ def test_fill_matches_host_regeneration():
         assert np.array_equal(got[n - 777:], oracle.fill(n - 777, 777, 0x5EED0001, pattern))
 
 
-def test_read_stream_probe_runs():
-    buf = torch.ones(1 << 24, dtype=torch.uint8, device=DEV)
+@pytest.mark.parametrize("probe", [0, 1, 2])
+def test_read_stream_probe_runs(probe):
+    buf = torch.ones((1 << 24) + 4096, dtype=torch.uint8, device=DEV)
     sink = torch.zeros(1, dtype=torch.int64, device=DEV)
-    netcsum.read_stream(buf, buf.numel(), sink)
-    torch.cuda.synchronize()
+    netcsum.tune(netcsum.TUNE_PROBE, probe)
+    try:
+        for n in (1 << 24, (1 << 24) + 4096 - 16, 16):          # whole runs, a short last run, one chunk
+            netcsum.read_stream(buf, n, sink)
+        torch.cuda.synchronize()
+    finally:
+        netcsum.tune(netcsum.TUNE_PROBE, 1)
     assert int(sink.item()) == 0
 
 
