@@ -512,10 +512,10 @@ bool stream_one(const SegBatchArgs& a) {
 namespace {
 
 // Read-stream probe in the run-stream form (NETCSUM_TUNE_PROBE 2): a wave reads a run of
-// kProbeRun bytes exactly like seg_stream_kernel (1-KiB pieces, D = 4 in flight, nt loads, the row
-// touch, 5 waves per SIMD) and only adds the bytes up — the read rate the checksum kernel's access
-// pattern can reach on this device, with none of its arithmetic.
-constexpr uint32_t kProbeRun = 24u * 1024u;
+// kProbeRun bytes (C2's 16 x 1500 B) exactly like seg_stream_kernel — pieces of 1 KiB from the 128-B
+// line below the run, D = 4 in flight, nt loads, the row touch, 5 waves per SIMD — and only adds the
+// bytes up: the read rate the checksum kernel's access pattern can reach, with none of its arithmetic.
+constexpr uint32_t kProbeRun = 16u * 1500u;
 
 __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint64_t n_bytes, unsigned long long* sink) {
     constexpr int D = 4;
@@ -525,9 +525,11 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
     if (start >= n_bytes) {
         return;
     }
-    const uint32_t span = (uint32_t)min<uint64_t>(kProbeRun, n_bytes - start);
+    const uintptr_t a_first = (uintptr_t)base + start;
+    const uintptr_t O = a_first & ~(uintptr_t)127;
+    const uint32_t span = (uint32_t)(a_first - O) + (uint32_t)min<uint64_t>(kProbeRun, n_bytes - start);
     const uint32_t npieces = (span + 1023u) >> 10;
-    const __amdgpu_buffer_rsrc_t rd = run_rsrc((uintptr_t)base + start, (span + 15u) & ~15u);
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);   // lead bytes read, like the kernel
     const uint32_t lane16 = 16u * lane;
     u32x4 dv[D];
 #pragma unroll
