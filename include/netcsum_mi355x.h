@@ -442,10 +442,13 @@ typedef enum netcsum_tune_key {
                                          SIMD, 3..8, enforced by reserving LDS per workgroup; 0 = as
                                          many as registers allow; -1 = each kernel's default (dense
                                          segment batches 5, others 0)                               */
-    NETCSUM_TUNE_STREAM_TOUCH  = 12   /* run-stream kernels: row-touch prologue (the first dword of
+    NETCSUM_TUNE_STREAM_TOUCH  = 12,  /* run-stream kernels: row-touch prologue (the first dword of
                                          every 1-KiB piece of a wave's run loaded up front): 1 on,
                                          0 off, -1 each kernel's default (segment batches on, packet
                                          batches off)                                               */
+    NETCSUM_TUNE_STREAM_XCD    = 13   /* dense segment stream kernel: 1 = XCD-aware block order (each
+                                         XCD's blocks take one contiguous 1/8 of the runs), 0 (default)
+                                         the dispatch order                                          */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -29,6 +29,7 @@ def _reset_tuning():
     netcsum.tune(netcsum.TUNE_TILE, -1)
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, 0)
 
 
 @pytest.fixture(autouse=True)
@@ -454,11 +455,13 @@ def test_stream_kernel_full_c2_equals_pipe_kernel():
 
 @pytest.mark.parametrize("touch", [0, 1])
 @pytest.mark.parametrize("waves", [0, 3, 5, 8])
-def test_stream_touch_and_residency_do_not_change_results(touch, waves):
-    """The row-touch prologue and the residency cap (NETCSUM_TUNE_STREAM_TOUCH / _WAVES) are launch
-    options only: dense, gapped and varlen stream batches — runs short and long enough that the touch
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_stream_touch_and_residency_do_not_change_results(touch, waves, xcd):
+    """The row-touch prologue, the residency cap and the XCD-aware block order
+    (NETCSUM_TUNE_STREAM_TOUCH / _WAVES / _XCD) are launch options only: dense, gapped and varlen stream batches — runs short and long enough that the touch
     covers only their first 128 pieces — give the oracle's results under every combination."""
-    rng = np.random.default_rng(100 * waves + touch)
+    rng = np.random.default_rng(100 * waves + touch + 7 * xcd)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)                   # XCD-aware block order: also a launch option
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, waves)
     netcsum.tune(netcsum.TUNE_KERNEL, 6)

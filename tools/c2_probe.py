@@ -27,7 +27,7 @@ def main():
     spws = [int(x) for x in os.environ.get("C2P_SPW", "8,16,32").split(",")]
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
-    n, L = 1 << 20, 1500
+    n, L = int(os.environ.get("C2P_N", 1 << 20)), 1500
     seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
     netcsum.fill(seg, n * L, SEED, 0)
     v = seg[: n * L].view(n, L)          # IPv4/TCP headers: the C2 kernels do not care, Rx needs them
@@ -62,35 +62,38 @@ def main():
         ph4 = torch.zeros(nv * 12, dtype=torch.uint8, device=dev)
         o4 = torch.empty(nv, dtype=torch.int16, device=dev)
         c4 = (lambda: netcsum.batch_varlen(base4, off_d, len_d, ph4, 12, 12, nv, o4, 0, stream=st), tot + nv * 14)
-    variants = [("read_lds", dict(grid=8192, nt=1, probe=1), (-1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16),
-                ("read_reg", dict(grid=8192, nt=1, probe=0), (-1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16)]
+    variants = [("read_lds", dict(grid=8192, nt=1, probe=1), (-1, -1, 0), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16),
+                ("read_reg", dict(grid=8192, nt=1, probe=0), (-1, -1, 0), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16)]
     touches = [int(x) for x in os.environ.get("C2P_TOUCH", "-1").split(",")]
     depths = [int(x) for x in os.environ.get("C2P_D", "0").split(",")]
-    for w, spw, tch, dd in [(w, spw, t, dd) for w in [int(x) for x in os.environ.get("C2P_WAVES", "-1").split(",")]
-                            for spw in spws for t in touches for dd in depths]:
-            sfx = f"_spw{spw}_waves{w}_touch{tch}" + (f"_D{dd}" if dd else "")
+    xcds = [int(x) for x in os.environ.get("C2P_XCD", "0").split(",")]
+    for w, spw, tch, dd, xc in [(w, spw, t, dd, xc) for w in [int(x) for x in os.environ.get("C2P_WAVES", "-1").split(",")]
+                                for spw in spws for t in touches for dd in depths for xc in xcds]:
+            sfx = f"_spw{spw}_waves{w}_touch{tch}" + (f"_D{dd}" if dd else "") + (f"_xcd{xc}" if xc else "")
             if c4 is not None:
-                variants.append(("c4" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch), c4[0], c4[1]))
+                variants.append(("c4" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch, xc), c4[0], c4[1]))
             if "calc_pseudo" in forms:
-                variants.append(("c2_calc_pseudo" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch), c2(True, 0), n * (L + 12 + 2)))
+                variants.append(("c2_calc_pseudo" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch, xc), c2(True, 0), n * (L + 12 + 2)))
             if "calc_nopseudo" in forms:
-                variants.append(("c2_calc_nopseudo" + sfx, dict(kernel=6, tile=spw), (w, tch), c2(False, 0), n * (L + 2)))
+                variants.append(("c2_calc_nopseudo" + sfx, dict(kernel=6, tile=spw), (w, tch, xc), c2(False, 0), n * (L + 2)))
             if "verify_pseudo" in forms:
-                variants.append(("c2_verify_pseudo" + sfx, dict(kernel=6, tile=spw), (w, tch), c2(True, 1), n * (L + 12 + 1)))
+                variants.append(("c2_verify_pseudo" + sfx, dict(kernel=6, tile=spw), (w, tch, xc), c2(True, 1), n * (L + 12 + 1)))
             if "rx" in forms:
-                variants.append(("rx_pkt" + sfx, dict(tile=spw), (w, tch),
+                variants.append(("rx_pkt" + sfx, dict(tile=spw), (w, tch, xc),
                                  lambda: netcsum.rx_validate_ipv4(seg, n, flags, stride=L, pkt_len=L, stream=st), n * (L + 1)))
     res = {}
     for _ in range(rounds):
-        for name, kw, (w, tch), fn, byts in variants:
+        for name, kw, (w, tch, xc), fn, byts in variants:
             set_tune(**kw)
             netcsum.tune(netcsum.TUNE_STREAM_WAVES, w)
             netcsum.tune(netcsum.TUNE_STREAM_TOUCH, tch)
+            netcsum.tune(netcsum.TUNE_STREAM_XCD, xc)
             med, mn = timeit(fn, st, reps=40, warm_s=0.3)
             res.setdefault(name, []).append((med, mn, byts, netcsum.last_launch()))
     set_tune()
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, 0)
     for name, r in res.items():
         med = statistics.median(x[0] for x in r)
         print(json.dumps({"variant": name, "kernel": r[0][3], "ms_med": round(med, 4),

@@ -920,6 +920,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         if (value != -1 && value != 0 && (value < 3 || value > 8)) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_waves(value);
         return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_STREAM_XCD:
+        if (value != 0 && value != 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_stream_xcd(value);
+        return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_STREAM_TOUCH:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_touch(value);

@@ -73,5 +73,13 @@ __device__ __forceinline__ void touch_retire(RunTouch t) {
     asm volatile("" ::"v"(t.a), "v"(t.b));
 }
 
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): blocks the dispatcher
+// places on one XCD (equal blockIdx mod 8) take one contiguous 1/8 of the grid's runs, so each XCD's
+// L2 and address translation see one slice of the batch instead of all of it.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t nwg) {
+    const uint32_t q = nwg >> 3, r = nwg & 7u, xcd = orig & 7u;
+    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (orig >> 3);
+}
+
 }  // namespace sv
 }  // namespace netcsum

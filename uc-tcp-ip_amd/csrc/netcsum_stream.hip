@@ -145,7 +145,8 @@ template <int D, int PH, bool NT, bool ONE>
 __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
     }
@@ -489,6 +490,7 @@ template <int D, int PH, bool NT, bool ONE>
 hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
+    a.xcd = stream_xcd() ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     // dense batches default to 5 waves per SIMD with the row touch: C2 0.2188 ms against 0.2346 ms
@@ -557,6 +559,7 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
 
 std::atomic<int> g_stream_waves{-1};
 std::atomic<int> g_stream_touch{-1};
+std::atomic<int> g_stream_xcd{0};
 }
 
 hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s) {
@@ -580,6 +583,14 @@ uint32_t stream_lds_bytes(int auto_waves) {
 
 void set_stream_touch(int t) {
     g_stream_touch.store(t);
+}
+
+void set_stream_xcd(int on) {
+    g_stream_xcd.store(on);
+}
+
+bool stream_xcd() {
+    return g_stream_xcd.load(std::memory_order_relaxed) != 0;
 }
 
 bool stream_touch(bool auto_on) {

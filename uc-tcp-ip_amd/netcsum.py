@@ -54,6 +54,7 @@ TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
 TUNE_TX_PASSES = 10
 TUNE_STREAM_WAVES = 11
 TUNE_STREAM_TOUCH = 12
+TUNE_STREAM_XCD = 13
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
