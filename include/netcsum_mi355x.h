@@ -446,9 +446,10 @@ typedef enum netcsum_tune_key {
                                          every 1-KiB piece of a wave's run loaded up front): 1 on,
                                          0 off, -1 each kernel's default (segment batches on, packet
                                          batches off)                                               */
-    NETCSUM_TUNE_STREAM_XCD    = 13   /* dense segment stream kernel: 1 = XCD-aware block order (each
-                                         XCD's blocks take one contiguous 1/8 of the runs), 0 (default)
-                                         the dispatch order                                          */
+    NETCSUM_TUNE_STREAM_XCD    = 13   /* segment / varlen / header stream kernels: 1 = XCD-aware block
+                                         order (each XCD's blocks take one contiguous 1/8 of the runs),
+                                         0 = the dispatch order, -1 = each kernel's default (segment
+                                         and varlen batches on, header batches off)                  */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -21,6 +21,8 @@ def _tuning():
         netcsum.tune(netcsum.TUNE_CHUNKS, 0)
         netcsum.tune(netcsum.TUNE_TILE, -1)
         netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
+        netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
+        netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
     reset()
     yield
     reset()
@@ -36,9 +38,12 @@ def _run(host, lead, L, n, op):
 
 
 @pytest.mark.parametrize("L", [20, 16])
-@pytest.mark.parametrize("spw,depth,nt", [(1024, 4, 1), (1, 4, 1), (7, 8, 0), (64, 8, 1), (4096, 4, 0)])
-def test_hdrstream_vs_oracle(L, spw, depth, nt):
+@pytest.mark.parametrize("spw,depth,nt,xcd,touch", [(1024, 4, 1, -1, -1), (1, 4, 1, 1, 0), (7, 8, 0, -1, 1),
+                                                    (64, 8, 1, 1, -1), (4096, 4, 0, 0, 0), (192, 4, 1, 1, 1)])
+def test_hdrstream_vs_oracle(L, spw, depth, nt, xcd, touch):
     netcsum.tune(netcsum.TUNE_KERNEL, 8)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)                   # launch options: block order, row touch
+    netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
     netcsum.tune(netcsum.TUNE_TILE, spw)
     netcsum.tune(netcsum.TUNE_CHUNKS, depth)
     netcsum.tune(netcsum.TUNE_NT_LOADS, nt)

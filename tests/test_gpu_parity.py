@@ -29,7 +29,7 @@ def _reset_tuning():
     netcsum.tune(netcsum.TUNE_TILE, -1)
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
-    netcsum.tune(netcsum.TUNE_STREAM_XCD, 0)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
 
 
 @pytest.fixture(autouse=True)

@@ -62,14 +62,14 @@ def main():
         ph4 = torch.zeros(nv * 12, dtype=torch.uint8, device=dev)
         o4 = torch.empty(nv, dtype=torch.int16, device=dev)
         c4 = (lambda: netcsum.batch_varlen(base4, off_d, len_d, ph4, 12, 12, nv, o4, 0, stream=st), tot + nv * 14)
-    variants = [("read_lds", dict(grid=8192, nt=1, probe=1), (-1, -1, 0), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16),
-                ("read_reg", dict(grid=8192, nt=1, probe=0), (-1, -1, 0), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16)]
+    variants = [("read_lds", dict(grid=8192, nt=1, probe=1), (-1, -1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16),
+                ("read_reg", dict(grid=8192, nt=1, probe=0), (-1, -1, -1), lambda: netcsum.read_stream(seg, n16, sink, stream=st), n16)]
     touches = [int(x) for x in os.environ.get("C2P_TOUCH", "-1").split(",")]
     depths = [int(x) for x in os.environ.get("C2P_D", "0").split(",")]
-    xcds = [int(x) for x in os.environ.get("C2P_XCD", "0").split(",")]
+    xcds = [int(x) for x in os.environ.get("C2P_XCD", "-1").split(",")]
     for w, spw, tch, dd, xc in [(w, spw, t, dd, xc) for w in [int(x) for x in os.environ.get("C2P_WAVES", "-1").split(",")]
                                 for spw in spws for t in touches for dd in depths for xc in xcds]:
-            sfx = f"_spw{spw}_waves{w}_touch{tch}" + (f"_D{dd}" if dd else "") + (f"_xcd{xc}" if xc else "")
+            sfx = f"_spw{spw}_waves{w}_touch{tch}" + (f"_D{dd}" if dd else "") + (f"_xcd{xc}" if xc >= 0 else "")
             if c4 is not None:
                 variants.append(("c4" + sfx, dict(kernel=6, tile=spw, k=dd), (w, tch, xc), c4[0], c4[1]))
             if "calc_pseudo" in forms:
@@ -93,7 +93,7 @@ def main():
     set_tune()
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
-    netcsum.tune(netcsum.TUNE_STREAM_XCD, 0)
+    netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
     for name, r in res.items():
         med = statistics.median(x[0] for x in r)
         print(json.dumps({"variant": name, "kernel": r[0][3], "ms_med": round(med, 4),

@@ -39,7 +39,8 @@ template <int M, int D, bool NT>
 __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
     }
@@ -134,6 +135,7 @@ template <int M, int D, bool NT>
 hipError_t launch_hs_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
+    a.xcd = stream_xcd(false) ? 1u : 0u;   // r2x: 0.0579-0.0584 ms off vs 0.0589 on
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT>), dim3((unsigned)((waves + 3u) / 4u)), dim3(256),
                        stream_lds_bytes(0), s, a, spw);

@@ -20,7 +20,7 @@ struct SegBatchArgs {
     uint32_t        tile;          // 0: grid-stride; J > 0: block b owns segments [b*gpb*J, (b+1)*gpb*J)
     void*           out;
     uint32_t        touch;         // run-stream kernels: row-touch prologue (set by the launcher)
-    uint32_t        xcd;           // seg_stream_kernel: XCD-aware block order (set by the launcher)
+    uint32_t        xcd;           // stream kernels: XCD-aware block order (set by the launcher)
 };
 
 struct LaunchCfg {
@@ -130,9 +130,11 @@ uint32_t stream_lds_bytes(int auto_waves);
 // default `auto_on`, 0 off, 1 on).
 void set_stream_touch(int t);
 bool stream_touch(bool auto_on);
-// XCD-aware block order of the dense segment stream kernel (NETCSUM_TUNE_STREAM_XCD; default off).
+// XCD-aware block order of the segment / varlen / header stream kernels (NETCSUM_TUNE_STREAM_XCD:
+// -1 each kernel's default `auto_on`, 0 off, 1 on). Measured (profiles/r2w_*, r2x_*): C5 shard
+// 3.614 -> 3.561 ms, C2 0.2186 -> 0.2181, C4 0.6777 -> 0.6747 (on); C3 0.0579-0.0584 -> 0.0589 (off).
 void set_stream_xcd(int on);
-bool stream_xcd();
+bool stream_xcd(bool auto_on);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s, uint32_t tag = 0u);   // tag != 0 (grid 1): completion word
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,

@@ -330,7 +330,8 @@ template <int D, int PH, bool NT>
 __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
     }
@@ -480,6 +481,7 @@ hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStrea
     // defaults from r2ct (C4, 1 M packed 40-9000 B): runs of 8, touch, 5 waves per SIMD: 0.680 ms
     // against 0.696 ms for runs of 16 at full residency without the touch
     a.touch = stream_touch(true) ? 1u : 0u;
+    a.xcd = stream_xcd(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256), stream_lds_bytes(5), s, a, spw);
@@ -490,7 +492,7 @@ template <int D, int PH, bool NT, bool ONE>
 hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
-    a.xcd = stream_xcd() ? 1u : 0u;
+    a.xcd = stream_xcd(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     // dense batches default to 5 waves per SIMD with the row touch: C2 0.2188 ms against 0.2346 ms
@@ -559,7 +561,7 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
 
 std::atomic<int> g_stream_waves{-1};
 std::atomic<int> g_stream_touch{-1};
-std::atomic<int> g_stream_xcd{0};
+std::atomic<int> g_stream_xcd{-1};
 }
 
 hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s) {
@@ -589,8 +591,9 @@ void set_stream_xcd(int on) {
     g_stream_xcd.store(on);
 }
 
-bool stream_xcd() {
-    return g_stream_xcd.load(std::memory_order_relaxed) != 0;
+bool stream_xcd(bool auto_on) {
+    const int x = g_stream_xcd.load(std::memory_order_relaxed);
+    return x < 0 ? auto_on : x != 0;
 }
 
 bool stream_touch(bool auto_on) {
