@@ -31,6 +31,7 @@ def _defaults():
         netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
         netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
+        netcsum.tune(netcsum.TUNE_TX_FLUSH, -1)
     reset()
     yield
     reset()
@@ -75,6 +76,22 @@ def _run(buf, n, stride, pkt_len, lead, udp_tx_csum):
     netcsum.tx_finalize_ipv4(b[lead:], n, ft, stride=stride, pkt_len=pkt_len, udp_tx_csum=udp_tx_csum)
     torch.cuda.synchronize()
     return rx, b.cpu().numpy(), ft.cpu().numpy(), rx_desc, netcsum.last_launch()
+
+
+@pytest.mark.parametrize("passes", [1, 2])
+@pytest.mark.parametrize("flush", [0, 1, 2, 3, 4])
+def test_tx_write_back_options_do_not_change_results(passes, flush):
+    """NETCSUM_TUNE_TX_FLUSH (measured, profiles/r2z_tx_flush_sweep.jsonl): write-through scatter
+    stores, a release per scatter wave, or a write-back launch after Tx: the same bytes."""
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    netcsum.tune(netcsum.TUNE_TX_FLUSH, flush)
+    rng = random.Random(97 + flush + 5 * passes)
+    stride, pkt_len, lead, n = 1501, 1500, 1, 900
+    buf = _batch(rng, n, stride, pkt_len, lead)
+    rx_w, tx_w, txf_w = _want(buf, n, stride, pkt_len, lead, True)
+    rx, tx, txf, _, d_tx = _run(buf, n, stride, pkt_len, lead, True)
+    assert d_tx.startswith("pkt_stream_kernel") and (" +pkt_scatter_kernel" in d_tx) == (passes == 2), d_tx
+    assert np.array_equal(rx, rx_w) and np.array_equal(tx, tx_w) and np.array_equal(txf, txf_w)
 
 
 SHAPES = [(1500, 1500), (1514, 1514), (1540, 1514), (1501, 1500), (64, 64), (100, 64), (577, 577), (9000, 9000),

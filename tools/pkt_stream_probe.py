@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Rx / Tx packet-batch timing on 1 M x 1500-B IPv4/TCP datagrams (strided, in place):
 the lane-group kernel (TUNE_KERNEL 2, tile 2) against the run-stream kernel over packets per wave
-(TUNE_TILE), load policy (TUNE_NT_LOADS) and pieces in flight (TUNE_CHUNKS 4 / 8). Tx restores
+(TUNE_TILE), load policy (TUNE_NT_LOADS), pieces in flight (TUNE_CHUNKS 4 / 8) and the write-back
+of the Tx field lines (TUNE_TX_FLUSH, env PS_FLUSH). Tx restores
 nothing between launches: its written fields are the same every time. Prints JSON lines."""
 import json
 import os
@@ -35,9 +36,11 @@ def main():
         for nt in [int(x) for x in os.environ.get("PS_NT", "1,0").split(",")]:
             for d in [int(x) for x in os.environ.get("PS_D", "4,8").split(",")]:
                 for passes in [int(x) for x in os.environ.get("PS_PASSES", "1,2").split(",")]:
-                    variants.append(dict(kernel=0, tile=spw, nt=nt, chunks=d, passes=passes))
+                    for fl in [int(x) for x in os.environ.get("PS_FLUSH", "-1").split(",")]:
+                        variants.append(dict(kernel=0, tile=spw, nt=nt, chunks=d, passes=passes, flush=fl))
     for var in variants:
         netcsum.tune(netcsum.TUNE_TX_PASSES, var["passes"])
+        netcsum.tune(netcsum.TUNE_TX_FLUSH, var.get("flush", -1))
         netcsum.tune(netcsum.TUNE_KERNEL, var["kernel"])
         netcsum.tune(netcsum.TUNE_TILE, var["tile"])
         netcsum.tune(netcsum.TUNE_NT_LOADS, var["nt"])

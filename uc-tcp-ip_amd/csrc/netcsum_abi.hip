@@ -924,6 +924,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_xcd(value);
         return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_TX_FLUSH:
+        if (value < -1 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_tx_flush(value);
+        return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_STREAM_TOUCH:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_touch(value);

@@ -112,6 +112,10 @@ int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
+// Tx finalize write-back of the dirty field lines (NETCSUM_TUNE_TX_FLUSH): -1 / 0 none, 1 scatter
+// stores at system scope, 2 release at the end of every scatter wave, 3 / 4 a write-back launch of
+// 8 / 256 workgroups after the Tx launch(es).
+void set_tx_flush(int mode);
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx,
                              hipStream_t s, PktTxRecord* rec = nullptr);   // rec: two-pass Tx (records + scatter)
 void set_last_launch(const char* desc);

@@ -36,6 +36,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "../../include/netcsum_mi355x.h"
 #include "netcsum_device.h"
@@ -555,24 +556,78 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 }
 
 // Second pass of the two-pass Tx: one thread per packet writes its fields (and flags) from its record.
+// WT (NETCSUM_TUNE_TX_FLUSH 1): the field bytes are stored at system scope, i.e. written through the
+// L2 to HBM during this pass instead of sitting dirty in the L2 until a later launch evicts them.
+// WB (TX_FLUSH 2): every wave ends with an agent-scope release (the L2 write-back of its XCD).
+template <bool WT, bool WB>
 __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const PktTxRecord* rec) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= A.n) {
-        return;
+    if (i < A.n) {
+        const uint64_t r = reinterpret_cast<const uint64_t*>(rec)[i];      // PktTxRecord, one 8-B load
+        const uint32_t vals = (uint32_t)r, l4_off = (uint32_t)(r >> 32) & 0xFFFFu;
+        const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
+        if (A.flags_out) {
+            A.flags_out[i] = (uint8_t)flags;
+        }
+        uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
+        if constexpr (WT) {
+            if (store & 1u) {
+                __hip_atomic_store(p + 10, (uint8_t)(vals & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(p + 11, (uint8_t)((vals >> 8) & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (store & 2u) {
+                __hip_atomic_store(p + l4_off, (uint8_t)((vals >> 16) & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(p + l4_off + 1u, (uint8_t)(vals >> 24), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            if (store & 1u) {
+                store_field(p + 10, vals & 0xFFFFu);
+            }
+            if (store & 2u) {
+                store_field(p + l4_off, vals >> 16);
+            }
+        }
     }
-    const uint64_t r = reinterpret_cast<const uint64_t*>(rec)[i];      // PktTxRecord, one 8-B load
-    const uint32_t vals = (uint32_t)r, l4_off = (uint32_t)(r >> 32) & 0xFFFFu;
-    const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
-    if (A.flags_out) {
-        A.flags_out[i] = (uint8_t)flags;
+    if constexpr (WB) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the wave ends when its write-back has
     }
-    uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
-    if (store & 1u) {
-        store_field(p + 10, vals & 0xFFFFu);
+}
+
+// TX_FLUSH 3 / 4: a separate launch of 8 / 256 one-wave workgroups, each an agent-scope release,
+// after the Tx launch(es): the dirty field lines are written back before the next launch's reads.
+__global__ void __launch_bounds__(64) l2_writeback_kernel() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+std::atomic<int> g_tx_flush{-1};
+
+int tx_flush_mode() {
+    const int m = g_tx_flush.load(std::memory_order_relaxed);
+    return m < 0 ? 0 : m;
+}
+
+hipError_t launch_scatter(const PktBatchArgs& a, const PktTxRecord* rec, hipStream_t s) {
+    const int m = tx_flush_mode();
+    const dim3 g((a.n + 255u) / 256u), b(256);
+    if (m == 1) {
+        hipLaunchKernelGGL((pkt_scatter_kernel<true, false>), g, b, 0, s, a, rec);
+    } else if (m == 2) {
+        hipLaunchKernelGGL((pkt_scatter_kernel<false, true>), g, b, 0, s, a, rec);
+    } else {
+        hipLaunchKernelGGL((pkt_scatter_kernel<false, false>), g, b, 0, s, a, rec);
     }
-    if (store & 2u) {
-        store_field(p + l4_off, vals >> 16);
+    return hipGetLastError();
+}
+
+hipError_t launch_tx_flush(hipStream_t s) {
+    const int m = tx_flush_mode();
+    if (m == 3 || m == 4) {
+        hipLaunchKernelGGL(l2_writeback_kernel, dim3(m == 3 ? 8 : 256), dim3(64), 0, s);
+        return hipGetLastError();
     }
+    return hipSuccess;
 }
 
 template <int D, bool NT, bool TX, int VER>
@@ -587,14 +642,19 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(pkt_scatter_kernel, dim3((a.n + 255u) / 256u), dim3(256), 0, s, a, (const PktTxRecord*)rec);
-        return hipGetLastError();
+        e = launch_scatter(a, rec, s);
+        return e != hipSuccess ? e : launch_tx_flush(s);
     }
     hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }
 
 }  // namespace
+
+void set_tx_flush(int mode) {
+    g_tx_flush.store(mode);
+}
 
 // Strided batches of >= 64-B packets (IPv4, IPv6 or mixed), dense (gap <= 64 B), whose runs span
 // < 2^31 bytes.

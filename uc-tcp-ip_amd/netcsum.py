@@ -55,6 +55,7 @@ TUNE_TX_PASSES = 10
 TUNE_STREAM_WAVES = 11
 TUNE_STREAM_TOUCH = 12
 TUNE_STREAM_XCD = 13
+TUNE_TX_FLUSH = 14
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
