@@ -4,6 +4,7 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   c2  1 M x 1500 B + 12-B pseudo, DataCalc       c3  16 M x 20-B IPv4 headers, HdrCalc
   c4  1 M packed UDP 40-9000 B + pseudo          c5  16 M x 1500 B + pseudo (one GPU's shard)
   rx / tx  fused Rx / Tx finalize, 1 M x 1500-B IPv4/TCP, strided; tx2 = two-pass Tx
+  rx6 / rxmix  fused Rx of the same datagrams as IPv6/TCP / alternating IPv4 and IPv6 (bench_configs)
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
 import os
 import sys
@@ -62,7 +63,19 @@ def main():
         flags = torch.zeros(n, dtype=torch.uint8, device=dev)
         if name == "tx2":
             netcsum.tune(netcsum.TUNE_TX_PASSES, 2)
-        if name == "rx":
+        if name in ("rx6", "rxmix"):
+            v[:, 0:8] = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8,
+                                     device=dev)
+            if name == "rxmix":
+                v[0::2, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0],
+                                             dtype=torch.uint8, device=dev)
+                v[0::2, 12:20] = 0x0A
+            netcsum.tx_finalize_ip(pk, n, flags, stride=L, pkt_len=L, stream=st)
+            fn = lambda: netcsum.rx_validate_ip(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
+            if name == "rx6":
+                fn = lambda: netcsum.rx_validate_ipv6(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
+            algo = n * (L + 1)
+        elif name == "rx":
             fn = lambda: netcsum.rx_validate_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
             algo = n * (L + 1)
         else:

@@ -739,9 +739,12 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     const int kern = g_tune_kernel.load();
     // Defaults from the r2tx sweep (tools/pkt_stream_probe.py, 1 M x 1500-B IPv4/TCP): runs of 8
     // packets, 4 pieces in flight, nt loads (Rx 0.215 ms); Tx in two passes (checksum pass writing
-    // 8-B records + scatter pass: 0.288 ms against 0.296 for in-pass field writes).
+    // 8-B records + scatter pass: 0.288 ms against 0.296 for in-pass field writes). Mixed rings run
+    // both parses in a wave whose lanes disagree on the version, and a run of 16 spreads that over
+    // twice the bytes (profiles/r2zb_pkt_stream_mixed_v6_v4.jsonl, alternating ring: Rx 0.243 ->
+    // 0.2185 ms, Tx 0.302 -> 0.292); IPv4 and IPv6 alone stay at 8 (16: +0.9 % / +0.2 %).
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
-        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : 8u;
+        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : (ip_ver == 0 ? 16u : 8u);
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
         const bool two = tx && g_tune_tx_passes.load() != 1;
