@@ -450,11 +450,16 @@ typedef enum netcsum_tune_key {
                                          order (each XCD's blocks take one contiguous 1/8 of the runs),
                                          0 = the dispatch order, -1 = each kernel's default (segment
                                          and varlen batches on, header batches off)                  */
-    NETCSUM_TUNE_TX_FLUSH      = 14   /* run-stream Tx finalize, write-back of the dirty checksum-field
+    NETCSUM_TUNE_TX_FLUSH      = 14,  /* run-stream Tx finalize, write-back of the dirty checksum-field
                                          lines: -1 / 0 none (they are evicted during later launches),
                                          1 scatter stores written through at system scope, 2 an L2
                                          release at the end of every scatter wave, 3 / 4 a write-back
                                          launch of 8 / 256 workgroups after the Tx launch(es)         */
+    NETCSUM_TUNE_CRC_KERNEL    = 15,  /* CRC-32 batches of segments > 256 B (and every varlen batch):
+                                         0 auto (2), 1 block combine (GF(2) multiplications by bit
+                                         loops, the round-2 form), 2 interleaved 16-B chunks with
+                                         table-driven shifts                                          */
+    NETCSUM_TUNE_CRC_NT        = 16   /* CRC-32 interleaved form: 1 non-temporal chunk loads, 0 plain */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

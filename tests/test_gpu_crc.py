@@ -1,6 +1,7 @@
 """GPU parity of the CRC-32 path (net_util.c:485-636): the drop-in NetUtil_32BitCRC_Calc / _CalcCpl
 on host buffers, the drivers' multicast hash built on them, and the strided / varlen batch kernels
-(one lane per short segment; 16-lane groups combining equal blocks by GF(2) shifts for long ones),
+(one lane per short segment; for long ones 16-lane groups over interleaved 16-B chunks with table-driven
+shifts, the default, or over equal blocks combined by GF(2) multiplications, NETCSUM_TUNE_CRC_KERNEL 1),
 against the C restatement (pinned to the CRC-32 check value and zlib in tests/test_crc_cpu.py).
 Full size: the Ethernet residue property — a segment followed by its little-endian CalcCpl value
 has CalcCpl 0x2144DF1C — over every segment of a 1 M x 1500-B batch."""
@@ -50,16 +51,31 @@ def test_dropin_multicast_hash_like_the_drivers():
         assert (netcsum.Reflect32(crc) >> 26) & 0x3F == (oracle.reflect32(want) >> 26) & 0x3F
 
 
+FORMS = [(0, 0), (1, 0), (2, 1)]        # (NETCSUM_TUNE_CRC_KERNEL, NETCSUM_TUNE_CRC_NT)
+LONG_NAME = {0: "crc_ilv_kernel", 1: "crc_group_kernel", 2: "crc_ilv_kernel<nt>"}
+
+
+@pytest.fixture(params=FORMS, ids=lambda f: f"form{f[0]}nt{f[1]}")
+def crc_form(request):
+    kern, nt = request.param
+    netcsum.tune(netcsum.TUNE_CRC_KERNEL, kern)
+    netcsum.tune(netcsum.TUNE_CRC_NT, nt)
+    yield kern
+    netcsum.tune(netcsum.TUNE_CRC_KERNEL, 0)
+    netcsum.tune(netcsum.TUNE_CRC_NT, 0)
+
+
 STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (255, 256), (256, 256), (257, 300),
-           (1500, 1500), (1514, 1518), (4096, 4100), (9000, 9001)]
+           (1500, 1500), (1514, 1518), (4096, 4100), (9000, 9001), (2048, 2048), (2049, 2050), (4111, 4111),
+           (65535, 65536)]
 
 
 @pytest.mark.parametrize("length,stride", STRIDED)
 @pytest.mark.parametrize("cpl", [0, 1])
-def test_crc_batch_strided_vs_oracle(length, stride, cpl):
+def test_crc_batch_strided_vs_oracle(length, stride, cpl, crc_form):
     rng = np.random.default_rng(length * 3 + stride + cpl)
-    n = 1000 if length <= 1514 else 200
-    for base_off in (0, 1, 2, 7):
+    n = 1000 if length <= 1514 else 200 if length <= 9001 else 24
+    for base_off in (0, 1, 2, 7, 13, 15):
         data = rng.integers(0, 256, size=base_off + n * stride + 64, dtype=np.uint8)
         d = torch.from_numpy(data).to(DEV)
         out = torch.zeros(n, dtype=torch.int32, device=DEV)
@@ -70,11 +86,11 @@ def test_crc_batch_strided_vs_oracle(length, stride, cpl):
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (base_off, [(int(i), hex(got[i]), hex(want[i])) for i in bad[:4]])
         kern = netcsum.last_launch()
-        assert kern.startswith("crc_lane_kernel" if length <= 256 else "crc_group_kernel"), kern
+        assert kern.startswith("crc_lane_kernel" if length <= 256 else LONG_NAME[crc_form] + " "), kern
 
 
 @pytest.mark.parametrize("cpl", [0, 1])
-def test_crc_batch_varlen_vs_oracle(cpl):
+def test_crc_batch_varlen_vs_oracle(cpl, crc_form):
     """Packed segments of 0..20000 B at every alignment, reversed and overlapping layouts."""
     rng = np.random.default_rng(40 + cpl)
     n = 3000
@@ -114,7 +130,7 @@ def test_crc_full_size_residue_1M():
     fcs = torch.zeros(n, dtype=torch.int32, device=DEV)
     netcsum.crc32_strided(buf, S, L, n, fcs, 1)
     torch.cuda.synchronize()
-    assert netcsum.last_launch().startswith("crc_group_kernel")
+    assert netcsum.last_launch().startswith("crc_ilv_kernel ")
     smp = np.sort(np.random.default_rng(9).choice(n, size=4096, replace=False))
     rows = buf[: n * S].view(n, S)[torch.from_numpy(smp).to(DEV)].cpu().numpy()
     want = oracle.crc32_batch(rows.reshape(-1).copy(), len(smp), True, stride=S, length=L)
@@ -131,3 +147,21 @@ def test_crc_full_size_residue_1M():
     torch.cuda.synchronize()
     wrong = torch.nonzero(res != RESIDUE).flatten()
     assert torch.equal(wrong, bad)
+
+
+def test_crc_varlen_every_length_and_alignment(crc_form):
+    """Every length 0..700 at every start alignment mod 16 (the interleaved form's head chunk, front
+    padding and tail cases; lengths < 32 take the group's sequential path)."""
+    lens = np.repeat(np.arange(0, 701, dtype=np.uint32), 16)
+    n = len(lens)
+    off = (np.arange(n, dtype=np.uint64) * 768 + np.tile(np.arange(16, dtype=np.uint64), 701)).astype(np.uint64)
+    data = np.random.default_rng(77).integers(0, 256, size=n * 768 + 64, dtype=np.uint8)
+    d = torch.from_numpy(data).to(DEV)
+    out = torch.zeros(n, dtype=torch.int32, device=DEV)
+    netcsum.crc32_varlen(d, torch.from_numpy(off.view(np.int64)).to(DEV), torch.from_numpy(lens.view(np.int32)).to(DEV),
+                         n, out, 1)
+    torch.cuda.synchronize()
+    want = oracle.crc32_batch(data, n, True, off=off, lens=lens)
+    got = out.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(off[i] % 16), hex(got[i]), hex(want[i])) for i in bad[:6]]

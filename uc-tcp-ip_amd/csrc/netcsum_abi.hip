@@ -645,7 +645,7 @@ NET_ERR NetUtil_MI355X_CRC32BatchStrided(const void* d_base, uint64_t stride, ui
     a.n = n;
     a.cpl = cpl ? 1u : 0u;
     a.out = d_out;
-    netcsum::set_last_launch(len <= netcsum::kCrcShortMax ? "crc_lane_kernel block=256" : "crc_group_kernel G=16 block=256");
+    netcsum::set_last_launch(netcsum::crc_launch_name(len));
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
     NC_HIP(netcsum::launch_crc_batch(a, len, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
@@ -663,7 +663,7 @@ NET_ERR NetUtil_MI355X_CRC32BatchVarLen(const void* d_base, const uint64_t* d_of
     a.n = n;
     a.cpl = cpl ? 1u : 0u;
     a.out = d_out;
-    netcsum::set_last_launch("crc_group_kernel G=16 block=256");
+    netcsum::set_last_launch(netcsum::crc_launch_name(0xFFFFFFFFu));
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
     NC_HIP(netcsum::launch_crc_batch(a, 0xFFFFFFFFu, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
@@ -934,6 +934,14 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_STREAM_TOUCH:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_touch(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CRC_KERNEL:
+        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_crc_kernel(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CRC_NT:
+        if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_crc_nt(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:
         if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)

@@ -5,22 +5,39 @@
 // The reference's callers hash 6-byte multicast MAC addresses (Dev/Ether/*/net_dev_*.c,
 // AddrMulticastAdd / Remove); the batch form here takes any number of segments of any length.
 //
-// Arithmetic. The register update is linear over GF(2): processing message M from state I gives
-// A^|M|(I) xor raw(M), where raw() is the CRC from state 0 and A^n multiplies by x^(8n) modulo the
-// polynomial. So
-//   * a segment splits into G equal blocks of s bytes (s a multiple of 4) after a front pad of
-//     P = G*s - L zero octets — leading zeros leave raw() unchanged — and lane j of a G-lane group
-//     computes raw(block j) with 4-KiB slicing-by-4 tables in LDS;
-//   * the group combines the blocks in log2(G) shuffle levels, level k merging pairs at distance
-//     2^k with the fixed multiplier x^(8 s 2^k) (squared from level to level);
-//   * the initial 0xFFFFFFFF contributes x^(8L) * 0xFFFFFFFF, added once per segment.
-// Powers x^(8n) come from the 32 squares x^(2^k) (kX2n) by square-and-multiply, as in zlib's
-// crc32_combine. Segments up to kShortMax bytes take one lane each (G = 1: register from
-// 0xFFFFFFFF, no combine).
+// Arithmetic. The register update is linear over GF(2). Write A^n for "advance the register over n
+// zero octets" (a linear map: multiplication by x^(8n) modulo the polynomial). Processing octets M
+// from state I gives A^|M|(I) xor raw(M), raw() = the CRC from state 0, and raw() of leading zero
+// octets is 0. Any linear map of the 32-bit register is four 256-entry tables, one per register
+// octet: A^n(c) = S[0][c & 0xFF] ^ S[1][(c >> 8) & 0xFF] ^ S[2][(c >> 16) & 0xFF] ^ S[3][c >> 24]
+// with S[k][b] = A^n(b << 8k). The four octets of a little-endian dword w enter the register
+// together: c <- A^4(c ^ w) (slicing-by-4; T = the tables of A^4, T[3] = the byte table of the
+// reference's bit loop).
+//
+// Interleaved chunks (crc_ilv_kernel, segments of 32 B and more). A 16-lane group owns a segment.
+// The segment's bytes from the 16-B line at or below its start up to the last 16-B boundary at or
+// below its end are 16-B chunks, front-padded with zero chunks to 16 M chunks; lane l takes chunks
+// l, l + 16, l + 32, ... The lane's register runs over its chunk's first three dwords with T and
+// over the fourth with Z = A^240 o A^4, i.e. it is carried past the 15 chunks the other lanes own,
+// so that it stands at the start of the lane's next chunk; the last chunk uses T, which leaves lane
+// l at the end of chunk l + 16 (M - 1). Four shuffle levels then merge pairs of lanes 16, 32, 64 and
+// 128 B apart (tables of A^16 .. A^128), giving raw() of the chunk area in lane 15, which finishes
+// the < 16 trailing octets alone. Every global load is a whole aligned 16-B chunk, a group's load
+// instruction reads 256 contiguous bytes, and every step of every lane is four independent table
+// lookups in LDS: no GF(2) multiplications at run time. The bytes of the first line below the
+// segment start are masked to zero, and the reference's initial register 0xFFFFFFFF enters as an
+// xor into the segment's first four octets (for a message of at least 4 octets, the initial register
+// and an xor of its first four octets are the same thing).
+//
+// Block combine (crc_group_kernel, the round-2 form, kept as NETCSUM_TUNE_CRC_KERNEL 1): lane j of
+// a 16-lane group runs over block j of the segment's equal blocks (byte-aligned, v_alignbyte_b32
+// windows) and the group merges the blocks by GF(2) multiplications with x^(8 s 2^k) computed by a
+// 32-step bit loop. Short segments (<= kCrcShortMax, strided) take one lane each (crc_lane_kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
@@ -31,64 +48,92 @@ namespace {
 
 constexpr uint32_t kPoly = 0xEDB88320u;
 
-// x^(2^k) mod P, reflected (bit 31 = x^0); kX2n[0] = x.
-__constant__ uint32_t kX2n[32] = {
-    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0xEDB88320u, 0xB1E6B092u, 0xA06A2517u,
-    0xED627DAEu, 0x88D14467u, 0xD7BBFE6Au, 0xEC447F11u, 0x8E7EA170u, 0x6427800Eu, 0x4D47BAE0u, 0x09FE548Fu,
-    0x83852D0Fu, 0x30362F1Au, 0x7B5A9CC3u, 0x31FEC169u, 0x9FEC022Au, 0x6C8DEDC4u, 0x15D6874Du, 0x5FDE7A4Eu,
-    0xBAD90E37u, 0x2E4E5EEFu, 0x4EABA214u, 0xA8A472C0u, 0x429A969Eu, 0x148D302Au, 0xC40BA6D0u, 0xC4E22C3Cu};
+// ---- compile-time tables -----------------------------------------------------------------------
+// Table sets of the linear maps used by the kernels, S[k][b] = A^n(b << 8k):
+enum : int { kSetT = 0, kSetZ = 1, kSet16 = 2, kSet32 = 3, kSet64 = 4, kSet128 = 5, kNumSets = 6 };
 
-// a * b mod P (reflected), fixed trip count (no divergence across the group).
-__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
-    uint32_t p = 0u;
-#pragma unroll 4
-    for (int i = 31; i >= 0; --i) {
-        p ^= ((a >> i) & 1u) ? b : 0u;
-        b = (b & 1u) ? ((b >> 1) ^ kPoly) : (b >> 1);
-    }
-    return p;
-}
+struct CrcTabs {
+    uint32_t s[kNumSets][4][256];
+};
 
-// x^(8 n) mod P.
-__device__ __forceinline__ uint32_t x8n(uint32_t n) {
-    uint32_t p = 0x80000000u;                                   // x^0
-    for (int k = 3; n != 0u; n >>= 1, ++k) {
-        if (n & 1u) {
-            p = multmodp(kX2n[k & 31], p);
-        }
-    }
-    return p;
-}
-
-struct CrcTables {
+struct Set {
     uint32_t t[4][256];
 };
 
-// T0 = the byte table of net_util.c:512-521's bit loop; T1..T3 = slicing-by-4 tables.
-__device__ __forceinline__ void build_tables(CrcTables& T) {
-    const uint32_t i = threadIdx.x;                             // blockDim.x == 256
-    uint32_t c = i;
-#pragma unroll
+constexpr uint32_t zero_octet(uint32_t c) {                     // A^1 by the reference's bit loop
     for (int j = 0; j < 8; ++j) {
         c = (c & 1u) ? ((c >> 1) ^ kPoly) : (c >> 1);
     }
-    T.t[0][i] = c;
-    __syncthreads();
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-        const uint32_t v = T.t[k - 1][i];
-        T.t[k][i] = (v >> 8) ^ T.t[0][v & 0xFFu];
-        __syncthreads();
+    return c;
+}
+
+constexpr uint32_t apply_set(const Set& S, uint32_t c) {
+    return S.t[0][c & 0xFFu] ^ S.t[1][(c >> 8) & 0xFFu] ^ S.t[2][(c >> 16) & 0xFFu] ^ S.t[3][c >> 24];
+}
+
+constexpr Set compose(const Set& outer, const Set& inner) {    // tables of outer o inner
+    Set r{};
+    for (int k = 0; k < 4; ++k) {
+        for (int b = 0; b < 256; ++b) {
+            r.t[k][b] = apply_set(outer, inner.t[k][b]);
+        }
     }
+    return r;
 }
 
-__device__ __forceinline__ uint32_t crc_byte(const CrcTables& T, uint32_t c, uint32_t b) {
-    return T.t[0][(c ^ b) & 0xFFu] ^ (c >> 8);
+constexpr CrcTabs make_tabs() {
+    Set t4{};
+    for (int k = 0; k < 4; ++k) {
+        for (uint32_t b = 0; b < 256u; ++b) {
+            uint32_t c = b << (8 * k);
+            for (int j = 0; j < 4; ++j) {
+                c = zero_octet(c);
+            }
+            t4.t[k][b] = c;
+        }
+    }
+    const Set t8 = compose(t4, t4);
+    const Set t16 = compose(t8, t8);
+    const Set t32 = compose(t16, t16);
+    const Set t64 = compose(t32, t32);
+    const Set t128 = compose(t64, t64);
+    const Set z = compose(t128, compose(t64, compose(t32, compose(t16, t4))));   // A^(4 + 240)
+    const Set* sets[kNumSets] = {&t4, &z, &t16, &t32, &t64, &t128};
+    CrcTabs r{};
+    for (int s = 0; s < kNumSets; ++s) {
+        for (int k = 0; k < 4; ++k) {
+            for (int b = 0; b < 256; ++b) {
+                r.s[s][k][b] = sets[s]->t[k][b];
+            }
+        }
+    }
+    return r;
 }
 
-__device__ __forceinline__ uint32_t crc_word(const CrcTables& T, uint32_t c, uint32_t w) {   // 4 octets, LE
-    c ^= w;
-    return T.t[3][c & 0xFFu] ^ T.t[2][(c >> 8) & 0xFFu] ^ T.t[1][(c >> 16) & 0xFFu] ^ T.t[0][c >> 24];
+__device__ const CrcTabs kTabs = make_tabs();
+static_assert(make_tabs().s[kSetT][3][1] == 0x77073096u, "byte table of the reflected IEEE polynomial");
+static_assert(make_tabs().s[kSetT][3][255] == 0x2D02EF8Du, "byte table of the reflected IEEE polynomial");
+
+// Copy the first `nsets` table sets into LDS (blockDim.x == 256, one uint4 per thread per KiB).
+__device__ __forceinline__ void load_sets(uint32_t (*L)[4][256], int nsets) {
+    const uint4* src = reinterpret_cast<const uint4*>(&kTabs.s[0][0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&L[0][0][0]);
+    for (int i = (int)threadIdx.x; i < nsets * 256; i += 256) {
+        dst[i] = src[i];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t apply(const uint32_t (*S)[256], uint32_t c) {
+    return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_word(const uint32_t (*T)[256], uint32_t c, uint32_t w) {   // 4 octets, LE
+    return apply(T, c ^ w);
+}
+
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t (*T)[256], uint32_t c, uint32_t b) {
+    return T[3][(c ^ b) & 0xFFu] ^ (c >> 8);
 }
 
 __device__ __forceinline__ uint32_t ovr(uint32_t x) {          // opaque register value (see below)
@@ -108,7 +153,8 @@ __device__ __forceinline__ uint32_t win16_dword(const uint4& a, const uint4& b, 
     return __builtin_amdgcn_alignbyte(hi, lo, sh & 3u);
 }
 
-__device__ __forceinline__ uint32_t crc_16(const CrcTables& T, uint32_t c, const uint4& a, const uint4& b, uint32_t sh) {
+__device__ __forceinline__ uint32_t crc_16(const uint32_t (*T)[256], uint32_t c, const uint4& a, const uint4& b,
+                                           uint32_t sh) {
     c = crc_word(T, c, win16_dword(a, b, sh, 0));
     c = crc_word(T, c, win16_dword(a, b, sh, 1));
     c = crc_word(T, c, win16_dword(a, b, sh, 2));
@@ -120,7 +166,7 @@ __device__ __forceinline__ uint32_t crc_16(const CrcTables& T, uint32_t c, const
 // step from five loads issued together, the stream's dwords cut out by v_alignbyte_b32; the last
 // n mod 4 octets one at a time. (A per-byte head loop with a load per octet made the lanes wait on
 // one dependent load after another: 1.75 ms for 1 M x 1500 B.)
-__device__ uint32_t crc_range(const CrcTables& T, uint32_t c, const uint8_t* p, uint32_t n) {
+__device__ uint32_t crc_range(const uint32_t (*T)[256], uint32_t c, const uint8_t* p, uint32_t n) {
     const uintptr_t a = (uintptr_t)p;
     const uint32_t sh = (uint32_t)(a & 15u);
     const uint4* q = reinterpret_cast<const uint4*>(a - sh);
@@ -156,24 +202,193 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t c, uint32_t len, bool cp
 }
 
 // One lane per segment (short segments, e.g. 6-B MAC addresses). Persistent blocks: the tables are
-// built once per block, which then walks its share of the batch 256 segments at a time.
+// copied once per block, which then walks its share of the batch 256 segments at a time.
 __global__ void __launch_bounds__(256) crc_lane_kernel(CrcBatchArgs A) {
-    __shared__ CrcTables T;
-    build_tables(T);
+    __shared__ uint32_t L[1][4][256];
+    load_sets(L, 1);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < A.n; i += gridDim.x * 256u) {
         const uint8_t* p;
         uint32_t len;
         seg_desc(A, i, p, len);
-        A.out[i] = crc_finish(crc_range(T, 0xFFFFFFFFu, p, len), len, A.cpl != 0u);
+        A.out[i] = crc_finish(crc_range(L[kSetT], 0xFFFFFFFFu, p, len), len, A.cpl != 0u);
     }
 }
 
-// A 16-lane group per segment (4 segments per wave, 16 per block and step), persistent blocks.
-constexpr int kG = 16;
+constexpr int kG = 16;                  // lanes per segment (both long-segment kernels)
 
+// ---- interleaved chunks ------------------------------------------------------------------------
+// The masks that make the segment's head chunk q (0 or 1; its other chunks are not touched) enter
+// the CRC as the reference sees it: the bytes below the segment start zeroed (q == 0), the initial
+// register xored into the segment's first 4 octets (chunk-relative offsets [lead - 16 q, + 4)).
+struct HeadMask {
+    uint32_t keep[4];
+    uint32_t flip[4];
+};
+
+__device__ __forceinline__ HeadMask head_mask(int q, int lead) {
+    HeadMask h;
+    const int s = lead - 16 * q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h.keep[j] = q == 0 ? dword_mask(lead, 16, 4 * j) : 0xFFFFFFFFu;
+        h.flip[j] = (q == 0 || q == 1) ? dword_mask(s, s + 4, 4 * j) : 0u;
+    }
+    return h;
+}
+
+__device__ __forceinline__ u32x4 apply_head(u32x4 v, const HeadMask& h) {
+    v.x = (v.x & h.keep[0]) ^ h.flip[0];
+    v.y = (v.y & h.keep[1]) ^ h.flip[1];
+    v.z = (v.z & h.keep[2]) ^ h.flip[2];
+    v.w = (v.w & h.keep[3]) ^ h.flip[3];
+    return v;
+}
+
+// The register advanced over the r < 16 octets of the aligned chunk v (the segment's tail).
+__device__ __forceinline__ uint32_t crc_tail(const uint32_t (*T)[256], uint32_t c, u32x4 v, uint32_t r) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = 4u * (uint32_t)j;
+        if (lo + 4u <= r) {
+            c = crc_word(T, c, w[j]);
+        } else if (lo < r) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                if (lo + (uint32_t)b < r) {
+                    c = crc_byte(T, c, (w[j] >> (8 * b)) & 0xFFu);
+                }
+            }
+        }
+    }
+    return c;
+}
+
+constexpr int kRound = 4;               // chunks per lane per round (one round prefetched)
+
+template <bool NT>
+__global__ void __launch_bounds__(256) crc_ilv_kernel(CrcBatchArgs A) {
+    __shared__ uint32_t L[kNumSets][4][256];                    // 24 KiB
+    load_sets(L, kNumSets);
+    const uint32_t lane = threadIdx.x & (kG - 1);
+    const uint32_t steps = (A.n + (256u / kG) - 1u) / (256u / kG);
+    // rounds per segment: wave-uniform for strided batches (bound from the common length)
+    const int r_strided = (int)(((A.len + 15u) / 16u + kG * kRound - 1u) / (kG * kRound));
+    for (uint32_t st = blockIdx.x; st < steps; st += gridDim.x) {          // block-uniform trip count
+        const uint32_t i = st * (256u / kG) + threadIdx.x / kG;
+        const uint8_t* p = A.base;
+        uint32_t len = 0u;
+        if (i < A.n) {
+            seg_desc(A, i, p, len);
+        }
+        uint32_t c;
+        if (len >= 32u) {                                                   // group-uniform
+            const uintptr_t a = (uintptr_t)p;
+            const uintptr_t fs = a & ~(uintptr_t)15u;
+            const uintptr_t e = a + len;
+            const uintptr_t ce = e & ~(uintptr_t)15u;
+            const uint32_t r = (uint32_t)(e - ce);                          // tail octets, < 16
+            const int kc = (int)((ce - fs) >> 4);                           // whole chunks, >= 2
+            const int m_n = (kc + kG - 1) / kG;                             // chunks per lane
+            const int pad = m_n * kG - kc;
+            const int lead = (int)(a - fs);
+            const int rounds = A.lens ? (m_n + kRound - 1) / kRound : r_strided;
+            // Chunk m of this lane is q = lane + 16 m - pad. A missing one (q < 0: the zero chunks in
+            // front, whose register stays 0; m >= m_n: past the lane's last chunk) is loaded from the
+            // first chunk (always present) and its steps are discarded by a select on the register,
+            // never on the loaded value (a select on it would pull the prefetch's wait forward).
+            const int q0 = (int)lane - pad;
+            auto fetch = [&](int m) -> u32x4 {
+                const int q = q0 + kG * m;
+                const bool ok = q >= 0 && m < m_n;
+                return load16<NT>(reinterpret_cast<gu32x4*>(fs + (ok ? 16u * (uint32_t)q : 0u)));
+            };
+            u32x4 cur[kRound];
+#pragma unroll
+            for (int j = 0; j < kRound; ++j) {
+                cur[j] = fetch(j);
+            }
+            const u32x4 tail = load16<NT>(reinterpret_cast<gu32x4*>(r != 0u ? ce : fs));
+            const int mh = q0 >= -1 ? 0 : 1;                                // the lane's chunk holding q 0 or 1
+            const HeadMask hm = head_mask(q0 + kG * mh, lead);
+            c = 0u;
+            for (int rd = 0; rd < rounds; ++rd) {
+                u32x4 nxt[kRound];
+#pragma unroll
+                for (int j = 0; j < kRound; ++j) {
+                    nxt[j] = fetch(kRound * (rd + 1) + j);                  // past the end: zeros
+                }
+                if (rd == 0) {
+                    cur[0] = mh == 0 ? apply_head(cur[0], hm) : cur[0];
+                    cur[1] = mh == 1 ? apply_head(cur[1], hm) : cur[1];
+                }
+#pragma unroll
+                for (int j = 0; j < kRound; ++j) {
+                    const int m = kRound * rd + j;
+                    uint32_t t = crc_word(L[kSetT], c, cur[j].x);
+                    t = crc_word(L[kSetT], t, cur[j].y);
+                    t = crc_word(L[kSetT], t, cur[j].z);
+                    t = crc_word(m + 1 == m_n ? L[kSetT] : L[kSetZ], t, cur[j].w);
+                    c = (m < m_n && q0 + kG * m >= 0) ? t : c;
+                }
+#pragma unroll
+                for (int j = 0; j < kRound; ++j) {
+                    cur[j] = nxt[j];
+                }
+            }
+            // lane j with j % 2d == 2d - 1 takes A^(16 d)(c[j - d]) ^ c[j]
+#pragma unroll
+            for (int k = 0, d = 1; d < kG; ++k, d <<= 1) {
+                const uint32_t left = (uint32_t)__shfl_up((int)c, d, kG);
+                const uint32_t sh = apply(L[kSet16 + k], left);
+                if ((lane & (2u * d - 1u)) == 2u * d - 1u) {
+                    c ^= sh;
+                }
+            }
+            c = crc_tail(L[kSetT], c, tail, r);
+        } else {
+            c = lane == kG - 1 ? crc_range(L[kSetT], 0xFFFFFFFFu, p, len) : 0u;
+        }
+        if (i < A.n && lane == kG - 1) {
+            A.out[i] = crc_finish(c, len, A.cpl != 0u);
+        }
+    }
+}
+
+// ---- block combine (round 2) -------------------------------------------------------------------
+// x^(2^k) mod P, reflected (bit 31 = x^0); kX2n[0] = x.
+__constant__ uint32_t kX2n[32] = {
+    0x40000000u, 0x20000000u, 0x08000000u, 0x00800000u, 0x00008000u, 0xEDB88320u, 0xB1E6B092u, 0xA06A2517u,
+    0xED627DAEu, 0x88D14467u, 0xD7BBFE6Au, 0xEC447F11u, 0x8E7EA170u, 0x6427800Eu, 0x4D47BAE0u, 0x09FE548Fu,
+    0x83852D0Fu, 0x30362F1Au, 0x7B5A9CC3u, 0x31FEC169u, 0x9FEC022Au, 0x6C8DEDC4u, 0x15D6874Du, 0x5FDE7A4Eu,
+    0xBAD90E37u, 0x2E4E5EEFu, 0x4EABA214u, 0xA8A472C0u, 0x429A969Eu, 0x148D302Au, 0xC40BA6D0u, 0xC4E22C3Cu};
+
+// a * b mod P (reflected), fixed trip count (no divergence across the group).
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t p = 0u;
+#pragma unroll 4
+    for (int i = 31; i >= 0; --i) {
+        p ^= ((a >> i) & 1u) ? b : 0u;
+        b = (b & 1u) ? ((b >> 1) ^ kPoly) : (b >> 1);
+    }
+    return p;
+}
+
+// x^(8 n) mod P.
+__device__ __forceinline__ uint32_t x8n(uint32_t n) {
+    uint32_t p = 0x80000000u;                                   // x^0
+    for (int k = 3; n != 0u; n >>= 1, ++k) {
+        if (n & 1u) {
+            p = multmodp(kX2n[k & 31], p);
+        }
+    }
+    return p;
+}
+
+// A 16-lane group per segment (4 segments per wave, 16 per block and step), persistent blocks.
 __global__ void __launch_bounds__(256) crc_group_kernel(CrcBatchArgs A) {
-    __shared__ CrcTables T;
-    build_tables(T);
+    __shared__ uint32_t L[1][4][256];
+    load_sets(L, 1);
     const uint32_t lane = threadIdx.x & (kG - 1);
     const uint32_t steps = (A.n + (256u / kG) - 1u) / (256u / kG);
     for (uint32_t st = blockIdx.x; st < steps; st += gridDim.x) {          // block-uniform trip count
@@ -190,7 +405,7 @@ __global__ void __launch_bounds__(256) crc_group_kernel(CrcBatchArgs A) {
         const uint32_t fb = lane * s;
         const uint32_t lo = fb > pad ? fb - pad : 0u;
         const uint32_t hi = fb + s > pad ? fb + s - pad : 0u;
-        uint32_t c = crc_range(T, 0u, p + lo, hi - lo);                // raw: from state 0
+        uint32_t c = crc_range(L[kSetT], 0u, p + lo, hi - lo);         // raw: from state 0
         // log2(G) combine levels: lane j with j % 2d == 2d - 1 takes shift(c[j - d], d s) ^ c[j].
         // Strided batches bring the level multipliers x^(8 s 2^k) and x^(8 L) from the host.
         const bool pre = A.lens == nullptr;
@@ -236,16 +451,31 @@ uint32_t h_x8n(uint64_t n) {
     return p;
 }
 
+std::atomic<int> g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL: 0 auto (2), 1 block combine, 2 interleaved
+std::atomic<int> g_crc_nt{0};          // NETCSUM_TUNE_CRC_NT: non-temporal chunk loads (interleaved form)
+
 }  // namespace
+
+void set_crc_kernel(int v) { g_crc_kernel.store(v); }
+void set_crc_nt(int v) { g_crc_nt.store(v); }
+
+const char* crc_launch_name(uint32_t max_len) {
+    if (max_len <= kCrcShortMax) return "crc_lane_kernel block=256";
+    if (g_crc_kernel.load() == 1) return "crc_group_kernel G=16 block=256";
+    return g_crc_nt.load() ? "crc_ilv_kernel<nt> G=16 block=256" : "crc_ilv_kernel G=16 block=256";
+}
 
 hipError_t launch_crc_batch(const CrcBatchArgs& a0, uint32_t max_len, int cus, hipStream_t s) {
     if (a0.n == 0u) return hipSuccess;
     CrcBatchArgs a = a0;
-    const uint32_t resident = (uint32_t)std::max(1, cus) * 8u;        // blocks that fit at once (LDS 4 KiB each)
+    const uint32_t cu = (uint32_t)std::max(1, cus);
     if (max_len <= kCrcShortMax) {
-        const uint32_t grid = std::min<uint32_t>((a.n + 255u) / 256u, resident);
+        const uint32_t grid = std::min<uint32_t>((a.n + 255u) / 256u, cu * 8u);   // LDS 4 KiB per block
         hipLaunchKernelGGL(crc_lane_kernel, dim3(grid), dim3(256), 0, s, a);
-    } else {
+        return hipGetLastError();
+    }
+    const uint32_t steps = (a.n + (256u / kG) - 1u) / (256u / kG);
+    if (g_crc_kernel.load() == 1) {
         if (a.lens == nullptr) {
             const uint32_t sb = ((a.len + kG * 4u - 1u) / (kG * 4u)) * 4u;
             uint32_t x = h_x8n(sb);
@@ -255,9 +485,15 @@ hipError_t launch_crc_batch(const CrcBatchArgs& a0, uint32_t max_len, int cus, h
             }
             a.xl = h_x8n(a.len);
         }
-        const uint32_t steps = (a.n + (256u / kG) - 1u) / (256u / kG);
-        const uint32_t grid = std::min<uint32_t>(steps, resident);
+        const uint32_t grid = std::min<uint32_t>(steps, cu * 8u);
         hipLaunchKernelGGL(crc_group_kernel, dim3(grid), dim3(256), 0, s, a);
+    } else {
+        const uint32_t grid = std::min<uint32_t>(steps, cu * 6u);          // LDS 24 KiB per block
+        if (g_crc_nt.load()) {
+            hipLaunchKernelGGL(crc_ilv_kernel<true>, dim3(grid), dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(crc_ilv_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+        }
     }
     return hipGetLastError();
 }

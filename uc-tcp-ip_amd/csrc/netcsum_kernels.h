@@ -95,6 +95,9 @@ struct CrcBatchArgs {
 };
 constexpr uint32_t kCrcShortMax = 256u;    // strided segments up to this length: one lane each
 hipError_t launch_crc_batch(const CrcBatchArgs& a, uint32_t max_len, int cus, hipStream_t s);
+const char* crc_launch_name(uint32_t max_len);
+void set_crc_kernel(int v);    // NETCSUM_TUNE_CRC_KERNEL
+void set_crc_nt(int v);        // NETCSUM_TUNE_CRC_NT
 
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, int ip_ver,  // 4, 6, 0 = per packet
                             hipStream_t s);

@@ -56,6 +56,8 @@ TUNE_STREAM_WAVES = 11
 TUNE_STREAM_TOUCH = 12
 TUNE_STREAM_XCD = 13
 TUNE_TX_FLUSH = 14
+TUNE_CRC_KERNEL = 15
+TUNE_CRC_NT = 16
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
