@@ -227,7 +227,12 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
  *               pkt_len for strided ones, or NETCSUM_TUNE_GROUP_LANES); a Fragment header (44) gives
  *               FRAGMENT; a header running past the payload gives MALFORMED
  *   EXT_HDR     any other extension header (50, 51, 59, 135, 139, 140, 253, 254), a late Hop-by-Hop
- *               header, or a chain past that window: no transport verdict in the batch
+ *               header, or a chain past that window: no transport verdict in the batch. For 50 / 51 /
+ *               59 / 135 this is also the reference's outcome: it never reaches a transport checksum
+ *               (ESP and Mobility: NET_IPv6_ERR_INVALID_EH, net_ipv6.c:8837-8846, :8956-8965; AH: the
+ *               next header is read from the IPv6 header's first octet, 0x6X, and rejected as
+ *               NET_IPv6_ERR_INVALID_PROTOCOL, :8885-8894, :8357-8360; No Next Header: no upper
+ *               layer, :8460-8462)
  * TxFinalizeIPv6 writes the TCP / UDP / ICMPv6 checksum in place (net_tcp.c:29839-29862,
  *   net_udp.c:2909-2937, net_icmpv6.c:1439 and :949-965); UDP 0x0000 -> 0xFFFF, udp_tx_csum = 0
  *   writes 0; no header checksum to write.
@@ -455,11 +460,16 @@ typedef enum netcsum_tune_key {
                                          1 scatter stores written through at system scope, 2 an L2
                                          release at the end of every scatter wave, 3 / 4 a write-back
                                          launch of 8 / 256 workgroups after the Tx launch(es)         */
-    NETCSUM_TUNE_CRC_KERNEL    = 15,  /* CRC-32 batches of segments > 256 B (and every varlen batch):
-                                         0 auto (2), 1 block combine (GF(2) multiplications by bit
-                                         loops, the round-2 form), 2 interleaved 16-B chunks with
-                                         table-driven shifts                                          */
-    NETCSUM_TUNE_CRC_NT        = 16   /* CRC-32 interleaved form: 1 non-temporal chunk loads, 0 plain */
+    NETCSUM_TUNE_CRC_KERNEL    = 15,  /* CRC-32 batches: 0 auto (strided segments <= 96 B one lane
+                                         each, longer ones and every varlen batch the interleaved
+                                         form), 1 block combine (GF(2) multiplications by bit loops,
+                                         the round-2 form), 2 interleaved for every length, 3 one lane
+                                         per segment for every length                                 */
+    NETCSUM_TUNE_CRC_NT        = 16,  /* CRC-32 interleaved form: 1 non-temporal chunk loads, 0 plain */
+    NETCSUM_TUNE_CRC_LANES     = 17,  /* CRC-32 interleaved form: lanes per segment, 1, 2, 4, 8, 16;
+                                         0 auto (8 for strided segments >= 1 KiB, else 4)             */
+    NETCSUM_TUNE_CRC_WIDE      = 18   /* CRC-32 interleaved form: 1 (default) 11-bit slicing tables
+                                         (3 LDS lookups per dword), 0 byte tables (4)                 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -51,21 +51,39 @@ def test_dropin_multicast_hash_like_the_drivers():
         assert (netcsum.Reflect32(crc) >> 26) & 0x3F == (oracle.reflect32(want) >> 26) & 0x3F
 
 
-FORMS = [(0, 0), (1, 0), (2, 1)]        # (NETCSUM_TUNE_CRC_KERNEL, NETCSUM_TUNE_CRC_NT)
-LONG_NAME = {0: "crc_ilv_kernel", 1: "crc_group_kernel", 2: "crc_ilv_kernel<nt>"}
+# (NETCSUM_TUNE_CRC_KERNEL, _NT, _LANES, _WIDE): auto, block combine, interleaved for every length (nt),
+# one lane per segment for every length, interleaved with 1 .. 16 lanes per segment, 11-bit or byte tables
+FORMS = [(0, 0, 0, 1), (1, 0, 0, 1), (2, 1, 0, 1), (3, 0, 0, 1), (2, 0, 1, 1), (2, 0, 2, 1), (2, 0, 4, 1),
+         (2, 0, 8, 1), (2, 0, 16, 1), (2, 0, 4, 0), (2, 1, 16, 0)]
 
 
-@pytest.fixture(params=FORMS, ids=lambda f: f"form{f[0]}nt{f[1]}")
+def expected_kernel(form, length, varlen=False):
+    kern, nt, lanes, wide = form
+    short = length <= 96 and not varlen
+    if kern == 3 or (kern in (0, 1) and short):
+        return "crc_lane_kernel "
+    if kern == 1:
+        return "crc_group_kernel G=16 "
+    tag = ",".join(t for t, on in (("nt", nt), ("w11", wide)) if on)
+    auto = 8 if (length >= 1024 and not varlen) else 4
+    return "crc_ilv_kernel" + (f"<{tag}>" if tag else "") + f" G={lanes or auto} "
+
+
+@pytest.fixture(params=FORMS, ids=lambda f: "k{}nt{}g{}w{}".format(*f))
 def crc_form(request):
-    kern, nt = request.param
+    kern, nt, lanes, wide = request.param
     netcsum.tune(netcsum.TUNE_CRC_KERNEL, kern)
     netcsum.tune(netcsum.TUNE_CRC_NT, nt)
-    yield kern
+    netcsum.tune(netcsum.TUNE_CRC_LANES, lanes)
+    netcsum.tune(netcsum.TUNE_CRC_WIDE, wide)
+    yield request.param
     netcsum.tune(netcsum.TUNE_CRC_KERNEL, 0)
     netcsum.tune(netcsum.TUNE_CRC_NT, 0)
+    netcsum.tune(netcsum.TUNE_CRC_LANES, 0)
+    netcsum.tune(netcsum.TUNE_CRC_WIDE, 1)
 
 
-STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (255, 256), (256, 256), (257, 300),
+STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (96, 96), (97, 100), (128, 128), (129, 130), (255, 256), (256, 256), (257, 300),
            (1500, 1500), (1514, 1518), (4096, 4100), (9000, 9001), (2048, 2048), (2049, 2050), (4111, 4111),
            (65535, 65536)]
 
@@ -86,7 +104,7 @@ def test_crc_batch_strided_vs_oracle(length, stride, cpl, crc_form):
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (base_off, [(int(i), hex(got[i]), hex(want[i])) for i in bad[:4]])
         kern = netcsum.last_launch()
-        assert kern.startswith("crc_lane_kernel" if length <= 256 else LONG_NAME[crc_form] + " "), kern
+        assert kern.startswith(expected_kernel(crc_form, length)), kern
 
 
 @pytest.mark.parametrize("cpl", [0, 1])
@@ -130,7 +148,7 @@ def test_crc_full_size_residue_1M():
     fcs = torch.zeros(n, dtype=torch.int32, device=DEV)
     netcsum.crc32_strided(buf, S, L, n, fcs, 1)
     torch.cuda.synchronize()
-    assert netcsum.last_launch().startswith("crc_ilv_kernel ")
+    assert netcsum.last_launch().startswith("crc_ilv_kernel<w11> G=8 ")
     smp = np.sort(np.random.default_rng(9).choice(n, size=4096, replace=False))
     rows = buf[: n * S].view(n, S)[torch.from_numpy(smp).to(DEV)].cpu().numpy()
     want = oracle.crc32_batch(rows.reshape(-1).copy(), len(smp), True, stride=S, length=L)
@@ -161,6 +179,7 @@ def test_crc_varlen_every_length_and_alignment(crc_form):
     netcsum.crc32_varlen(d, torch.from_numpy(off.view(np.int64)).to(DEV), torch.from_numpy(lens.view(np.int32)).to(DEV),
                          n, out, 1)
     torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith(expected_kernel(crc_form, 0, varlen=True)), netcsum.last_launch()
     want = oracle.crc32_batch(data, n, True, off=off, lens=lens)
     got = out.cpu().numpy().view(np.uint32)
     bad = np.nonzero(got != want)[0]

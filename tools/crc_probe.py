@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """CRC-32 batch probe (net_util.c:485-636): the long-segment kernel forms side by side in one process
-(NETCSUM_TUNE_CRC_KERNEL 1 = block combine, 2 = interleaved chunks; NETCSUM_TUNE_CRC_NT), interleaved
+(NETCSUM_TUNE_CRC_KERNEL 1 = block combine, 2 = interleaved chunks, 3 = one lane per segment;
+NETCSUM_TUNE_CRC_LANES, NETCSUM_TUNE_CRC_NT), interleaved
 passes, every timed batch spot-checked against the oracle. One JSON line per (workload, variant).
     python tools/crc_probe.py [passes]"""
 import json
@@ -18,7 +19,9 @@ import oracle  # noqa: E402
 from bench_configs import events_ms  # noqa: E402
 
 SEED = 0x5EED0C3C
-VARIANTS = [{"kernel": 1, "nt": 0}, {"kernel": 2, "nt": 0}, {"kernel": 2, "nt": 1}]
+VARIANTS = ([{"kernel": 0, "nt": 0, "lanes": 0, "wide": 1}, {"kernel": 1, "nt": 0, "lanes": 0, "wide": 0},
+             {"kernel": 3, "nt": 0, "lanes": 0, "wide": 0}]
+            + [{"kernel": 2, "nt": 0, "lanes": g, "wide": w} for w in (0, 1) for g in (2, 4, 8)])
 
 
 def main():
@@ -27,7 +30,8 @@ def main():
     st = torch.cuda.current_stream(dev)
     work = []
     # strided frames: (n, length, stride)
-    for n, L, S in ((1 << 20, 1500, 1500), (1 << 20, 1514, 1518), (1 << 18, 9000, 9000), (1 << 22, 300, 300)):
+    for n, L, S in ((1 << 20, 1500, 1500), (1 << 20, 1514, 1518), (1 << 18, 9000, 9000), (1 << 22, 300, 300),
+                    (1 << 22, 600, 600), (1 << 23, 64, 64), (1 << 23, 128, 128), (1 << 22, 256, 256)):
         buf = torch.empty(n * S + 64, dtype=torch.uint8, device=dev)
         netcsum.fill(buf, n * S, SEED, 0)
         out = torch.empty(n, dtype=torch.int32, device=dev)
@@ -55,6 +59,8 @@ def main():
             for v in VARIANTS:
                 netcsum.tune(netcsum.TUNE_CRC_KERNEL, v["kernel"])
                 netcsum.tune(netcsum.TUNE_CRC_NT, v["nt"])
+                netcsum.tune(netcsum.TUNE_CRC_LANES, v["lanes"])
+                netcsum.tune(netcsum.TUNE_CRC_WIDE, v["wide"])
                 ms = events_ms(fn, st)
                 key = (name, json.dumps(v))
                 if p == 0:
@@ -74,6 +80,8 @@ def main():
                                   "same": res[key]["same"]}), flush=True)
     netcsum.tune(netcsum.TUNE_CRC_KERNEL, 0)
     netcsum.tune(netcsum.TUNE_CRC_NT, 0)
+    netcsum.tune(netcsum.TUNE_CRC_LANES, 0)
+    netcsum.tune(netcsum.TUNE_CRC_WIDE, 1)
 
 
 if __name__ == "__main__":

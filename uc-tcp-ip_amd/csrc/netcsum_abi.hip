@@ -645,7 +645,7 @@ NET_ERR NetUtil_MI355X_CRC32BatchStrided(const void* d_base, uint64_t stride, ui
     a.n = n;
     a.cpl = cpl ? 1u : 0u;
     a.out = d_out;
-    netcsum::set_last_launch(netcsum::crc_launch_name(len));
+    netcsum::set_last_launch(netcsum::crc_launch_name(len, false));
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
     NC_HIP(netcsum::launch_crc_batch(a, len, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
@@ -663,7 +663,7 @@ NET_ERR NetUtil_MI355X_CRC32BatchVarLen(const void* d_base, const uint64_t* d_of
     a.n = n;
     a.cpl = cpl ? 1u : 0u;
     a.out = d_out;
-    netcsum::set_last_launch(netcsum::crc_launch_name(0xFFFFFFFFu));
+    netcsum::set_last_launch(netcsum::crc_launch_name(0xFFFFFFFFu, true));
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
     NC_HIP(netcsum::launch_crc_batch(a, 0xFFFFFFFFu, cu_count(dev), static_cast<hipStream_t>(hip_stream)));
@@ -936,8 +936,18 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         netcsum::set_stream_touch(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CRC_KERNEL:
-        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_crc_kernel(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CRC_LANES:
+        if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16)) {
+            return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        }
+        netcsum::set_crc_lanes(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CRC_WIDE:
+        if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_crc_wide(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CRC_NT:
         if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

@@ -14,15 +14,15 @@
 // together: c <- A^4(c ^ w) (slicing-by-4; T = the tables of A^4, T[3] = the byte table of the
 // reference's bit loop).
 //
-// Interleaved chunks (crc_ilv_kernel, segments of 32 B and more). A 16-lane group owns a segment.
-// The segment's bytes from the 16-B line at or below its start up to the last 16-B boundary at or
-// below its end are 16-B chunks, front-padded with zero chunks to 16 M chunks; lane l takes chunks
-// l, l + 16, l + 32, ... The lane's register runs over its chunk's first three dwords with T and
-// over the fourth with Z = A^240 o A^4, i.e. it is carried past the 15 chunks the other lanes own,
-// so that it stands at the start of the lane's next chunk; the last chunk uses T, which leaves lane
-// l at the end of chunk l + 16 (M - 1). Four shuffle levels then merge pairs of lanes 16, 32, 64 and
-// 128 B apart (tables of A^16 .. A^128), giving raw() of the chunk area in lane 15, which finishes
-// the < 16 trailing octets alone. Every global load is a whole aligned 16-B chunk, a group's load
+// Interleaved chunks (crc_ilv_kernel<G>, segments of 32 B and more). A G-lane group (G = 4, 8, 16
+// by segment length) owns a segment. The segment's bytes from the 16-B line at or below its start
+// up to the last 16-B boundary at or below its end are 16-B chunks, front-padded with zero chunks to
+// G M chunks; lane l takes chunks l, l + G, l + 2G, ... The lane's register runs over its chunk's
+// first three dwords with T and over the fourth with Z = A^(16 (G - 1)) o A^4, i.e. it is carried
+// past the G - 1 chunks the other lanes own, so that it stands at the start of the lane's next
+// chunk; the last chunk uses T, which leaves lane l at the end of chunk l + G (M - 1). log2(G)
+// shuffle levels then merge pairs of lanes 16, 32, 64, 128 B apart (tables of A^16 .. A^128), giving
+// raw() of the chunk area in lane G - 1, which finishes the < 16 trailing octets alone. Every global load is a whole aligned 16-B chunk, a group's load
 // instruction reads 256 contiguous bytes, and every step of every lane is four independent table
 // lookups in LDS: no GF(2) multiplications at run time. The bytes of the first line below the
 // segment start are masked to zero, and the reference's initial register 0xFFFFFFFF enters as an
@@ -38,6 +38,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <string>
+#include <vector>
 
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
@@ -50,7 +52,12 @@ constexpr uint32_t kPoly = 0xEDB88320u;
 
 // ---- compile-time tables -----------------------------------------------------------------------
 // Table sets of the linear maps used by the kernels, S[k][b] = A^n(b << 8k):
-enum : int { kSetT = 0, kSetZ = 1, kSet16 = 2, kSet32 = 3, kSet64 = 4, kSet128 = 5, kNumSets = 6 };
+enum : int {
+    kSetT = 0,                          // A^4 (slicing-by-4; [3] = the byte table)
+    kSet16 = 1, kSet32 = 2, kSet64 = 3, kSet128 = 4,   // A^16 .. A^128: the combine levels
+    kSetZ16 = 5, kSetZ8 = 6, kSetZ4 = 7, kSetZ2 = 8,   // A^(16 (G - 1)) o A^4 for G = 16, 8, 4, 2 lanes
+    kNumSets = 9
+};
 
 struct CrcTabs {
     uint32_t s[kNumSets][4][256];
@@ -97,8 +104,11 @@ constexpr CrcTabs make_tabs() {
     const Set t32 = compose(t16, t16);
     const Set t64 = compose(t32, t32);
     const Set t128 = compose(t64, t64);
-    const Set z = compose(t128, compose(t64, compose(t32, compose(t16, t4))));   // A^(4 + 240)
-    const Set* sets[kNumSets] = {&t4, &z, &t16, &t32, &t64, &t128};
+    const Set z16 = compose(t128, compose(t64, compose(t32, compose(t16, t4))));   // A^(240 + 4)
+    const Set z8 = compose(t64, compose(t32, compose(t16, t4)));                   // A^(112 + 4)
+    const Set z4 = compose(t32, compose(t16, t4));                                 // A^(48 + 4)
+    const Set z2 = compose(t16, t4);                                               // A^(16 + 4)
+    const Set* sets[kNumSets] = {&t4, &t16, &t32, &t64, &t128, &z16, &z8, &z4, &z2};
     CrcTabs r{};
     for (int s = 0; s < kNumSets; ++s) {
         for (int k = 0; k < 4; ++k) {
@@ -111,17 +121,72 @@ constexpr CrcTabs make_tabs() {
 }
 
 __device__ const CrcTabs kTabs = make_tabs();
+
+// 11-bit slicing: the same linear maps as three tables indexed by register bits [0, 11), [11, 22)
+// and [22, 32): 3 LDS lookups per dword instead of 4 (20 KiB per map).
+constexpr int kWide = 5120;
+enum : int { kWideT = 0, kWideZ16 = 1, kWideZ8 = 2, kWideZ4 = 3, kWideZ2 = 4, kNumWide = 5 };
+
+struct CrcWide {
+    uint32_t w[kNumWide][kWide];
+};
+
+constexpr CrcWide make_wide() {
+    const CrcTabs t = make_tabs();
+    const int src[kNumWide] = {kSetT, kSetZ16, kSetZ8, kSetZ4, kSetZ2};
+    CrcWide r{};
+    for (int m = 0; m < kNumWide; ++m) {
+        const uint32_t(&S)[4][256] = t.s[src[m]];
+        auto ap = [&](uint32_t c) {
+            return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
+        };
+        for (uint32_t b = 0; b < 2048u; ++b) {
+            r.w[m][b] = ap(b);
+            r.w[m][2048 + b] = ap(b << 11);
+        }
+        for (uint32_t b = 0; b < 1024u; ++b) {
+            r.w[m][4096 + b] = ap(b << 22);
+        }
+    }
+    return r;
+}
+
+__device__ const CrcWide kWideTabs = make_wide();
 static_assert(make_tabs().s[kSetT][3][1] == 0x77073096u, "byte table of the reflected IEEE polynomial");
 static_assert(make_tabs().s[kSetT][3][255] == 0x2D02EF8Du, "byte table of the reflected IEEE polynomial");
 
-// Copy the first `nsets` table sets into LDS (blockDim.x == 256, one uint4 per thread per KiB).
-__device__ __forceinline__ void load_sets(uint32_t (*L)[4][256], int nsets) {
+// Copy table sets into LDS: sets [0, n) to slots [0, n) and, if z >= 0, set z to slot n
+// (blockDim.x == B; one uint4 = 16 B per thread and step). No barrier: the caller's.
+template <int B = 256>
+__device__ __forceinline__ void copy_sets(uint32_t (*L)[4][256], int n, int z) {
     const uint4* src = reinterpret_cast<const uint4*>(&kTabs.s[0][0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&L[0][0][0]);
-    for (int i = (int)threadIdx.x; i < nsets * 256; i += 256) {
+    for (int i = (int)threadIdx.x; i < n * 256; i += B) {
         dst[i] = src[i];
     }
+    if (z >= 0) {
+        for (int i = (int)threadIdx.x; i < 256; i += B) {
+            dst[n * 256 + i] = src[z * 256 + i];
+        }
+    }
+}
+
+__device__ __forceinline__ void load_sets(uint32_t (*L)[4][256], int n, int z) {
+    copy_sets<256>(L, n, z);
     __syncthreads();
+}
+
+template <int B>
+__device__ __forceinline__ void copy_wide(uint32_t* dst_w, int m) {
+    const uint4* src = reinterpret_cast<const uint4*>(&kWideTabs.w[m][0]);
+    uint4* dst = reinterpret_cast<uint4*>(dst_w);
+    for (int i = (int)threadIdx.x; i < kWide / 4; i += B) {
+        dst[i] = src[i];
+    }
+}
+
+__device__ __forceinline__ uint32_t apply_wide(const uint32_t* W, uint32_t c) {
+    return W[c & 0x7FFu] ^ W[2048u + ((c >> 11) & 0x7FFu)] ^ W[4096u + (c >> 22)];
 }
 
 __device__ __forceinline__ uint32_t apply(const uint32_t (*S)[256], uint32_t c) {
@@ -205,16 +270,16 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t c, uint32_t len, bool cp
 // copied once per block, which then walks its share of the batch 256 segments at a time.
 __global__ void __launch_bounds__(256) crc_lane_kernel(CrcBatchArgs A) {
     __shared__ uint32_t L[1][4][256];
-    load_sets(L, 1);
+    load_sets(L, 1, -1);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < A.n; i += gridDim.x * 256u) {
         const uint8_t* p;
         uint32_t len;
         seg_desc(A, i, p, len);
-        A.out[i] = crc_finish(crc_range(L[kSetT], 0xFFFFFFFFu, p, len), len, A.cpl != 0u);
+        A.out[i] = crc_finish(crc_range(L[0], 0xFFFFFFFFu, p, len), len, A.cpl != 0u);
     }
 }
 
-constexpr int kG = 16;                  // lanes per segment (both long-segment kernels)
+constexpr int kG = 16;                  // lanes per segment of the block-combine kernel
 
 // ---- interleaved chunks ------------------------------------------------------------------------
 // The masks that make the segment's head chunk q (0 or 1; its other chunks are not touched) enter
@@ -266,16 +331,45 @@ __device__ __forceinline__ uint32_t crc_tail(const uint32_t (*T)[256], uint32_t 
 
 constexpr int kRound = 4;               // chunks per lane per round (one round prefetched)
 
-template <bool NT>
-__global__ void __launch_bounds__(256) crc_ilv_kernel(CrcBatchArgs A) {
-    __shared__ uint32_t L[kNumSets][4][256];                    // 24 KiB
-    load_sets(L, kNumSets);
-    const uint32_t lane = threadIdx.x & (kG - 1);
-    const uint32_t steps = (A.n + (256u / kG) - 1u) / (256u / kG);
+constexpr int log2i(int g) { return g <= 1 ? 0 : 1 + log2i(g / 2); }
+
+// W11: chunk steps with the 11-bit tables (blocks of 512 threads), else the byte tables (256).
+template <int G, bool NT, bool W11>
+__global__ void __launch_bounds__(W11 ? 512 : 256) crc_ilv_kernel(CrcBatchArgs A) {
+    constexpr uint32_t B = W11 ? 512u : 256u;
+    constexpr int kLevels = log2i(G);                           // combine levels: A^16 .. A^(8 G)
+    constexpr int kZ = kLevels + 1;                             // LDS slot of this G's Z (byte tables)
+    constexpr int kZset = G == 16 ? kSetZ16 : G == 8 ? kSetZ8 : G == 4 ? kSetZ4 : G == 2 ? kSetZ2 : kSetT;
+    constexpr int kZwide = G == 16 ? kWideZ16 : G == 8 ? kWideZ8 : G == 4 ? kWideZ4 : G == 2 ? kWideZ2 : kWideT;
+    // T, A^16.., Z: 8 .. 24 KiB (byte tables); T, A^16.. + 2 x 20 KiB wide maps (W11)
+    __shared__ uint32_t L[W11 ? kLevels + 1 : kLevels + 2][4][256];
+    __shared__ uint32_t LW[W11 ? 2 : 1][W11 ? kWide : 1];
+    copy_sets<B>(L, kLevels + 1, W11 ? -1 : kZset);
+    if constexpr (W11) {
+        copy_wide<B>(LW[0], kWideT);
+        copy_wide<B>(LW[1], kZwide);
+    }
+    __syncthreads();
+    auto step = [&](uint32_t c, uint32_t w, bool last) -> uint32_t {   // T (last) or Z on c ^ w
+        if constexpr (W11) {
+            return apply_wide(last ? LW[0] : LW[1], c ^ w);
+        } else {
+            return crc_word(last ? L[0] : L[kZ], c, w);
+        }
+    };
+    auto step_t = [&](uint32_t c, uint32_t w) -> uint32_t {
+        if constexpr (W11) {
+            return apply_wide(LW[0], c ^ w);
+        } else {
+            return crc_word(L[0], c, w);
+        }
+    };
+    const uint32_t lane = threadIdx.x & (G - 1);
+    const uint32_t steps = (A.n + (B / G) - 1u) / (B / G);
     // rounds per segment: wave-uniform for strided batches (bound from the common length)
-    const int r_strided = (int)(((A.len + 15u) / 16u + kG * kRound - 1u) / (kG * kRound));
+    const int r_strided = (int)(((A.len + 15u) / 16u + G * kRound - 1u) / (G * kRound));
     for (uint32_t st = blockIdx.x; st < steps; st += gridDim.x) {          // block-uniform trip count
-        const uint32_t i = st * (256u / kG) + threadIdx.x / kG;
+        const uint32_t i = st * (B / G) + threadIdx.x / G;
         const uint8_t* p = A.base;
         uint32_t len = 0u;
         if (i < A.n) {
@@ -289,17 +383,17 @@ __global__ void __launch_bounds__(256) crc_ilv_kernel(CrcBatchArgs A) {
             const uintptr_t ce = e & ~(uintptr_t)15u;
             const uint32_t r = (uint32_t)(e - ce);                          // tail octets, < 16
             const int kc = (int)((ce - fs) >> 4);                           // whole chunks, >= 2
-            const int m_n = (kc + kG - 1) / kG;                             // chunks per lane
-            const int pad = m_n * kG - kc;
+            const int m_n = (kc + G - 1) / G;                               // chunks per lane
+            const int pad = m_n * G - kc;                                   // zero chunks in front, < G
             const int lead = (int)(a - fs);
             const int rounds = A.lens ? (m_n + kRound - 1) / kRound : r_strided;
-            // Chunk m of this lane is q = lane + 16 m - pad. A missing one (q < 0: the zero chunks in
+            // Chunk m of this lane is q = lane + G m - pad. A missing one (q < 0: the zero chunks in
             // front, whose register stays 0; m >= m_n: past the lane's last chunk) is loaded from the
             // first chunk (always present) and its steps are discarded by a select on the register,
             // never on the loaded value (a select on it would pull the prefetch's wait forward).
             const int q0 = (int)lane - pad;
             auto fetch = [&](int m) -> u32x4 {
-                const int q = q0 + kG * m;
+                const int q = q0 + G * m;
                 const bool ok = q >= 0 && m < m_n;
                 return load16<NT>(reinterpret_cast<gu32x4*>(fs + (ok ? 16u * (uint32_t)q : 0u)));
             };
@@ -309,47 +403,57 @@ __global__ void __launch_bounds__(256) crc_ilv_kernel(CrcBatchArgs A) {
                 cur[j] = fetch(j);
             }
             const u32x4 tail = load16<NT>(reinterpret_cast<gu32x4*>(r != 0u ? ce : fs));
-            const int mh = q0 >= -1 ? 0 : 1;                                // the lane's chunk holding q 0 or 1
-            const HeadMask hm = head_mask(q0 + kG * mh, lead);
+            // chunks 0 and 1 are the m = 0 chunks of lanes pad and pad + 1, or chunk 1 is the m = 1
+            // chunk of lane 0 when pad = G - 1 (G = 1: both are lane 0's, m = 0 and 1)
+            const int mh = q0 == 1 - G ? 1 : 0;
+            const HeadMask hm = head_mask(q0 + G * mh, lead);
+            [[maybe_unused]] HeadMask hm1;
+            if constexpr (G == 1) {
+                hm1 = head_mask(1, lead);
+            }
             c = 0u;
             for (int rd = 0; rd < rounds; ++rd) {
                 u32x4 nxt[kRound];
 #pragma unroll
                 for (int j = 0; j < kRound; ++j) {
-                    nxt[j] = fetch(kRound * (rd + 1) + j);                  // past the end: zeros
+                    nxt[j] = fetch(kRound * (rd + 1) + j);
                 }
                 if (rd == 0) {
-                    cur[0] = mh == 0 ? apply_head(cur[0], hm) : cur[0];
-                    cur[1] = mh == 1 ? apply_head(cur[1], hm) : cur[1];
+                    if constexpr (G == 1) {
+                        cur[0] = apply_head(cur[0], head_mask(0, lead));
+                        cur[1] = apply_head(cur[1], hm1);
+                    } else {
+                        cur[0] = mh == 0 ? apply_head(cur[0], hm) : cur[0];
+                        cur[1] = mh == 1 ? apply_head(cur[1], hm) : cur[1];
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < kRound; ++j) {
                     const int m = kRound * rd + j;
-                    uint32_t t = crc_word(L[kSetT], c, cur[j].x);
-                    t = crc_word(L[kSetT], t, cur[j].y);
-                    t = crc_word(L[kSetT], t, cur[j].z);
-                    t = crc_word(m + 1 == m_n ? L[kSetT] : L[kSetZ], t, cur[j].w);
-                    c = (m < m_n && q0 + kG * m >= 0) ? t : c;
+                    uint32_t t = step_t(c, cur[j].x);
+                    t = step_t(t, cur[j].y);
+                    t = step_t(t, cur[j].z);
+                    t = step(t, cur[j].w, m + 1 == m_n);
+                    c = (m < m_n && q0 + G * m >= 0) ? t : c;
                 }
 #pragma unroll
                 for (int j = 0; j < kRound; ++j) {
                     cur[j] = nxt[j];
                 }
             }
-            // lane j with j % 2d == 2d - 1 takes A^(16 d)(c[j - d]) ^ c[j]
+            // level k: lane j with j % 2d == 2d - 1 (d = 2^k) takes A^(16 d)(c[j - d]) ^ c[j]
 #pragma unroll
-            for (int k = 0, d = 1; d < kG; ++k, d <<= 1) {
-                const uint32_t left = (uint32_t)__shfl_up((int)c, d, kG);
-                const uint32_t sh = apply(L[kSet16 + k], left);
+            for (int k = 0, d = 1; d < G; ++k, d <<= 1) {
+                const uint32_t left = (uint32_t)__shfl_up((int)c, d, G);
                 if ((lane & (2u * d - 1u)) == 2u * d - 1u) {
-                    c ^= sh;
+                    c ^= apply(L[1 + k], left);
                 }
             }
-            c = crc_tail(L[kSetT], c, tail, r);
+            c = crc_tail(L[0], c, tail, r);
         } else {
-            c = lane == kG - 1 ? crc_range(L[kSetT], 0xFFFFFFFFu, p, len) : 0u;
+            c = lane == G - 1 ? crc_range(L[0], 0xFFFFFFFFu, p, len) : 0u;
         }
-        if (i < A.n && lane == kG - 1) {
+        if (i < A.n && lane == G - 1) {
             A.out[i] = crc_finish(c, len, A.cpl != 0u);
         }
     }
@@ -388,7 +492,7 @@ __device__ __forceinline__ uint32_t x8n(uint32_t n) {
 // A 16-lane group per segment (4 segments per wave, 16 per block and step), persistent blocks.
 __global__ void __launch_bounds__(256) crc_group_kernel(CrcBatchArgs A) {
     __shared__ uint32_t L[1][4][256];
-    load_sets(L, 1);
+    load_sets(L, 1, -1);
     const uint32_t lane = threadIdx.x & (kG - 1);
     const uint32_t steps = (A.n + (256u / kG) - 1u) / (256u / kG);
     for (uint32_t st = blockIdx.x; st < steps; st += gridDim.x) {          // block-uniform trip count
@@ -405,7 +509,7 @@ __global__ void __launch_bounds__(256) crc_group_kernel(CrcBatchArgs A) {
         const uint32_t fb = lane * s;
         const uint32_t lo = fb > pad ? fb - pad : 0u;
         const uint32_t hi = fb + s > pad ? fb + s - pad : 0u;
-        uint32_t c = crc_range(L[kSetT], 0u, p + lo, hi - lo);         // raw: from state 0
+        uint32_t c = crc_range(L[0], 0u, p + lo, hi - lo);         // raw: from state 0
         // log2(G) combine levels: lane j with j % 2d == 2d - 1 takes shift(c[j - d], d s) ^ c[j].
         // Strided batches bring the level multipliers x^(8 s 2^k) and x^(8 L) from the host.
         const bool pre = A.lens == nullptr;
@@ -451,32 +555,102 @@ uint32_t h_x8n(uint64_t n) {
     return p;
 }
 
-std::atomic<int> g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL: 0 auto (2), 1 block combine, 2 interleaved
+std::atomic<int> g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL (netcsum_mi355x.h)
+std::atomic<int> g_crc_lanes{0};       // NETCSUM_TUNE_CRC_LANES: interleaved lanes per segment, 0 auto
 std::atomic<int> g_crc_nt{0};          // NETCSUM_TUNE_CRC_NT: non-temporal chunk loads (interleaved form)
+std::atomic<int> g_crc_wide{1};        // NETCSUM_TUNE_CRC_WIDE: 11-bit tables (interleaved form)
+
+enum class CrcForm { Lane, Block, Ilv1, Ilv2, Ilv4, Ilv8, Ilv16 };
+
+CrcForm ilv_form(uint32_t max_len, bool varlen) {
+    switch (g_crc_lanes.load()) {
+    case 1: return CrcForm::Ilv1;
+    case 2: return CrcForm::Ilv2;
+    case 4: return CrcForm::Ilv4;
+    case 8: return CrcForm::Ilv8;
+    case 16: return CrcForm::Ilv16;
+    default: return !varlen && max_len >= 1024u ? CrcForm::Ilv8 : CrcForm::Ilv4;   // tools/crc_probe.py sweep
+    }
+}
+
+CrcForm crc_form(uint32_t max_len, bool varlen) {
+    switch (g_crc_kernel.load()) {
+    case 1: return max_len <= kCrcShortMax && !varlen ? CrcForm::Lane : CrcForm::Block;
+    case 2: return ilv_form(max_len, varlen);
+    case 3: return CrcForm::Lane;
+    default: return max_len <= kCrcShortMax && !varlen ? CrcForm::Lane : ilv_form(max_len, varlen);
+    }
+}
 
 }  // namespace
 
 void set_crc_kernel(int v) { g_crc_kernel.store(v); }
+void set_crc_lanes(int v) { g_crc_lanes.store(v); }
 void set_crc_nt(int v) { g_crc_nt.store(v); }
+void set_crc_wide(int v) { g_crc_wide.store(v); }
 
-const char* crc_launch_name(uint32_t max_len) {
-    if (max_len <= kCrcShortMax) return "crc_lane_kernel block=256";
-    if (g_crc_kernel.load() == 1) return "crc_group_kernel G=16 block=256";
-    return g_crc_nt.load() ? "crc_ilv_kernel<nt> G=16 block=256" : "crc_ilv_kernel G=16 block=256";
+const char* crc_launch_name(uint32_t max_len, bool varlen) {
+    // [wide][nt][log2 G]: "crc_ilv_kernel<nt,w11> G=4 block=512", ...
+    static const std::vector<std::string> names = [] {
+        std::vector<std::string> v;
+        for (int w = 0; w < 2; ++w) {
+            for (int nt = 0; nt < 2; ++nt) {
+                for (int g = 1; g <= 16; g *= 2) {
+                    std::string t = nt ? (w ? "<nt,w11>" : "<nt>") : (w ? "<w11>" : "");
+                    v.push_back("crc_ilv_kernel" + t + " G=" + std::to_string(g) + (w ? " block=512" : " block=256"));
+                }
+            }
+        }
+        return v;
+    }();
+    const int base = (g_crc_wide.load() != 0 ? 10 : 0) + (g_crc_nt.load() != 0 ? 5 : 0);
+    switch (crc_form(max_len, varlen)) {
+    case CrcForm::Lane: return "crc_lane_kernel block=256";
+    case CrcForm::Block: return "crc_group_kernel G=16 block=256";
+    case CrcForm::Ilv1: return names[base + 0].c_str();
+    case CrcForm::Ilv2: return names[base + 1].c_str();
+    case CrcForm::Ilv4: return names[base + 2].c_str();
+    case CrcForm::Ilv8: return names[base + 3].c_str();
+    default: return names[base + 4].c_str();
+    }
+}
+
+template <int G, bool W11>
+static void launch_ilv_w(const CrcBatchArgs& a, uint32_t cu, hipStream_t s) {
+    constexpr uint32_t B = W11 ? 512u : 256u;
+    const uint32_t steps = (a.n + (B / G) - 1u) / (B / G);
+    // blocks resident per CU by LDS: byte tables 24 / 20 / <= 16 KiB (256 threads); W11 44 .. 60 KiB (512)
+    const uint32_t per_cu = W11 ? (G >= 8 ? 2u : 3u) : (G == 16 ? 6u : G == 8 ? 8u : 10u);
+    const uint32_t grid = std::min<uint32_t>(steps, cu * per_cu);
+    if (g_crc_nt.load()) {
+        hipLaunchKernelGGL((crc_ilv_kernel<G, true, W11>), dim3(grid), dim3(B), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((crc_ilv_kernel<G, false, W11>), dim3(grid), dim3(B), 0, s, a);
+    }
+}
+
+template <int G>
+static void launch_ilv(const CrcBatchArgs& a, uint32_t cu, hipStream_t s) {
+    if (g_crc_wide.load()) {
+        launch_ilv_w<G, true>(a, cu, s);
+    } else {
+        launch_ilv_w<G, false>(a, cu, s);
+    }
 }
 
 hipError_t launch_crc_batch(const CrcBatchArgs& a0, uint32_t max_len, int cus, hipStream_t s) {
     if (a0.n == 0u) return hipSuccess;
     CrcBatchArgs a = a0;
     const uint32_t cu = (uint32_t)std::max(1, cus);
-    if (max_len <= kCrcShortMax) {
+    const bool varlen = a.lens != nullptr;
+    switch (crc_form(max_len, varlen)) {
+    case CrcForm::Lane: {
         const uint32_t grid = std::min<uint32_t>((a.n + 255u) / 256u, cu * 8u);   // LDS 4 KiB per block
         hipLaunchKernelGGL(crc_lane_kernel, dim3(grid), dim3(256), 0, s, a);
-        return hipGetLastError();
+        break;
     }
-    const uint32_t steps = (a.n + (256u / kG) - 1u) / (256u / kG);
-    if (g_crc_kernel.load() == 1) {
-        if (a.lens == nullptr) {
+    case CrcForm::Block: {
+        if (!varlen) {
             const uint32_t sb = ((a.len + kG * 4u - 1u) / (kG * 4u)) * 4u;
             uint32_t x = h_x8n(sb);
             for (int k = 0; k < 4; ++k) {
@@ -485,15 +659,15 @@ hipError_t launch_crc_batch(const CrcBatchArgs& a0, uint32_t max_len, int cus, h
             }
             a.xl = h_x8n(a.len);
         }
-        const uint32_t grid = std::min<uint32_t>(steps, cu * 8u);
-        hipLaunchKernelGGL(crc_group_kernel, dim3(grid), dim3(256), 0, s, a);
-    } else {
-        const uint32_t grid = std::min<uint32_t>(steps, cu * 6u);          // LDS 24 KiB per block
-        if (g_crc_nt.load()) {
-            hipLaunchKernelGGL(crc_ilv_kernel<true>, dim3(grid), dim3(256), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(crc_ilv_kernel<false>, dim3(grid), dim3(256), 0, s, a);
-        }
+        const uint32_t steps = (a.n + (256u / kG) - 1u) / (256u / kG);
+        hipLaunchKernelGGL(crc_group_kernel, dim3(std::min<uint32_t>(steps, cu * 8u)), dim3(256), 0, s, a);
+        break;
+    }
+    case CrcForm::Ilv1: launch_ilv<1>(a, cu, s); break;
+    case CrcForm::Ilv2: launch_ilv<2>(a, cu, s); break;
+    case CrcForm::Ilv4: launch_ilv<4>(a, cu, s); break;
+    case CrcForm::Ilv8: launch_ilv<8>(a, cu, s); break;
+    default: launch_ilv<16>(a, cu, s); break;
     }
     return hipGetLastError();
 }

@@ -93,11 +93,13 @@ struct CrcBatchArgs {
     uint32_t        xs[4];         // strided: x^(8 s 2^k) mod P of the 16-lane combine (set by the launcher)
     uint32_t        xl;            // strided: x^(8 len) mod P
 };
-constexpr uint32_t kCrcShortMax = 256u;    // strided segments up to this length: one lane each
+constexpr uint32_t kCrcShortMax = 96u;     // strided segments up to this length: one lane each
 hipError_t launch_crc_batch(const CrcBatchArgs& a, uint32_t max_len, int cus, hipStream_t s);
-const char* crc_launch_name(uint32_t max_len);
+const char* crc_launch_name(uint32_t max_len, bool varlen);
 void set_crc_kernel(int v);    // NETCSUM_TUNE_CRC_KERNEL
 void set_crc_nt(int v);        // NETCSUM_TUNE_CRC_NT
+void set_crc_lanes(int v);     // NETCSUM_TUNE_CRC_LANES
+void set_crc_wide(int v);      // NETCSUM_TUNE_CRC_WIDE
 
 hipError_t launch_pkt_batch(const PktBatchArgs& a, const LaunchCfg& c, bool tx, int ip_ver,  // 4, 6, 0 = per packet
                             hipStream_t s);

@@ -58,6 +58,8 @@ TUNE_STREAM_XCD = 13
 TUNE_TX_FLUSH = 14
 TUNE_CRC_KERNEL = 15
 TUNE_CRC_NT = 16
+TUNE_CRC_LANES = 17
+TUNE_CRC_WIDE = 18
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
