@@ -5,6 +5,7 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   c4  1 M packed UDP 40-9000 B + pseudo          c5  16 M x 1500 B + pseudo (one GPU's shard)
   rx / tx  fused Rx / Tx finalize, 1 M x 1500-B IPv4/TCP, strided; tx2 = two-pass Tx
   rx6 / rxmix  fused Rx of the same datagrams as IPv6/TCP / alternating IPv4 and IPv6 (bench_configs)
+  crc  CRC-32 CalcCpl of 1 M x 1500-B frames, strided (the library's default CRC form)
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
 import os
 import sys
@@ -39,6 +40,13 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device=dev)
         fn = lambda: netcsum.batch_strided(hdr, L, L, None, 0, 0, n, out, 2, stream=st)  # noqa: E731
         algo = n * (L + 2)
+    elif name == "crc":
+        n, L = 1 << 20, 1500
+        fr = torch.empty(n * L + 64, dtype=torch.uint8, device=dev)
+        netcsum.fill(fr, n * L, SEED, 0)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        fn = lambda: netcsum.crc32_strided(fr, L, L, n, out, 1, stream=st)  # noqa: E731
+        algo = n * (L + 4)
     elif name == "c4":
         n = 1 << 20
         lens = np.random.default_rng(7).integers(40, 9001, size=n).astype(np.uint16)
