@@ -52,9 +52,11 @@ def test_dropin_multicast_hash_like_the_drivers():
 
 
 # (NETCSUM_TUNE_CRC_KERNEL, _NT, _LANES, _WIDE): auto, block combine, interleaved for every length (nt),
-# one lane per segment for every length, interleaved with 1 .. 16 lanes per segment, 11-bit or byte tables
+# one lane per segment for every length, interleaved with 1 .. 16 lanes per segment; byte (0), 11-bit (1) or
+# lane-replicated 6-bit (2) tables
 FORMS = [(0, 0, 0, 1), (1, 0, 0, 1), (2, 1, 0, 1), (3, 0, 0, 1), (2, 0, 1, 1), (2, 0, 2, 1), (2, 0, 4, 1),
-         (2, 0, 8, 1), (2, 0, 16, 1), (2, 0, 4, 0), (2, 1, 16, 0)]
+         (2, 0, 8, 1), (2, 0, 16, 1), (2, 0, 4, 0), (2, 1, 16, 0), (2, 0, 1, 2), (2, 0, 4, 2), (2, 0, 8, 2),
+         (2, 1, 16, 2)]
 
 
 def expected_kernel(form, length, varlen=False):
@@ -64,7 +66,7 @@ def expected_kernel(form, length, varlen=False):
         return "crc_lane_kernel "
     if kern == 1:
         return "crc_group_kernel G=16 "
-    tag = ",".join(t for t, on in (("nt", nt), ("w11", wide)) if on)
+    tag = ",".join(t for t, on in (("nt", nt), ("w11", wide == 1), ("k6", wide == 2)) if on)
     auto = 8 if (length >= 1024 and not varlen) else 4
     return "crc_ilv_kernel" + (f"<{tag}>" if tag else "") + f" G={lanes or auto} "
 

@@ -21,7 +21,7 @@ from bench_configs import events_ms  # noqa: E402
 SEED = 0x5EED0C3C
 VARIANTS = ([{"kernel": 0, "nt": 0, "lanes": 0, "wide": 1}, {"kernel": 1, "nt": 0, "lanes": 0, "wide": 0},
              {"kernel": 3, "nt": 0, "lanes": 0, "wide": 0}]
-            + [{"kernel": 2, "nt": 0, "lanes": g, "wide": w} for w in (0, 1) for g in (2, 4, 8)])
+            + [{"kernel": 2, "nt": 0, "lanes": g, "wide": w} for w in (1, 2) for g in (2, 4, 8, 16)])
 
 
 def main():

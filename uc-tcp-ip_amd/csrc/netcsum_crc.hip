@@ -152,6 +152,54 @@ constexpr CrcWide make_wide() {
 }
 
 __device__ const CrcWide kWideTabs = make_wide();
+
+// 6-bit slicing with lane-private replicas (conflict-free): six tables indexed by register bits
+// [0, 6), [6, 12), .., [24, 30) and [30, 32) (64, .., 64, 4 entries, 324 in all). ds_read_b32 serves a
+// wave in two 32-lane groups and its bank is (address / 4) mod 32 (MI355X_MICROARCH.md, LDS table),
+// so LDS entry e of a map is stored 32 times, lane l's copy at word 32 e + (l mod 32): the 32 lanes
+// of a group always hit 32 different banks, whatever their indices. 40.5 KiB per map in LDS; random
+// lookups into the byte / 11-bit tables cost 6.4 LDS cycles per instruction, 4.4 of them bank
+// conflicts (profiles/r2zd_crc_lds_pmc.json), these 2.
+constexpr int kK6 = 324;
+constexpr int kK6Lds = kK6 * 32;                                // words per replicated map
+
+struct CrcK6 {
+    uint32_t m[kNumWide][kK6];
+};
+
+constexpr CrcK6 make_k6() {
+    const CrcTabs t = make_tabs();
+    const int src[kNumWide] = {kSetT, kSetZ16, kSetZ8, kSetZ4, kSetZ2};
+    CrcK6 r{};
+    for (int m = 0; m < kNumWide; ++m) {
+        const uint32_t(&S)[4][256] = t.s[src[m]];
+        auto ap = [&](uint32_t c) {
+            return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
+        };
+        for (int j = 0; j < 6; ++j) {
+            for (uint32_t e = 0; e < (j < 5 ? 64u : 4u); ++e) {
+                r.m[m][64 * j + (int)e] = ap(e << (6 * j));
+            }
+        }
+    }
+    return r;
+}
+
+__device__ const CrcK6 kK6Tabs = make_k6();
+
+// Replicate map m of kK6Tabs into dst (kK6Lds words). No barrier: the caller's.
+template <int B>
+__device__ __forceinline__ void fill_k6(uint32_t* dst, int m) {
+    for (int i = (int)threadIdx.x; i < kK6Lds; i += B) {
+        dst[i] = kK6Tabs.m[m][i >> 5];
+    }
+}
+
+// R = the map's replica base + (lane mod 32): six conflict-free lookups.
+__device__ __forceinline__ uint32_t apply_k6(const uint32_t* R, uint32_t c) {
+    return R[32u * (c & 63u)] ^ R[32u * (64u + ((c >> 6) & 63u))] ^ R[32u * (128u + ((c >> 12) & 63u))] ^
+           R[32u * (192u + ((c >> 18) & 63u))] ^ R[32u * (256u + ((c >> 24) & 63u))] ^ R[32u * (320u + (c >> 30))];
+}
 static_assert(make_tabs().s[kSetT][3][1] == 0x77073096u, "byte table of the reflected IEEE polynomial");
 static_assert(make_tabs().s[kSetT][3][255] == 0x2D02EF8Du, "byte table of the reflected IEEE polynomial");
 
@@ -333,32 +381,45 @@ constexpr int kRound = 4;               // chunks per lane per round (one round 
 
 constexpr int log2i(int g) { return g <= 1 ? 0 : 1 + log2i(g / 2); }
 
-// W11: chunk steps with the 11-bit tables (blocks of 512 threads), else the byte tables (256).
-template <int G, bool NT, bool W11>
-__global__ void __launch_bounds__(W11 ? 512 : 256) crc_ilv_kernel(CrcBatchArgs A) {
-    constexpr uint32_t B = W11 ? 512u : 256u;
+// Table form of the chunk steps: W = 0 byte tables (256-thread blocks), 1 11-bit tables (512),
+// 2 lane-replicated 6-bit tables (1024; one block per CU).
+constexpr uint32_t ilv_block(int w) { return w == 2 ? 1024u : w == 1 ? 512u : 256u; }
+
+template <int G, bool NT, int W>
+__global__ void __launch_bounds__(ilv_block(W)) crc_ilv_kernel(CrcBatchArgs A) {
+    constexpr uint32_t B = ilv_block(W);
     constexpr int kLevels = log2i(G);                           // combine levels: A^16 .. A^(8 G)
     constexpr int kZ = kLevels + 1;                             // LDS slot of this G's Z (byte tables)
     constexpr int kZset = G == 16 ? kSetZ16 : G == 8 ? kSetZ8 : G == 4 ? kSetZ4 : G == 2 ? kSetZ2 : kSetT;
     constexpr int kZwide = G == 16 ? kWideZ16 : G == 8 ? kWideZ8 : G == 4 ? kWideZ4 : G == 2 ? kWideZ2 : kWideT;
-    // T, A^16.., Z: 8 .. 24 KiB (byte tables); T, A^16.. + 2 x 20 KiB wide maps (W11)
-    __shared__ uint32_t L[W11 ? kLevels + 1 : kLevels + 2][4][256];
-    __shared__ uint32_t LW[W11 ? 2 : 1][W11 ? kWide : 1];
-    copy_sets<B>(L, kLevels + 1, W11 ? -1 : kZset);
-    if constexpr (W11) {
+    // byte tables: T, A^16.., Z (8 .. 24 KiB); W 1: T, A^16.. + 2 x 20 KiB; W 2: T, A^16.. + 2 x 40.5 KiB
+    constexpr int kWords = W == 2 ? kK6Lds : W == 1 ? kWide : 1;
+    __shared__ uint32_t L[W != 0 ? kLevels + 1 : kLevels + 2][4][256];
+    __shared__ uint32_t LW[W != 0 ? 2 : 1][kWords];
+    copy_sets<B>(L, kLevels + 1, W != 0 ? -1 : kZset);
+    if constexpr (W == 1) {
         copy_wide<B>(LW[0], kWideT);
         copy_wide<B>(LW[1], kZwide);
+    } else if constexpr (W == 2) {
+        fill_k6<B>(LW[0], kWideT);
+        fill_k6<B>(LW[1], kZwide);
     }
     __syncthreads();
+    const uint32_t* RT = &LW[0][threadIdx.x & 31u];             // W 2: this lane's replicas
+    const uint32_t* RZ = &LW[W != 0 ? 1 : 0][threadIdx.x & 31u];
     auto step = [&](uint32_t c, uint32_t w, bool last) -> uint32_t {   // T (last) or Z on c ^ w
-        if constexpr (W11) {
+        if constexpr (W == 2) {
+            return apply_k6(last ? RT : RZ, c ^ w);
+        } else if constexpr (W == 1) {
             return apply_wide(last ? LW[0] : LW[1], c ^ w);
         } else {
             return crc_word(last ? L[0] : L[kZ], c, w);
         }
     };
     auto step_t = [&](uint32_t c, uint32_t w) -> uint32_t {
-        if constexpr (W11) {
+        if constexpr (W == 2) {
+            return apply_k6(RT, c ^ w);
+        } else if constexpr (W == 1) {
             return apply_wide(LW[0], c ^ w);
         } else {
             return crc_word(L[0], c, w);
@@ -558,7 +619,7 @@ uint32_t h_x8n(uint64_t n) {
 std::atomic<int> g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL (netcsum_mi355x.h)
 std::atomic<int> g_crc_lanes{0};       // NETCSUM_TUNE_CRC_LANES: interleaved lanes per segment, 0 auto
 std::atomic<int> g_crc_nt{0};          // NETCSUM_TUNE_CRC_NT: non-temporal chunk loads (interleaved form)
-std::atomic<int> g_crc_wide{1};        // NETCSUM_TUNE_CRC_WIDE: 11-bit tables (interleaved form)
+std::atomic<int> g_crc_wide{1};        // NETCSUM_TUNE_CRC_WIDE: 0 byte, 1 11-bit, 2 lane-replicated 6-bit tables
 
 enum class CrcForm { Lane, Block, Ilv1, Ilv2, Ilv4, Ilv8, Ilv16 };
 
@@ -590,20 +651,23 @@ void set_crc_nt(int v) { g_crc_nt.store(v); }
 void set_crc_wide(int v) { g_crc_wide.store(v); }
 
 const char* crc_launch_name(uint32_t max_len, bool varlen) {
-    // [wide][nt][log2 G]: "crc_ilv_kernel<nt,w11> G=4 block=512", ...
+    // [table form][nt][log2 G]: "crc_ilv_kernel<nt,w11> G=4 block=512", ...
     static const std::vector<std::string> names = [] {
         std::vector<std::string> v;
-        for (int w = 0; w < 2; ++w) {
+        for (int w = 0; w < 3; ++w) {
             for (int nt = 0; nt < 2; ++nt) {
                 for (int g = 1; g <= 16; g *= 2) {
-                    std::string t = nt ? (w ? "<nt,w11>" : "<nt>") : (w ? "<w11>" : "");
-                    v.push_back("crc_ilv_kernel" + t + " G=" + std::to_string(g) + (w ? " block=512" : " block=256"));
+                    std::string t = nt ? "nt" : "";
+                    if (w != 0) t += std::string(t.empty() ? "" : ",") + (w == 1 ? "w11" : "k6");
+                    v.push_back("crc_ilv_kernel" + (t.empty() ? t : "<" + t + ">") + " G=" + std::to_string(g) +
+                                " block=" + std::to_string(ilv_block(w)));
                 }
             }
         }
         return v;
     }();
-    const int base = (g_crc_wide.load() != 0 ? 10 : 0) + (g_crc_nt.load() != 0 ? 5 : 0);
+    const int w = std::min(std::max(g_crc_wide.load(), 0), 2);
+    const int base = 10 * w + (g_crc_nt.load() != 0 ? 5 : 0);
     switch (crc_form(max_len, varlen)) {
     case CrcForm::Lane: return "crc_lane_kernel block=256";
     case CrcForm::Block: return "crc_group_kernel G=16 block=256";
@@ -615,26 +679,27 @@ const char* crc_launch_name(uint32_t max_len, bool varlen) {
     }
 }
 
-template <int G, bool W11>
+template <int G, int W>
 static void launch_ilv_w(const CrcBatchArgs& a, uint32_t cu, hipStream_t s) {
-    constexpr uint32_t B = W11 ? 512u : 256u;
+    constexpr uint32_t B = ilv_block(W);
     const uint32_t steps = (a.n + (B / G) - 1u) / (B / G);
-    // blocks resident per CU by LDS: byte tables 24 / 20 / <= 16 KiB (256 threads); W11 44 .. 60 KiB (512)
-    const uint32_t per_cu = W11 ? (G >= 8 ? 2u : 3u) : (G == 16 ? 6u : G == 8 ? 8u : 10u);
+    // blocks resident per CU by LDS: byte tables 24 / 20 / <= 16 KiB (256 threads); W 1 44 .. 60 KiB
+    // (512); W 2 85 .. 97 KiB (1024)
+    const uint32_t per_cu = W == 2 ? 1u : W == 1 ? (G >= 8 ? 2u : 3u) : (G == 16 ? 6u : G == 8 ? 8u : 10u);
     const uint32_t grid = std::min<uint32_t>(steps, cu * per_cu);
     if (g_crc_nt.load()) {
-        hipLaunchKernelGGL((crc_ilv_kernel<G, true, W11>), dim3(grid), dim3(B), 0, s, a);
+        hipLaunchKernelGGL((crc_ilv_kernel<G, true, W>), dim3(grid), dim3(B), 0, s, a);
     } else {
-        hipLaunchKernelGGL((crc_ilv_kernel<G, false, W11>), dim3(grid), dim3(B), 0, s, a);
+        hipLaunchKernelGGL((crc_ilv_kernel<G, false, W>), dim3(grid), dim3(B), 0, s, a);
     }
 }
 
 template <int G>
 static void launch_ilv(const CrcBatchArgs& a, uint32_t cu, hipStream_t s) {
-    if (g_crc_wide.load()) {
-        launch_ilv_w<G, true>(a, cu, s);
-    } else {
-        launch_ilv_w<G, false>(a, cu, s);
+    switch (g_crc_wide.load()) {
+    case 0: launch_ilv_w<G, 0>(a, cu, s); break;
+    case 2: launch_ilv_w<G, 2>(a, cu, s); break;
+    default: launch_ilv_w<G, 1>(a, cu, s); break;
     }
 }
 
