@@ -312,9 +312,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; a box with fewer GPUs than local ranks (a rehearsal) folds them onto its devices
+    local = local % max(1, torch.cuda.device_count())
+    # RCCL ("nccl") carries the barrier and the two reductions; NETCSUM_BENCH_DIST_BACKEND=gloo (host
+    # tensors) lets several ranks share one GPU to rehearse the N > 1 path (RCCL refuses duplicate GPUs)
+    backend = os.environ.get("NETCSUM_BENCH_DIST_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -372,7 +380,7 @@ def main():
     kern_med_ms = kern[len(kern) // 2]
 
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
@@ -414,7 +422,7 @@ def main():
 
     parity_all = parity_ok
     if world > 1:                                  # every rank's sample must match its oracle
-        t = torch.tensor([1 if parity_ok is True else 0], dtype=torch.int32, device=dev)
+        t = torch.tensor([1 if parity_ok is True else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         parity_all = bool(t.item()) if not isinstance(parity_ok, str) else parity_ok
 
