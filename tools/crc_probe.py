@@ -26,12 +26,16 @@ VARIANTS = ([{"kernel": 0, "nt": 0, "lanes": 0, "wide": 1}, {"kernel": 1, "nt": 
 
 def main():
     passes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None      # e.g. "6,20": those lengths only
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
     work = []
     # strided frames: (n, length, stride)
     for n, L, S in ((1 << 20, 1500, 1500), (1 << 20, 1514, 1518), (1 << 18, 9000, 9000), (1 << 22, 300, 300),
-                    (1 << 22, 600, 600), (1 << 23, 64, 64), (1 << 23, 128, 128), (1 << 22, 256, 256)):
+                    (1 << 22, 600, 600), (1 << 23, 64, 64), (1 << 23, 128, 128), (1 << 22, 256, 256),
+                    (1 << 24, 6, 6), (1 << 24, 20, 20)):
+        if only and str(L) not in only:
+            continue
         buf = torch.empty(n * S + 64, dtype=torch.uint8, device=dev)
         netcsum.fill(buf, n * S, SEED, 0)
         out = torch.empty(n, dtype=torch.int32, device=dev)
