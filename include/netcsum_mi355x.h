@@ -468,8 +468,12 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_CRC_NT        = 16,  /* CRC-32 interleaved form: 1 non-temporal chunk loads, 0 plain */
     NETCSUM_TUNE_CRC_LANES     = 17,  /* CRC-32 interleaved form: lanes per segment, 1, 2, 4, 8, 16;
                                          0 auto (8 for strided segments >= 1 KiB, else 4)             */
-    NETCSUM_TUNE_CRC_WIDE      = 18   /* CRC-32 interleaved form: 1 (default) 11-bit slicing tables
-                                         (3 LDS lookups per dword), 0 byte tables (4)                 */
+    NETCSUM_TUNE_CRC_WIDE      = 18,  /* CRC-32 interleaved form: 1 (default) 11-bit slicing tables
+                                         (3 LDS lookups per dword), 0 byte tables (4), 2 lane-private
+                                         6-bit replicas (6, conflict-free)                            */
+    NETCSUM_TUNE_HDR_BURST     = 19   /* header stream kernel (C3): 1 = a run's results gathered in LDS
+                                         and written as whole 16-B pieces, 0 = one store per piece,
+                                         -1 = the default                                             */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

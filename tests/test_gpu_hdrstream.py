@@ -23,6 +23,7 @@ def _tuning():
         netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
         netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
+        netcsum.tune(netcsum.TUNE_HDR_BURST, -1)
     reset()
     yield
     reset()
@@ -39,9 +40,12 @@ def _run(host, lead, L, n, op):
 
 @pytest.mark.parametrize("L", [20, 16])
 @pytest.mark.parametrize("spw,depth,nt,xcd,touch", [(1024, 4, 1, -1, -1), (1, 4, 1, 1, 0), (7, 8, 0, -1, 1),
-                                                    (64, 8, 1, 1, -1), (4096, 4, 0, 0, 0), (192, 4, 1, 1, 1)])
-def test_hdrstream_vs_oracle(L, spw, depth, nt, xcd, touch):
+                                                    (64, 8, 1, 1, -1), (4096, 4, 0, 0, 0), (192, 4, 1, 1, 1),
+                                                    (16, 4, 1, 0, 1), (384, 8, 1, -1, 1)])
+@pytest.mark.parametrize("burst", [0, 1])      # results per run through LDS (spw <= 384, multiple of 16) or per piece
+def test_hdrstream_vs_oracle(L, spw, depth, nt, xcd, touch, burst):
     netcsum.tune(netcsum.TUNE_KERNEL, 8)
+    netcsum.tune(netcsum.TUNE_HDR_BURST, burst)
     netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)                   # launch options: block order, row touch
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
     netcsum.tune(netcsum.TUNE_TILE, spw)

@@ -37,8 +37,11 @@ def main():
     touch_l = [int(x) for x in os.environ.get("C3_TOUCH", "-1").split(",")]
     xcd_l = [int(x) for x in os.environ.get("C3_XCD", "-1").split(",")]
     d_l = [int(x) for x in os.environ.get("C3_D", "4,8").split(",")]
-    for spw, d, nt, w, tch, xc in [(spw, d, nt, w, t, xc) for spw in spws for d in d_l for nt in (1,) for w in waves_l
-                                   for t in touch_l for xc in xcd_l]:
+    burst_l = [int(x) for x in os.environ.get("C3_BURST", "-1").split(",")]
+    passes = int(os.environ.get("C3_PASSES", "1"))
+    for spw, d, nt, w, tch, xc, bu in [(spw, d, nt, w, t, xc, bu) for _ in range(passes) for spw in spws for d in d_l
+                                       for nt in (1,) for w in waves_l for t in touch_l for xc in xcd_l for bu in burst_l]:
+                netcsum.tune(netcsum.TUNE_HDR_BURST, bu)
                 netcsum.tune(netcsum.TUNE_STREAM_XCD, xc)
                 netcsum.tune(netcsum.TUNE_STREAM_WAVES, w)
                 netcsum.tune(netcsum.TUNE_STREAM_TOUCH, tch)
@@ -51,13 +54,14 @@ def main():
                 r = out.clone()
                 same = True if ref is None else bool(torch.equal(r, ref))
                 ref = r if ref is None else ref
-                print(json.dumps({"variant": dict(kernel=8, spw=spw, d=d, nt=nt, waves=w, touch=tch, xcd=xc),
+                print(json.dumps({"variant": dict(kernel=8, spw=spw, d=d, nt=nt, waves=w, touch=tch, xcd=xc, burst=bu),
                                   "kernel": netcsum.last_launch(),
                                   "ms": round(ms, 4), "GBps_algo": round(algo / ms / 1e6, 1), "same": same}), flush=True)
     netcsum.tune(netcsum.TUNE_NT_LOADS, -1)
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
     netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
+    netcsum.tune(netcsum.TUNE_HDR_BURST, -1)
     if os.environ.get("C3_NO_K7"):
         return
     for h in (2, 4):

@@ -945,6 +945,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         }
         netcsum::set_crc_lanes(value);
         return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_HDR_BURST:
+        if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_hdr_burst(value);
+        return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_CRC_WIDE:
         if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_crc_wide(value);

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
 #include "netcsum_stream.h"
@@ -35,7 +37,12 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-template <int M, int D, bool NT>
+// BURST: a whole run's results (spw <= kBurstMax) are gathered in LDS and written by one store
+// instruction of whole 16-B pieces (the run's 2 spw or spw result bytes are 16-B aligned and
+// contiguous), instead of one 2-B (1-B) store instruction per piece; a short last run stores per piece.
+constexpr uint32_t kBurstMax = 384u;
+
+template <int M, int D, bool NT, bool BURST>
 __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -64,6 +71,8 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
     const __amdgpu_buffer_rsrc_t ro = run_rsrc((uintptr_t)(((uint64_t)ob_hi << 32) | ob_lo),
                                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(nres * (verify ? 1u : 2u))));
     const uint32_t lane16 = 16u * lane;
+    __shared__ __attribute__((aligned(16))) uint32_t res[BURST ? 4 : 1][BURST ? kBurstMax / 2 : 1];   // 768 B per wave
+    const bool burst = BURST && nres == spw && spw <= kBurstMax && (spw & 15u) == 0u;   // wave-uniform
 
     u32x4 dv[D];
 #pragma unroll
@@ -103,7 +112,15 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
         carry = (uint32_t)__builtin_amdgcn_readlane((int)Bl, 63);
         const uint32_t k = hp ? (uint32_t)((rp + bp - r0) / M) : 0u;   // run-relative header index
         const uint32_t t = fold16(Bp + Al);
-        if (verify) {
+        if (burst) {
+            if (hp) {
+                if (verify) {
+                    reinterpret_cast<uint8_t*>(res[w])[k] = (uint8_t)(t == 0xFFFFu ? 1u : 0u);
+                } else {
+                    reinterpret_cast<uint16_t*>(res[w])[k] = (uint16_t)(~t);
+                }
+            }
+        } else if (verify) {
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(t == 0xFFFFu ? 1u : 0u), ro, (int)(hp ? k : kOOB), 0, 0);
         } else {
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(~t), ro, (int)(hp ? 2u * k : kOOB), 0, 0);
@@ -127,9 +144,27 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
             asm volatile("" ::: "memory");
         }
     }
+    if (burst) {                       // the wave's LDS writes retire in order before its reads
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t nbytes = verify ? spw : 2u * spw;
+        if (lane16 < nbytes) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint8_t*>(res[w]) + lane16);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)lane16, 0, 0);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     touch_retire(touch);
 }
+
+std::atomic<int> g_hdr_burst{-1};      // NETCSUM_TUNE_HDR_BURST: -1 default (kHdrBurstDefault), 0, 1
+constexpr bool kHdrBurstDefault = true;     // C3 0.0584 -> 0.0571-0.0575 ms (profiles/r2zi_c3_burst_sweep.jsonl)
+
+}  // namespace
+
+void set_hdr_burst(int v) { g_hdr_burst.store(v); }
+bool hdr_burst() { const int v = g_hdr_burst.load(); return v < 0 ? kHdrBurstDefault : v > 0; }
+
+namespace {
 
 template <int M, int D, bool NT>
 hipError_t launch_hs_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
@@ -137,12 +172,17 @@ hipError_t launch_hs_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     a.touch = stream_touch(true) ? 1u : 0u;
     a.xcd = stream_xcd(false) ? 1u : 0u;   // r2x: 0.0579-0.0584 ms off vs 0.0589 on
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
-    hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT>), dim3((unsigned)((waves + 3u) / 4u)), dim3(256),
-                       stream_lds_bytes(0), s, a, spw);
+    const dim3 grid((unsigned)((waves + 3u) / 4u));
+    if (hdr_burst()) {
+        hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT, true>), grid, dim3(256), stream_lds_bytes(0), s, a, spw);
+    } else {
+        hipLaunchKernelGGL((seg_hdrstream_kernel<M, D, NT, false>), grid, dim3(256), stream_lds_bytes(0), s, a, spw);
+    }
     return hipGetLastError();
 }
 
 }  // namespace
+
 
 // Packed (stride == len), no pseudo-header, len 16 or 20, base a multiple of 4; runs < 2^31 bytes.
 bool hdrstream_supported(const SegBatchArgs& a) {

@@ -116,6 +116,8 @@ uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
+void set_hdr_burst(int v);     // NETCSUM_TUNE_HDR_BURST: header stream results written per run (1) or per piece (0)
+bool hdr_burst();
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
 // Tx finalize write-back of the dirty field lines (NETCSUM_TUNE_TX_FLUSH): -1 / 0 none, 1 scatter
 // stores at system scope, 2 release at the end of every scatter wave, 3 / 4 a write-back launch of

@@ -973,8 +973,8 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
                                   "seg_small_kernel", "seg_stream_kernel", "seg_hdr_kernel", "seg_hdrstream_kernel"};
     const int kid = (c.kernel >= 1 && c.kernel <= 8) ? c.kernel : 0;
     if (kid == 8) {
-        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdrstream_kernel<M=%u,D=%d%s> block=256 hdrs_per_wave=%u",
-                 a.seg_len / 4u, c.chunks_per_pass, c.nt ? ",nt" : "", c.stream_spw);
+        snprintf(g_last_launch, sizeof(g_last_launch), "seg_hdrstream_kernel<M=%u,D=%d%s%s> block=256 hdrs_per_wave=%u",
+                 a.seg_len / 4u, c.chunks_per_pass, c.nt ? ",nt" : "", hdr_burst() ? ",burst" : "", c.stream_spw);
         return;
     }
     if (kid == 7) {

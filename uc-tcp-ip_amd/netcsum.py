@@ -60,6 +60,7 @@ TUNE_CRC_KERNEL = 15
 TUNE_CRC_NT = 16
 TUNE_CRC_LANES = 17
 TUNE_CRC_WIDE = 18
+TUNE_HDR_BURST = 19
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
