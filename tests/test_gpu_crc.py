@@ -63,7 +63,7 @@ def expected_kernel(form, length, varlen=False):
     kern, nt, lanes, wide = form
     short = length <= 96 and not varlen
     if kern == 3 or (kern in (0, 1) and short):
-        return "crc_lane_kernel "
+        return "crc_tiny_kernel " if (length <= 16 and not varlen) else "crc_lane_kernel "
     if kern == 1:
         return "crc_group_kernel G=16 "
     tag = ",".join(t for t, on in (("nt", nt), ("w11", wide == 1), ("k6", wide == 2)) if on)

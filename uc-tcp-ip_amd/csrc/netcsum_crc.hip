@@ -274,6 +274,29 @@ __device__ __forceinline__ uint32_t crc_16(const uint32_t (*T)[256], uint32_t c,
     return crc_word(T, c, win16_dword(a, b, sh, 3));
 }
 
+// Register c advanced over the rem <= 16 octets starting sh bytes into the 32-B window [v0, v1].
+__device__ __forceinline__ uint32_t crc_window(const uint32_t (*T)[256], uint32_t c, const uint4& v0, const uint4& v1,
+                                               uint32_t sh, uint32_t rem) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = 4u * (uint32_t)i;
+        if (lo < rem) {
+            const uint32_t w = win16_dword(v0, v1, sh, i);
+            if (lo + 4u <= rem) {
+                c = crc_word(T, c, w);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    if (lo + (uint32_t)b < rem) {
+                        c = crc_byte(T, c, (w >> (8 * b)) & 0xFFu);
+                    }
+                }
+            }
+        }
+    }
+    return c;
+}
+
 // Register c advanced over bytes [p, p + n): whole ALIGNED 16-B loads (a chunk holding any byte of
 // the range lies in the range's pages, so reading all of it cannot fault), 64 B of the range per
 // step from five loads issued together, the stream's dwords cut out by v_alignbyte_b32; the last
@@ -344,6 +367,46 @@ __global__ void __launch_bounds__(256) crc_lane_kernel(CrcBatchArgs A) {
         uint32_t len;
         seg_desc(A, i, p, len);
         A.out[i] = crc_finish(crc_range(L[0], 0xFFFFFFFFu, p, len), len, A.cpl != 0u);
+    }
+}
+
+// Strided segments of <= 16 B (the drivers' 6-B MAC addresses): one lane each, and the two aligned
+// chunks of the lane's NEXT segment are loaded before its current one is computed (one load round
+// trip per segment otherwise bounds the persistent loop: 0.0645 ms for 16 M MACs, 0.0416 with it).
+// The address of a segment past the batch is clamped to the current one, so every load is issued on
+// every path; global (not flat) loads, since a flat load is waited for with lgkmcnt(0) at once.
+__global__ void __launch_bounds__(256) crc_tiny_kernel(CrcBatchArgs A) {
+    __shared__ uint32_t L[1][4][256];
+    load_sets(L, 1, -1);
+    const uint32_t step = gridDim.x * 256u;
+    const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
+    auto win = [&](uint32_t i, u32x4& v0, u32x4& v1) {
+        const uintptr_t a = (uintptr_t)(A.base + (uint64_t)i * A.stride);
+        const uintptr_t q = a & ~(uintptr_t)15u;
+        v0 = load16<false>(reinterpret_cast<gu32x4*>(q));
+        v1 = load16<false>(reinterpret_cast<gu32x4*>(q + ((a & 15u) + A.len > 16u ? 16u : 0u)));
+    };
+    auto emit = [&](uint32_t i, const u32x4& v0, const u32x4& v1) {
+        const uint32_t sh = (uint32_t)((uintptr_t)(A.base + (uint64_t)i * A.stride) & 15u);
+        const uint4 w0{v0.x, v0.y, v0.z, v0.w}, w1{v1.x, v1.y, v1.z, v1.w};
+        const uint32_t c = A.len ? crc_window(L[0], 0xFFFFFFFFu, w0, w1, sh, A.len) : 0u;
+        A.out[i] = crc_finish(c, A.len, A.cpl != 0u);
+    };
+    if (i0 >= A.n) {
+        return;
+    }
+    // two segments per trip in alternating registers (a copy of a register a load is still filling
+    // would wait for that load)
+    u32x4 a0, a1, b0, b1;
+    win(i0, a0, a1);
+    for (uint32_t i = i0; i < A.n; i += 2u * step) {
+        const uint32_t j = i + step, k = i + 2u * step;
+        win(j < A.n ? j : i, b0, b1);
+        emit(i, a0, a1);
+        win(k < A.n ? k : i, a0, a1);
+        if (j < A.n) {
+            emit(j, b0, b1);
+        }
     }
 }
 
@@ -689,7 +752,7 @@ const char* crc_launch_name(uint32_t max_len, bool varlen) {
     const int w = std::min(std::max(g_crc_wide.load(), 0), 2);
     const int base = 10 * w + (g_crc_nt.load() != 0 ? 5 : 0);
     switch (crc_form(max_len, varlen)) {
-    case CrcForm::Lane: return "crc_lane_kernel block=256";
+    case CrcForm::Lane: return !varlen && max_len <= 16u ? "crc_tiny_kernel block=256" : "crc_lane_kernel block=256";
     case CrcForm::Block: return "crc_group_kernel G=16 block=256";
     case CrcForm::Ilv1: return names[base + 0].c_str();
     case CrcForm::Ilv2: return names[base + 1].c_str();
@@ -731,7 +794,11 @@ hipError_t launch_crc_batch(const CrcBatchArgs& a0, uint32_t max_len, int cus, h
     switch (crc_form(max_len, varlen)) {
     case CrcForm::Lane: {
         const uint32_t grid = std::min<uint32_t>((a.n + 255u) / 256u, cu * 8u);   // LDS 4 KiB per block
-        hipLaunchKernelGGL(crc_lane_kernel, dim3(grid), dim3(256), 0, s, a);
+        if (!varlen && a.off == nullptr && a.len <= 16u) {
+            hipLaunchKernelGGL(crc_tiny_kernel, dim3(grid), dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(crc_lane_kernel, dim3(grid), dim3(256), 0, s, a);
+        }
         break;
     }
     case CrcForm::Block: {
