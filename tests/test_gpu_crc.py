@@ -186,3 +186,18 @@ def test_crc_varlen_every_length_and_alignment(crc_form):
     got = out.cpu().numpy().view(np.uint32)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(lens[i]), int(off[i] % 16), hex(got[i]), hex(want[i])) for i in bad[:6]]
+
+
+@pytest.mark.parametrize("crc_kernel", [0, 2, 3])
+def test_crc_batch_strided_empty_segments(crc_kernel):
+    """len 0: every result 0 (the reference's NET_UTIL_ERR_NULL_SIZE value), nothing read."""
+    netcsum.tune(netcsum.TUNE_CRC_KERNEL, crc_kernel)
+    try:
+        n = 5000
+        d = torch.full((n * 6 + 64,), 0xAB, dtype=torch.uint8, device=DEV)
+        out = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+        netcsum.crc32_strided(d, 6, 0, n, out, 1)
+        torch.cuda.synchronize()
+        assert bool((out == 0).all())
+    finally:
+        netcsum.tune(netcsum.TUNE_CRC_KERNEL, 0)

@@ -389,10 +389,15 @@ __global__ void __launch_bounds__(256) crc_tiny_kernel(CrcBatchArgs A) {
     auto emit = [&](uint32_t i, const u32x4& v0, const u32x4& v1) {
         const uint32_t sh = (uint32_t)((uintptr_t)(A.base + (uint64_t)i * A.stride) & 15u);
         const uint4 w0{v0.x, v0.y, v0.z, v0.w}, w1{v1.x, v1.y, v1.z, v1.w};
-        const uint32_t c = A.len ? crc_window(L[0], 0xFFFFFFFFu, w0, w1, sh, A.len) : 0u;
-        A.out[i] = crc_finish(c, A.len, A.cpl != 0u);
+        A.out[i] = crc_finish(crc_window(L[0], 0xFFFFFFFFu, w0, w1, sh, A.len), A.len, A.cpl != 0u);
     };
     if (i0 >= A.n) {
+        return;
+    }
+    if (A.len == 0u) {                 // empty segments (the base may be NULL then): 0, nothing read
+        for (uint32_t i = i0; i < A.n; i += step) {
+            A.out[i] = 0u;
+        }
         return;
     }
     // two segments per trip in alternating registers (a copy of a register a load is still filling
