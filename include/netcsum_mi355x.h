@@ -471,9 +471,12 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_CRC_WIDE      = 18,  /* CRC-32 interleaved form: 1 (default) 11-bit slicing tables
                                          (3 LDS lookups per dword), 0 byte tables (4), 2 lane-private
                                          6-bit replicas (6, conflict-free)                            */
-    NETCSUM_TUNE_HDR_BURST     = 19   /* header stream kernel (C3): 1 = a run's results gathered in LDS
+    NETCSUM_TUNE_HDR_BURST     = 19,  /* header stream kernel (C3): 1 = a run's results gathered in LDS
                                          and written as whole 16-B pieces, 0 = one store per piece,
                                          -1 = the default                                             */
+    NETCSUM_TUNE_VARLEN_RUN_BYTES = 20 /* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
+                                         run length chosen on the device from sampled lengths; 0 =
+                                         runs of 8 segments; -1 = the default (16 KiB)                 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -558,3 +558,32 @@ def test_sum_align32_hook_matches_reference_inner_sum():
             assert hb.ptr % 4 == 0
             want = sum(int.from_bytes(data[i:i + 2], "big") for i in range(0, size, 2)) & 0xFFFFFFFF
             assert netcsum.SumDataCalcAlign_32(hb.ptr, size) == want, (size, pat)
+
+
+@pytest.mark.parametrize("run_bytes", [0, 1, 4096, 16384, 1 << 20])
+def test_varlen_adaptive_runs_vs_oracle(run_bytes):
+    """The varlen stream kernel's device-chosen run length (NETCSUM_TUNE_VARLEN_RUN_BYTES: 0 = fixed
+    runs of 8; 1 -> the shortest run the grid covers, 3; 2^20 -> the longest, 128): every segment is
+    covered exactly once whatever the sampled mean, for batches smaller and larger than the 4096
+    samples, with long, short and empty segments and packed or reversed layouts."""
+    rng = np.random.default_rng(run_bytes + 11)
+    netcsum.tune(netcsum.TUNE_VARLEN_RUN_BYTES, run_bytes)
+    try:
+        for n, lo, hi in ((1, 40, 9000), (7, 0, 300), (300, 40, 1500), (5000, 40, 9000), (20000, 0, 600)):
+            base, off, lens, ph = _packed_udp(rng, n, lo, hi)
+            lens[::13] = 0
+            if n > 1000:
+                off, lens = off[::-1].copy(), lens[::-1].copy()      # not packed: the group path
+            base_d, off_d = torch.from_numpy(base).to(DEV), torch.from_numpy(off.view(np.int64)).to(DEV)
+            len_d, ph_d = torch.from_numpy(lens.view(np.int16)).to(DEV), torch.from_numpy(ph).to(DEV)
+            for op in (0, 1):
+                out = _out(n, op)
+                netcsum.batch_varlen(base_d, off_d, len_d, ph_d, 12, 12, n, out, op)
+                torch.cuda.synchronize()
+                kern = netcsum.last_launch()
+                assert kern.startswith("seg_stream_varlen_kernel"), kern
+                assert ("adaptive" in kern) == (run_bytes != 0), kern
+                want = oracle.batch_varlen(base, off, lens, ph, 12, 12, op)
+                assert np.array_equal(_np_out(out), want), (n, op, kern)
+    finally:
+        netcsum.tune(netcsum.TUNE_VARLEN_RUN_BYTES, -1)

@@ -208,8 +208,11 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
             } else if (c.grid_mult > 1) {
                 waves = (uint64_t)netcsum::stream_occupancy(d, a, c.nt) * 4u * (uint64_t)c.cus * (uint64_t)c.grid_mult;
             } else {
-                // runs of 16 segments for dense batches (C2), 8 for varlen ones (C4, r2ct)
-                const uint64_t run = varlen ? 8u : 16u;
+                // runs of 16 segments for dense batches (C2); varlen ones (C4) size their runs on the
+                // device to about RUN_BYTES (launch_batch), the grid covering the shortest run, or take
+                // runs of 8 (r2ct) with VARLEN_RUN_BYTES 0
+                c.run_bytes = varlen ? netcsum::varlen_run_bytes() : 0u;
+                const uint64_t run = !varlen ? 16u : c.run_bytes ? netcsum::kVarlenSpwMin : 8u;
                 waves = ((uint64_t)a.n_seg + run - 1u) / run;
             }
             c.stream_spw = netcsum::stream_spw(a, waves);
@@ -341,10 +344,21 @@ hipError_t stream_scratch(int dev, hipStream_t st, size_t bytes, void** out) {
     return hipSuccess;
 }
 
-NET_ERR launch_batch(const netcsum::SegBatchArgs& a, uint32_t len_hint, hipStream_t s) {
+NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStream_t s) {
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
-    const netcsum::LaunchCfg c = choose_cfg(dev, a, len_hint);
+    const netcsum::LaunchCfg c = choose_cfg(dev, a0, len_hint);
+    netcsum::SegBatchArgs a = a0;
+    if (c.kernel == 6 && c.run_bytes != 0u && a.seg_off != nullptr) {
+        // adaptive varlen runs: a one-block kernel samples the lengths and leaves the run length in
+        // this stream's scratch word, which the batch kernel reads (stream order; any value is safe:
+        // the kernel never runs shorter runs than its grid covers)
+        void* word = nullptr;
+        NC_HIP(stream_scratch(dev, s, 256u, &word));
+        NC_HIP(netcsum::launch_varlen_runlen(a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
+                                             c.stream_spw, static_cast<uint32_t*>(word), s));
+        a.run_dev = static_cast<const uint32_t*>(word);
+    }
     NC_HIP(netcsum::launch_seg_batch(a, c, s));
     return NET_UTIL_ERR_NONE;
 }
@@ -944,6 +958,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
             return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         }
         netcsum::set_crc_lanes(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_VARLEN_RUN_BYTES:
+        if (value < -1 || value > (1 << 20)) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_varlen_run_bytes(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_HDR_BURST:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

@@ -21,6 +21,8 @@ struct SegBatchArgs {
     void*           out;
     uint32_t        touch;         // run-stream kernels: row-touch prologue (set by the launcher)
     uint32_t        xcd;           // stream kernels: XCD-aware block order (set by the launcher)
+    const uint32_t* run_dev;       // varlen stream kernel: run length chosen on the device (used when
+                                   // larger than the launch's), nullptr = the launch's
 };
 
 struct LaunchCfg {
@@ -41,6 +43,8 @@ struct LaunchCfg {
     int  tile;             // segments per group per block in tile mode (0 = grid-stride)
     int  tile_pieces;      // v4: KiB of LDS image per stage (P)
     uint32_t stream_spw;   // kernel 6: segments per wave (one contiguous run each)
+    uint32_t run_bytes;    // kernel 6, varlen: runs of about this many bytes, sized on the device from
+                           // sampled lengths (stream_spw is then the shortest run the grid allows)
 };
 
 struct PktBatchArgs {
@@ -116,6 +120,12 @@ uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
+// Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128).
+hipError_t launch_varlen_runlen(const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
+                                uint32_t spw_min, uint32_t* out, hipStream_t s);
+void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
+uint32_t varlen_run_bytes();
+constexpr uint32_t kVarlenSpwMin = 3u;
 void set_hdr_burst(int v);     // NETCSUM_TUNE_HDR_BURST: header stream results written per run (1) or per piece (0)
 bool hdr_burst();
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain

@@ -988,6 +988,13 @@ static void note_launch(const LaunchCfg& c, const SegBatchArgs& a) {
         return;
     }
     if (kid == 6) {
+        if (a.seg_off && c.run_bytes) {
+            snprintf(g_last_launch, sizeof(g_last_launch),
+                     "seg_stream_varlen_kernel<D=%d%s%s> block=256 segs_per_wave=adaptive(>=%u, ~%u B)",
+                     c.chunks_per_pass, (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "",
+                     c.stream_spw, c.run_bytes);
+            return;
+        }
         snprintf(g_last_launch, sizeof(g_last_launch), "%s<D=%d%s%s> block=256 segs_per_wave=%u",
                  a.seg_off ? "seg_stream_varlen_kernel" : "seg_stream_kernel", c.chunks_per_pass,
                  (a.pseudo && a.pseudo_len) ? ",pseudo" : "", c.nt ? ",nt" : "", c.stream_spw);

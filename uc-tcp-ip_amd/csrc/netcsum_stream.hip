@@ -330,7 +330,17 @@ template <int D, int PH, bool NT>
 __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    // Adaptive runs: the grid was sized for runs of `spw`; a longer device-chosen run leaves the
+    // blocks past the ones it needs idle, and the XCD order is taken over the blocks in use.
+    uint32_t nwg = gridDim.x;
+    if (A.run_dev != nullptr) {
+        spw = max(spw, min((uint32_t)__builtin_amdgcn_readfirstlane((int)*A.run_dev), kMaxRun));
+        nwg = (uint32_t)((((uint64_t)A.n_seg + spw - 1u) / spw + 3u) / 4u);
+        if (blockIdx.x >= nwg) {
+            return;
+        }
+    }
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg) : blockIdx.x;
     const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
@@ -478,15 +488,67 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
 template <int D, int PH, bool NT>
 hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
-    // defaults from r2ct (C4, 1 M packed 40-9000 B): runs of 8, touch, 5 waves per SIMD: 0.680 ms
-    // against 0.696 ms for runs of 16 at full residency without the touch
+    // r2ct (C4, 1 M packed 40-9000 B): runs of 8, touch, 5 waves per SIMD: 0.680 ms against 0.696 ms
+    // for runs of 16 at full residency without the touch. r2zm: the best run is a byte budget, not a
+    // count (C4: 3 segments = 13.6 KB, 0.657 ms; 40-1500 B: 32 segments = 25 KB, 0.158 ms against
+    // 0.273 for runs of 8), so adaptive runs (run_dev) at full residency are the default.
     a.touch = stream_touch(true) ? 1u : 0u;
     a.xcd = stream_xcd(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
-    hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256), stream_lds_bytes(5), s, a, spw);
+    hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256),
+                       stream_lds_bytes(a.run_dev != nullptr ? 0 : 5), s, a, spw);
     return hipGetLastError();
 }
+
+// One block: the mean of up to 4096 evenly spaced lengths -> run length for about run_bytes per run.
+__global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint16_t* lens, uint32_t n, uint32_t extra,
+                                                             uint32_t run_bytes, uint32_t spw_min, uint32_t* out) {
+    __shared__ uint32_t part[16];
+    const uint32_t m = min(n, 4096u);
+    uint32_t acc = 0u;
+    for (uint32_t j = threadIdx.x; j < m; j += 1024u) {
+        acc += lens[(uint32_t)(((uint64_t)j * n) / m)];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        acc += (uint32_t)__shfl_xor((int)acc, d, 64);
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        part[threadIdx.x >> 6] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        uint32_t tot = 0u;
+        for (int i = 0; i < 16; ++i) {
+            tot += part[i];
+        }
+        const uint32_t mean = (m ? tot / m : 0u) + extra;
+        const uint32_t spw = run_bytes / max(mean, 1u);
+        *out = min(max(spw, spw_min), kMaxRun);
+    }
+}
+
+}  // namespace
+
+namespace {
+std::atomic<int> g_varlen_run_bytes{-1};   // NETCSUM_TUNE_VARLEN_RUN_BYTES: -1 default, 0 fixed runs of 8
+constexpr uint32_t kVarlenRunBytes = 16384u;
+}  // namespace
+
+void set_varlen_run_bytes(int v) { g_varlen_run_bytes.store(v); }
+uint32_t varlen_run_bytes() {
+    const int v = g_varlen_run_bytes.load();
+    return v < 0 ? kVarlenRunBytes : (uint32_t)v;
+}
+
+hipError_t launch_varlen_runlen(const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
+                                uint32_t spw_min, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(varlen_runlen_kernel, dim3(1), dim3(1024), 0, s, lens, n, extra, run_bytes, spw_min, out);
+    return hipGetLastError();
+}
+
+namespace {
 
 template <int D, int PH, bool NT, bool ONE>
 hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {

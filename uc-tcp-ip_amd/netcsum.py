@@ -61,6 +61,7 @@ TUNE_CRC_NT = 16
 TUNE_CRC_LANES = 17
 TUNE_CRC_WIDE = 18
 TUNE_HDR_BURST = 19
+TUNE_VARLEN_RUN_BYTES = 20
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
