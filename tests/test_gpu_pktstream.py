@@ -318,3 +318,19 @@ def test_pkt_stream_v6_c2_shape_round_trip_1M():
     torch.cuda.synchronize()
     failed = torch.nonzero((f & op.L4_OK) == 0).flatten()
     assert torch.equal(failed, bad)
+
+
+@pytest.mark.parametrize("stride,pkt_len,run", [(1500, 1500, 8), (1000, 1000, 16), (577, 577, 32), (256, 200, 64),
+                                                (128, 128, 64), (9000, 9000, 8)])
+def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run):
+    """Default run: about 20 KB of datagrams per wave in multiples of 8, 8..64 (r2zq sweep); results equal the
+    lane-group kernel's."""
+    rng = random.Random(stride)
+    n = 300
+    buf = _batch(rng, n, stride, pkt_len, 2)
+    netcsum.tune(netcsum.TUNE_KERNEL, 2)
+    rx_ref, tx_ref, txf_ref, _, _ = _run(buf, n, stride, pkt_len, 2, True)
+    netcsum.tune(netcsum.TUNE_KERNEL, 0)
+    rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, 2, True)
+    assert f"pkts_per_wave={run}" in d_rx and f"pkts_per_wave={run}" in d_tx, (d_rx, d_tx)
+    assert np.array_equal(rx, rx_ref) and np.array_equal(tx, tx_ref) and np.array_equal(txf, txf_ref)

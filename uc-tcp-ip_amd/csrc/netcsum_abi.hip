@@ -756,9 +756,16 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // 8-B records + scatter pass: 0.288 ms against 0.296 for in-pass field writes). Mixed rings run
     // both parses in a wave whose lanes disagree on the version, and a run of 16 spreads that over
     // twice the bytes (profiles/r2zb_pkt_stream_mixed_v6_v4.jsonl, alternating ring: Rx 0.243 ->
-    // 0.2185 ms, Tx 0.302 -> 0.292); IPv4 and IPv6 alone stay at 8 (16: +0.9 % / +0.2 %).
+    // 0.2185 ms, Tx 0.302 -> 0.292); IPv4 and IPv6 alone stay at 8 (16: +0.9 % / +0.2 %). Shorter
+    // datagrams need longer runs (a run's cost is per datagram event AND per wave): about 20 KB per
+    // run in multiples of 8 datagrams, 8..64 (40 KB in multiples of 16 for mixed rings); r2zq sweep
+    // (tools/pkt_run_probe.py): Rx of 256-B datagrams 0.891 -> 0.567 ms, 576-B 0.424 -> 0.29,
+    // 1000-B 0.259 -> 0.222; 1500-B keeps 8.
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
-        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : (ip_ver == 0 ? 16u : 8u);
+        const uint64_t per = std::max<uint64_t>(a.stride, 1u);
+        const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
+                                         : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
+        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : run;
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
         const bool two = tx && g_tune_tx_passes.load() != 1;
