@@ -152,13 +152,12 @@ def tx_finalize(pkt: bytes, udp_tx_csum: bool = True):
 #              other types: rejected before the checksum (no verdict) :2945-2948
 #           Tx DataCalc(NET_BUF{ICMP_V6}, pseudo, 40) for every type   net_icmpv6.c:1439 (the error
 #              messages' ~HdrCalc(pseudo) field trick, :949-965, is tested equal in tests/)
-# Extension headers (net_ipv6.c:8290-8360): Hop-by-Hop (0, first only), Routing (43), Destination
-# Options (60), length (HdrExtLen + 1) * 8 (net_ipv6.c:8601), are skipped -- up to 4, and only while
-# the chain and the transport fields (transport offset + 24) lie within the first `window` bytes of
-# the packet's frame (the batch kernel's first-pass chunks; window(G, lead) = 16 G - lead) -- and the
-# upper-layer length becomes payload - extension bytes (net_ipv6.c:5682). Fragment (44) -> FRAGMENT;
-# an extension header past the payload -> MALFORMED; any other extension header, a Hop-by-Hop
-# header after the first, or a chain beyond the window -> EXT_HDR. No transport verdict for those.
+# Extension headers (net_ipv6.c:8290-8360, 8396-8510): Hop-by-Hop (0, first only), Routing (43),
+# Destination Options (60), length (HdrExtLen + 1) * 8 (net_ipv6.c:8601), are skipped -- a chain of
+# any length, as NetIPv6_RxPktProcessExtHdr walks it -- and the upper-layer length becomes payload -
+# extension bytes (net_ipv6.c:5682). Fragment (44) -> FRAGMENT; an extension header running past the
+# payload -> MALFORMED; any other extension header or a Hop-by-Hop header after the first -> EXT_HDR.
+# No transport verdict for those.
 # ---------------------------------------------------------------------------------------------
 EXT_HDR = 128
 IPV6_EXT = {0, 43, 44, 50, 51, 59, 60, 135, 139, 140, 253, 254}
@@ -166,7 +165,7 @@ ICMPV6_PSEUDO_TYPES = {128, 129, 130, 131, 134, 135, 136, 137}
 ICMPV6_NOPSEUDO_TYPES = {1, 3, 4}
 
 
-def _parse6(pkt: bytes, window: int = 1 << 30):
+def _parse6(pkt: bytes):
     """-> None (malformed) or (flags_so_far, transport offset, upper-layer length, next header, addrs)."""
     if len(pkt) < 40 or pkt[0] >> 4 != 6:
         return None
@@ -175,17 +174,17 @@ def _parse6(pkt: bytes, window: int = 1 << 30):
     if tot > len(pkt):
         return None
     nh, off = pkt[6], 40
-    for _ in range(4):
-        if nh not in (0, 43, 60):
-            break
-        if (nh == 0 and off != 40) or off + 8 > window:
+    while nh in (0, 43, 60):                   # net_ipv6.c:8411-8418: until a non-extension header
+        if nh == 0 and off != 40:              # Hop-by-Hop only first (net_ipv6.c:8307-8309)
             return EXT_HDR, off, 0, nh, pkt[8:40]
+        if off + 8 > tot:                      # the header itself would run past the payload
+            return None
         nh, off = pkt[off], off + (pkt[off + 1] + 1) * 8
         if off > tot:
             return None
     if nh == 44:
         return FRAGMENT, off, 0, nh, pkt[8:40]
-    if nh in IPV6_EXT or (off != 40 and off + 24 > window):
+    if nh in IPV6_EXT:
         return EXT_HDR, off, 0, nh, pkt[8:40]
     return 0, off, tot - off, nh, pkt[8:40]
 
@@ -202,9 +201,9 @@ def _l4_chain6(pkt: bytes, proto_type: int, l4len: int, icmp=False, ix=40):
                            "data_len": l4len}])
 
 
-def rx_validate_v6(pkt: bytes, window: int = 1 << 30) -> int:
+def rx_validate_v6(pkt: bytes) -> int:
     pkt = bytes(pkt)
-    p = _parse6(pkt, window)
+    p = _parse6(pkt)
     if p is None:
         return MALFORMED
     fx, off, plen, nh, addrs = p
@@ -248,10 +247,10 @@ def rx_validate_v6(pkt: bytes, window: int = 1 << 30) -> int:
     return f
 
 
-def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
+def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True):
     """-> (finalized packet bytes, flags)."""
     pkt = bytes(pkt)
-    p = _parse6(pkt, window)
+    p = _parse6(pkt)
     if p is None:
         return pkt, MALFORMED
     fx, off, plen, nh, addrs = p
@@ -291,12 +290,12 @@ def tx_finalize_v6(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
     return bytes(pkt), f
 
 
-def rx_validate_ip(pkt: bytes, window: int = 1 << 30) -> int:
+def rx_validate_ip(pkt: bytes) -> int:
     """Mixed batches: version nibble 6 -> IPv6, anything else -> IPv4 (include/netcsum_mi355x.h)."""
-    return rx_validate_v6(pkt, window) if len(pkt) and pkt[0] >> 4 == 6 else rx_validate(pkt)
+    return rx_validate_v6(pkt) if len(pkt) and pkt[0] >> 4 == 6 else rx_validate(pkt)
 
 
-def tx_finalize_ip(pkt: bytes, udp_tx_csum: bool = True, window: int = 1 << 30):
+def tx_finalize_ip(pkt: bytes, udp_tx_csum: bool = True):
     if len(pkt) and pkt[0] >> 4 == 6:
-        return tx_finalize_v6(pkt, udp_tx_csum, window)
+        return tx_finalize_v6(pkt, udp_tx_csum)
     return tx_finalize(pkt, udp_tx_csum)

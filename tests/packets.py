@@ -139,7 +139,7 @@ def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) ->
             nh, ext = _ext_chain(rng, chain, inner_nh)
         elif kind == "ext_frag":
             nh, ext = _ext_chain(rng, [(60, 1)] * rng.randint(0, 1) + [(44, 1)], inner_nh)
-        elif kind == "ext_long":                               # 1032+ B: beyond every window
+        elif kind == "ext_long":                               # 1032+ B: beyond every batch kernel's window (walk pass)
             nh, ext = _ext_chain(rng, [(60, rng.randint(129, 200))], inner_nh)
         elif kind == "ext_hbh_late":
             nh, ext = _ext_chain(rng, [(60, 1), (0, 1)], inner_nh)
@@ -165,9 +165,3 @@ def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) ->
         k = rng.randint(8, len(b) - 1)                            # addresses are covered too
         b[k] ^= 1 << rng.randint(0, 7)
     return bytes(b)
-
-
-def v6_window(group: int, addr: int) -> int:
-    """Bytes of a packet at device address `addr` that the IPv6 batch kernel's first-pass chunks hold
-    (extension-header chains are walked only inside them): 16 * G - (addr % 16)."""
-    return 16 * group - (addr & 15)

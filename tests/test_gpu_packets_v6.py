@@ -10,7 +10,7 @@ import pytest
 
 import netcsum
 import oracle_packets as op
-from packets import KINDS6, make_packet_v6, packed_batch, v6_window
+from packets import KINDS6, make_packet_v6, packed_batch
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -62,7 +62,7 @@ def test_rx_validate_v6_mixed_varlen(group, grid, tile):
     netcsum.tune(netcsum.TUNE_TILE, tile)
     got = _rx_gpu(buf, offs, lens)
     g = group or _auto_group(True)
-    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]), v6_window(g, o))
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]))
                      for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(pkts[i][:48].hex(), int(got[i]), int(want[i])) for i in bad[:5]]
@@ -111,12 +111,12 @@ def test_tx_finalize_v6_varlen_then_rx_accepts(udp_tx_csum, group):
     g = group or _auto_group(True)
     for i, (off, n) in enumerate(zip(offs.tolist(), lens.tolist())):
         pkt = bytes(buf[off:off + n])
-        want_pkt, want_f = op.tx_finalize_v6(pkt, udp_tx_csum, v6_window(g, off))
+        want_pkt, want_f = op.tx_finalize_v6(pkt, udp_tx_csum)
         assert bytes(out[off:off + n]) == want_pkt, (i, pkt[:48].hex())
         assert flags[i] == want_f, (i, int(flags[i]), want_f)
     assert np.array_equal(out[:offs[0]], buf[:offs[0]])
     got = _rx_gpu(out, offs, lens)
-    want = np.array([op.rx_validate_v6(bytes(out[o:o + n]), v6_window(g, o))
+    want = np.array([op.rx_validate_v6(bytes(out[o:o + n]))
                      for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     assert np.array_equal(got, want)
     tcp_udp = np.array([len(p) >= 48 and p[0] >> 4 == 6 and p[6] in (6, 17) for p in pkts])
@@ -150,8 +150,7 @@ def test_tx_finalize_v6_strided_vs_oracle(stride, pkt_len, group):
     want = buf.copy()
     want_f = np.zeros(n, np.uint8)
     for i in range(n):
-        pk, want_f[i] = op.tx_finalize_v6(bytes(buf[i * stride:i * stride + pkt_len]), True,
-                                          v6_window(g, i * stride))
+        pk, want_f[i] = op.tx_finalize_v6(bytes(buf[i * stride:i * stride + pkt_len]), True)
         want[i * stride:i * stride + pkt_len] = np.frombuffer(pk, np.uint8)
     bad = np.nonzero(out != want)[0]
     assert bad.size == 0, [(int(j), int(j) // stride, int(j) % stride, int(out[j]), int(want[j])) for j in bad[:8]]
@@ -164,29 +163,58 @@ def test_v6_empty_batch_and_null_flags():
     assert netcsum.rx_validate_ipv6(b, 1, None, stride=64, pkt_len=64, check=False) != netcsum.NET_UTIL_ERR_NONE
 
 
-@pytest.mark.parametrize("group", [8, 16, 64])
-def test_rx_v6_extension_chains_at_the_window_edge(group):
-    """Extension-header chains of every length around the group's window (16 G bytes of the frame
-    minus the packet's lead): walked when the transport fields fit, EXT_HDR when they do not, at
-    every lead 0-15."""
-    rng = random.Random(700 + group)
+def _long_chain_pkts(rng, max_units, n_hdrs=(1,), reps=3):
+    """Valid datagrams whose transport follows Routing / Destination Options chains of n headers of
+    1..max_units 8-B units each (the walk pass finishes whatever the batch kernel's window holds not)."""
     pkts = []
-    for units in range(1, 2 * group + 5):
-        for _ in range(3):
-            inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 200))
-            nh_in = inner[6]
-            ext = struct.pack("!BB", nh_in, units - 1) + rng.randbytes(units * 8 - 2)
-            body = ext + inner[40:]
-            hdr = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40]
-            pkts.append(op.tx_finalize_v6(hdr + body)[0])
+    for units in range(1, max_units + 1):
+        for h in n_hdrs:
+            for _ in range(reps):
+                inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo", "icmp_err"]), payload=rng.randint(24, 200))
+                nh, ext = inner[6], b""
+                for _k in range(h):
+                    u = rng.randint(1, units)
+                    ext = struct.pack("!BB", nh, u - 1) + rng.randbytes(u * 8 - 2) + ext
+                    nh = rng.choice([43, 60])
+                body = ext + inner[40:]
+                hdr = inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40]
+                pkts.append(op.tx_finalize_v6(hdr + body)[0])
+    return pkts
+
+
+@pytest.mark.parametrize("group", [8, 16, 64])
+def test_rx_tx_v6_extension_chains_of_any_length(group):
+    """Extension-header chains of every length around and far past the group's window (16 G bytes of
+    the frame minus the packet's lead) and of 1..12 headers, at every lead 0-15: every one walked to
+    its transport header like the reference (net_ipv6.c:8396-8510), Rx verdicts and Tx bytes equal
+    the oracle's, no EXT_HDR left."""
+    rng = random.Random(700 + group)
+    pkts = _long_chain_pkts(rng, 2 * group + 5) + _long_chain_pkts(rng, 3, n_hdrs=(4, 5, 8, 12), reps=4)
     rng.shuffle(pkts)
     buf, offs, lens = packed_batch(pkts, rng)
     netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     got = _rx_gpu(buf, offs, lens)
-    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]), v6_window(group, o))
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]))
                      for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
-    assert np.array_equal(got, want)
-    assert (want & op.EXT_HDR).any() and ((want & op.L4_OK) != 0).any()
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+    assert not (want & op.EXT_HDR).any() and (want & op.L4_CHECKED).all() and ((want & op.L4_OK) != 0).any()
+    # Tx of the same datagrams with stale transport fields: the oracle's bytes and flags
+    stale = buf.copy()
+    for o, n in zip(offs.tolist(), lens.tolist()):
+        fx, off, _ul, nh, _ = op._parse6(bytes(buf[o:o + n]))
+        fld = o + off + {6: 16, 17: 6, 58: 2}[nh]
+        stale[fld:fld + 2] = np.frombuffer(rng.randbytes(2), np.uint8)
+    b, o, ln = _dev(stale, offs, lens)
+    fl = torch.zeros(len(lens), dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv6(b, len(lens), fl, off=o, lens=ln)
+    torch.cuda.synchronize()
+    assert np.array_equal(b.cpu().numpy(), buf)
+    assert (fl.cpu().numpy() == (op.IP_OK | op.L4_CHECKED | op.L4_OK)).all()
+    # Tx without flags: the walk pass keeps its flags in scratch, the bytes are the same
+    b, o, ln = _dev(stale, offs, lens)
+    netcsum.tx_finalize_ipv6(b, len(lens), None, off=o, lens=ln)
+    torch.cuda.synchronize()
+    assert np.array_equal(b.cpu().numpy(), buf)
 
 
 @pytest.mark.parametrize("group", [0, 16, 64])
@@ -206,7 +234,7 @@ def test_mixed_ip_batch_rx_and_tx(group, udp_tx_csum):
     f = torch.zeros(len(pkts), dtype=torch.uint8, device=DEV)
     netcsum.rx_validate_ip(b, len(pkts), f, off=o, lens=ln)
     torch.cuda.synchronize()
-    want = np.array([op.rx_validate_ip(bytes(buf[p:p + n]), v6_window(g, p))
+    want = np.array([op.rx_validate_ip(bytes(buf[p:p + n]))
                      for p, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     got = f.cpu().numpy()
     bad = np.nonzero(got != want)[0]
@@ -215,7 +243,7 @@ def test_mixed_ip_batch_rx_and_tx(group, udp_tx_csum):
     torch.cuda.synchronize()
     out, flags = b.cpu().numpy(), f.cpu().numpy()
     for i, (p, n) in enumerate(zip(offs.tolist(), lens.tolist())):
-        want_pkt, want_f = op.tx_finalize_ip(bytes(buf[p:p + n]), udp_tx_csum, v6_window(g, p))
+        want_pkt, want_f = op.tx_finalize_ip(bytes(buf[p:p + n]), udp_tx_csum)
         assert bytes(out[p:p + n]) == want_pkt, (i, pkts[i][:24].hex())
         assert flags[i] == want_f, (i, int(flags[i]), want_f)
 
@@ -259,7 +287,7 @@ def test_v6_extreme_sizes(group):
     netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     g = group or _auto_group(True)
     got = _rx_gpu(buf, offs, lens)
-    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]), v6_window(g, o))
+    want = np.array([op.rx_validate_v6(bytes(buf[o:o + n]))
                      for o, n in zip(offs.tolist(), lens.tolist())], np.uint8)
     assert np.array_equal(got, want), (got, want)
     assert ((want[1:] & op.L4_OK) != 0).all()
@@ -272,6 +300,6 @@ def test_v6_extreme_sizes(group):
     torch.cuda.synchronize()
     out = b.cpu().numpy()
     for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
-        want_pkt, want_f = op.tx_finalize_v6(bytes(stale[o:o + n]), True, v6_window(g, o))
+        want_pkt, want_f = op.tx_finalize_v6(bytes(stale[o:o + n]), True)
         assert bytes(out[o:o + n]) == want_pkt, i
         assert f.cpu().numpy()[i] == want_f, i

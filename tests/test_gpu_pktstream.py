@@ -176,12 +176,6 @@ def test_pkt_stream_c2_shape_round_trip_1M():
 
 # ---- IPv6 and mixed IPv4 / IPv6 batches in the run-stream form (VER 6 / VER 0) -----------------
 
-def _stream_window(lead, i, stride):
-    """Bytes of datagram i the lane's 96-B window holds: 96 - (its address mod 16); the batch buffer
-    is 256-B aligned (torch), the datagrams start at lead + i * stride."""
-    return 96 - ((lead + i * stride) & 15)
-
-
 def _batch_ip(rng, n, stride, pkt_len, lead, v6_share):
     from packets import KINDS6, make_packet_v6
     buf = np.frombuffer(rng.randbytes(lead + n * stride + 96), np.uint8).copy()
@@ -205,13 +199,12 @@ def _want_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver):
     for i in range(n):
         o = lead + i * stride
         pkt = bytes(buf[o:o + pkt_len])
-        w = _stream_window(lead, i, stride)
         if ver == 6:
-            rx[i] = op.rx_validate_v6(pkt, w)
-            q, tx_f[i] = op.tx_finalize_v6(pkt, udp_tx_csum, w)
+            rx[i] = op.rx_validate_v6(pkt)
+            q, tx_f[i] = op.tx_finalize_v6(pkt, udp_tx_csum)
         else:
-            rx[i] = op.rx_validate_ip(pkt, w)
-            q, tx_f[i] = op.tx_finalize_ip(pkt, udp_tx_csum, w)
+            rx[i] = op.rx_validate_ip(pkt)
+            q, tx_f[i] = op.tx_finalize_ip(pkt, udp_tx_csum)
         tx_buf[o:o + pkt_len] = np.frombuffer(q, np.uint8)
     return rx, tx_buf, tx_f
 
@@ -240,8 +233,8 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     """Every IPv6 kind (TCP / UDP / UDP without checksum, ICMPv6 echo / error / NDP / other types,
     extension-header chains inside and beyond the lane's window, Hop-by-Hop after the first, Fragment,
     opaque extension headers, malformed versions / lengths, corrupted bytes), alone (VER 6) or mixed
-    with every IPv4 kind (VER 0), Rx verdicts and Tx bytes + verdicts against the oracle with the
-    window of the lane's 96-B prologue (96 - address mod 16)."""
+    with every IPv4 kind (VER 0), Rx verdicts and Tx bytes + verdicts against the oracle (chains past
+    the lane's 96-B prologue finished by the walk pass)."""
     netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
     rng = random.Random(ver * 1000 + stride * 7 + pkt_len + lead * 131 + passes)
     n = 600 if stride < 5000 else 150
@@ -262,20 +255,25 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
 
 
 @pytest.mark.parametrize("lead", list(range(16)))
-def test_pkt_stream_v6_extension_chains_at_the_window_edge(lead):
-    """Destination Options headers of 1..10 units (8..80 B) before TCP / UDP / ICMPv6 at every lead:
-    walked while the chain and the transport fields fit the lane's 96 - lead bytes, EXT_HDR beyond —
-    the oracle's window rule — and Tx finalizes exactly the walked ones."""
+def test_pkt_stream_v6_extension_chains_of_any_length(lead):
+    """Destination Options / Routing chains before TCP / UDP / ICMPv6 at every lead: one header of
+    1..40 units (8..320 B, inside and past the lane's 96 - lead bytes) or 4..9 headers — every chain
+    walked to its transport header (the batch kernel's window, then the walk pass), Rx verdicts and
+    Tx bytes + flags equal the oracle's, no EXT_HDR left."""
     from packets import make_packet_v6
     rng = random.Random(900 + lead)
-    stride = pkt_len = 512
+    stride = pkt_len = 1024
     pkts = []
-    for units in range(1, 11):
-        for _ in range(6):
+    for units in list(range(1, 13)) + [20, 40]:
+        for n_hdr in (1, 4, 9):
             inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 300))
-            ext = struct.pack("!BB", inner[6], units - 1) + rng.randbytes(units * 8 - 2)
+            nh, ext = inner[6], b""
+            for _k in range(n_hdr):
+                u = units if n_hdr == 1 else rng.randint(1, 3)
+                ext = struct.pack("!BB", nh, u - 1) + rng.randbytes(u * 8 - 2) + ext
+                nh = rng.choice([43, 60])
             body = ext + inner[40:]
-            hdr = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40]
+            hdr = inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40]
             pkts.append(op.tx_finalize_v6(hdr + body)[0][:pkt_len])
     rng.shuffle(pkts)
     n = len(pkts)
@@ -286,7 +284,7 @@ def test_pkt_stream_v6_extension_chains_at_the_window_edge(lead):
     rx, tx, txf, d_rx, _ = _run_ip(buf, n, stride, pkt_len, lead, True, 6)
     assert d_rx.startswith("pkt_stream_kernel"), d_rx
     assert np.array_equal(rx, rx_w) and np.array_equal(tx, tx_w) and np.array_equal(txf, txf_w)
-    assert (rx_w & op.EXT_HDR).any() and ((rx_w & op.L4_OK) != 0).any()
+    assert not (rx_w & op.EXT_HDR).any() and ((rx_w & op.L4_OK) != 0).all()
 
 
 def test_pkt_stream_v6_c2_shape_round_trip_1M():

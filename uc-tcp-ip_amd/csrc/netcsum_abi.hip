@@ -761,6 +761,12 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // run in multiples of 8 datagrams, 8..64 (40 KB in multiples of 16 for mixed rings); r2zq sweep
     // (tools/pkt_run_probe.py): Rx of 256-B datagrams 0.891 -> 0.567 ms, 576-B 0.424 -> 0.29,
     // 1000-B 0.259 -> 0.222; 1500-B keeps 8.
+    // IPv6 / mixed batches: a second pass walks the extension-header chains the batch kernel left as
+    // EXT_HDR (netcsum_v6walk.hip). It reads the flags, so a Tx batch without d_flags gets them in the
+    // stream's scratch buffer (after the two-pass records when there are records).
+    const bool walk = ip_ver != 4;
+    const bool own_flags = walk && d_flags == nullptr;
+    hipStream_t hs = static_cast<hipStream_t>(hip_stream);
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
         const uint64_t per = std::max<uint64_t>(a.stride, 1u);
         const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
@@ -773,15 +779,22 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
                  tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "");
         netcsum::set_last_launch(desc);
-        hipStream_t hs = static_cast<hipStream_t>(hip_stream);
         if (two) {
             // the records live in this stream's scratch buffer (stream_scratch)
+            const size_t rec_bytes = (size_t)n_pkt * sizeof(netcsum::PktTxRecord);
             void* rec = nullptr;
-            NC_HIP(stream_scratch(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord), &rec));
+            NC_HIP(stream_scratch(dev, hs, rec_bytes + (own_flags ? n_pkt : 0u), &rec));
+            if (own_flags) a.flags_out = static_cast<uint8_t*>(rec) + rec_bytes;
             NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs, static_cast<netcsum::PktTxRecord*>(rec)));
-            return NET_UTIL_ERR_NONE;
+        } else {
+            if (own_flags) {
+                void* fl = nullptr;
+                NC_HIP(stream_scratch(dev, hs, n_pkt, &fl));
+                a.flags_out = static_cast<uint8_t*>(fl);
+            }
+            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs));
         }
-        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs));
+        if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
         return NET_UTIL_ERR_NONE;
     }
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
@@ -789,7 +802,13 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u", c.group_lanes,
              c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile);
     netcsum::set_last_launch(desc);
-    NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, static_cast<hipStream_t>(hip_stream)));
+    if (own_flags) {
+        void* fl = nullptr;
+        NC_HIP(stream_scratch(dev, hs, n_pkt, &fl));
+        a.flags_out = static_cast<uint8_t*>(fl);
+    }
+    NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, hs));
+    if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
     return NET_UTIL_ERR_NONE;
 }
 

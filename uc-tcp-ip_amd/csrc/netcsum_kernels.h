@@ -135,6 +135,9 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream p
 void set_tx_flush(int mode);
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx,
                              hipStream_t s, PktTxRecord* rec = nullptr);   // rec: two-pass Tx (records + scatter)
+// IPv6 extension-header chains past the batch kernels' window (flags EXT_HDR): walked to the end and
+// finished in place (netcsum_v6walk.hip); a.flags_out holds the batch kernel's flags.
+hipError_t launch_pkt_v6_walk(const PktBatchArgs& a, bool tx, int cus, hipStream_t s);
 void set_last_launch(const char* desc);
 hipError_t launch_hdr_batch(const SegBatchArgs& a, int stages, int h, int grid, hipStream_t s);
 bool stream_supported(const SegBatchArgs& a);  // strided, stride in [len, len+64], len >= 256

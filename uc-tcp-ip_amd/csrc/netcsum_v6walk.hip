@@ -1,0 +1,230 @@
+// netcsum_v6walk.hip — IPv6 extension-header chains of any length in the packet batches.
+//
+// The batch kernels (netcsum_packets.hip, netcsum_pktstream.hip) parse each datagram from the bytes
+// their first loads hold (a 96 - lead / 16 G - lead byte window) and walk at most 4 extension
+// headers; a chain past that comes back as NETCSUM_PKT_EXT_HDR. The reference walks any chain
+// (NetIPv6_RxPktProcessExtHdr, net_ipv6.c:8396-8510: Hop-by-Hop / Destination Options via
+// NetIPv6_RxOptHdr, Routing via NetIPv6_RxRoutingHdr, length (HdrExtLen + 1) * 8, net_ipv6.c:8601,
+// until the next header is not an extension header), so this pass finishes exactly those datagrams:
+//
+//   one wave per 1024 flags; the datagrams whose flag has EXT_HDR are found by a ballot, and the whole wave
+//   takes each of them in turn: the chain is walked with wave-uniform loads (no window, no header
+//   count), then the transport part [off, tot) and the addresses [8, 40) are summed with the wave's
+//   64 lanes reading half-words in parallel, and the verdict (Rx) or the checksum field (Tx) and the
+//   flag are written by lane 0 (vector stores).
+//
+// Datagrams are rare on this path (chains of more than 4 headers or longer than ~50 bytes), so the
+// pass costs one launch that reads the n flag bytes (1 MB for 1 M datagrams) when no datagram needs
+// it. The verdict rules are pkt_parse_v6's (netcsum_packets.hip; the same reference lines):
+//   TCP (6)     DataVerify / DataCalc + pseudo {src, dst, ulen, 0, 6}        net_tcp.c:7871-7879, 29839-29862
+//   UDP (17)    length check, field 0 = no checksum (Rx), 0 -> 0xFFFF (Tx)   net_udp.c:1903-1957, 2909-2937
+//   ICMPv6 (58) Rx types 1, 3, 4 without the pseudo-header, 128-131 / 134-137 with it, others no verdict;
+//               Tx every type with it                                         net_icmpv6.c:2910-2948, 1439
+// with ulen = payload length - extension-header bytes (net_ipv6.c:5682); Fragment (44) -> FRAGMENT,
+// another extension header or a late Hop-by-Hop -> EXT_HDR (no transport verdict, the reference
+// rejects those, net_ipv6.c:8307-8309, 8465-8476), a header running past the payload -> MALFORMED.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "netcsum_kernels.h"
+
+namespace netcsum {
+
+namespace {
+
+constexpr uint32_t W_IP_OK = 0x01u, W_L4_OK = 0x02u, W_L4_CHECKED = 0x04u, W_UDP_NO_CSUM = 0x08u,
+                   W_MALFORMED = 0x10u, W_FRAGMENT = 0x20u, W_L4_MALFORMED = 0x40u, W_EXT_HDR = 0x80u;
+
+__device__ __forceinline__ bool ext_hdr_value(uint32_t nh) {   // net_ipv6.h NET_IP_HDR_PROTOCOL_EXT_*
+    return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 59u || nh == 60u ||
+           nh == 135u || nh == 139u || nh == 140u || nh == 253u || nh == 254u;
+}
+
+__device__ __forceinline__ uint32_t be16(const uint8_t* p, uint32_t k) {
+    return ((uint32_t)p[k] << 8) | (uint32_t)p[k + 1u];
+}
+
+// Big-endian half-word sum of packet bytes [lo, hi) (lo even; an odd last octet padded with zero),
+// the half-word at `skip` (even, or ~0u) counted as zero; the wave's lanes take every 64th half-word.
+__device__ __forceinline__ uint32_t wave_sum(const uint8_t* p, uint32_t lo, uint32_t hi, uint32_t skip, uint32_t lane) {
+    uint32_t s = 0u;
+    for (uint32_t k = lo + 2u * lane; k < hi; k += 128u) {
+        const uint32_t w = ((uint32_t)p[k] << 8) | ((k + 1u < hi) ? (uint32_t)p[k + 1u] : 0u);
+        s += (k == skip) ? 0u : w;                  // <= 512 half-words per lane: no overflow
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += (uint32_t)__shfl_xor((int)s, o, 64);
+    }
+    return s;                                       // < 2^31 for a 65 575-byte datagram
+}
+
+__device__ __forceinline__ uint32_t fold(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    return s;                                       // 0 iff every summed half-word was 0
+}
+
+// The whole wave finishes datagram i (all values below are wave-uniform).
+template <bool TX>
+__device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
+    uint64_t off64;
+    uint32_t avail;
+    if (A.off) {
+        off64 = A.off[i];
+        avail = A.len[i];
+    } else {
+        off64 = (uint64_t)i * A.stride;
+        avail = A.len_u;
+    }
+    uint8_t* p = const_cast<uint8_t*>(A.base) + off64;
+    if (avail < 40u || (p[0] >> 4) != 6u) {
+        return;                                     // not IPv6: the batch kernel's flag stands
+    }
+    const uint32_t tot = 40u + be16(p, 4u);
+    if (tot > avail) {
+        return;                                     // MALFORMED already (never EXT_HDR)
+    }
+    uint32_t nh = p[6], off = 40u, f = 0u;
+    while (nh == 0u || nh == 43u || nh == 60u) {   // off grows by >= 8 per header: ends by tot
+        if (nh == 0u && off != 40u) {
+            f = W_IP_OK | W_EXT_HDR;                // Hop-by-Hop only first (net_ipv6.c:8307)
+            break;
+        }
+        if (off + 8u > tot) {
+            f = W_MALFORMED;                        // the header would run past the payload
+            break;
+        }
+        const uint32_t nx = p[off];
+        off += ((uint32_t)p[off + 1u] + 1u) * 8u;
+        nh = nx;
+        if (off > tot) {
+            f = W_MALFORMED;                        // NET_IPv6_ERR_INVALID_EH_LEN
+            break;
+        }
+    }
+    uint32_t csum_off = ~0u;
+    bool pseudo = false, check = false;
+    if (f == 0u) {
+        f = W_IP_OK;
+        const uint32_t ulen = tot - off;
+        if (nh == 44u) {
+            f |= W_FRAGMENT;
+        } else if (ext_hdr_value(nh)) {
+            f |= W_EXT_HDR;
+        } else if (nh == 6u) {
+            if (ulen < 20u) {
+                f |= W_L4_MALFORMED;
+            } else {
+                csum_off = off + 16u;
+                pseudo = check = true;
+            }
+        } else if (nh == 17u) {
+            if (ulen < 8u || be16(p, off + 4u) != ulen) {
+                f |= W_L4_MALFORMED;
+            } else {
+                csum_off = off + 6u;
+                if (!TX && be16(p, off + 6u) == 0u) {
+                    f |= W_UDP_NO_CSUM | W_L4_OK;
+                } else if (TX && !A.udp_tx_csum) {
+                    f |= W_UDP_NO_CSUM;
+                    if (lane == 0u) {
+                        p[csum_off] = 0u;           // NET_UDP_HDR_CHK_SUM_NONE (net_udp.c:2935)
+                        p[csum_off + 1u] = 0u;
+                    }
+                } else {
+                    pseudo = check = true;
+                }
+            }
+        } else if (nh == 58u) {
+            if (ulen < 4u) {
+                f |= W_L4_MALFORMED;
+            } else {
+                csum_off = off + 2u;
+                const uint32_t type = p[off];
+                if (TX || (type >= 128u && type <= 131u) || (type >= 134u && type <= 137u)) {
+                    pseudo = check = true;
+                } else if (type == 1u || type == 3u || type == 4u) {
+                    check = true;                   // HdrVerify over the message alone
+                }
+            }
+        }
+    }
+    if (check) {
+        uint32_t s = wave_sum(p, off, tot, TX ? csum_off : ~0u, lane);
+        if (pseudo) {
+            s += wave_sum(p, 8u, 40u, ~0u, lane) + (tot - off) + nh;   // addresses, length, next header
+        }
+        const uint32_t r = fold(s);
+        if constexpr (TX) {
+            uint32_t c = (~r) & 0xFFFFu;
+            if (nh == 17u && c == 0u) {
+                c = 0xFFFFu;                        // RFC 768 (net_udp.c:2929-2931)
+            }
+            if (lane == 0u) {
+                p[csum_off] = (uint8_t)(c >> 8);
+                p[csum_off + 1u] = (uint8_t)c;
+            }
+            f |= W_L4_CHECKED | W_L4_OK;
+        } else {
+            f |= W_L4_CHECKED | (r == 0xFFFFu ? W_L4_OK : 0u);
+        }
+    }
+    if (lane == 0u) {
+        A.flags_out[i] = (uint8_t)f;
+    }
+}
+
+// Each lane scans 16 flags (one 16-B load when the flags are 16-B aligned): a wave covers 1024
+// datagrams, so 1 M datagrams take 256 workgroups.
+template <bool TX>
+__global__ void __launch_bounds__(256) pkt_v6_walk_kernel(PktBatchArgs A) {
+    constexpr uint64_t kPerWave = 64u * 16u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool vec = (((uintptr_t)A.flags_out) & 15u) == 0u;
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * kPerWave; w0 < A.n;
+         w0 += (uint64_t)gridDim.x * 4u * kPerWave) {
+        const uint64_t b0 = w0 + 16u * lane;
+        uint32_t hit = 0u;                          // bit k: datagram b0 + k has EXT_HDR
+        if (vec && b0 + 16u <= A.n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(A.flags_out + b0);
+            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                hit |= ((d[k >> 2] >> (8 * (k & 3) + 7)) & 1u) << k;
+            }
+        } else {
+            for (uint32_t k = 0; k < 16u && b0 + k < A.n; ++k) {
+                hit |= ((A.flags_out[b0 + k] & W_EXT_HDR) ? 1u : 0u) << k;
+            }
+        }
+        uint64_t m = __ballot(hit != 0u);           // wave-uniform
+        while (m != 0u) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1u;
+            uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)j);
+            while (h != 0u) {
+                const uint32_t k = (uint32_t)__builtin_ctz(h);
+                h &= h - 1u;
+                walk_one<TX>(A, (uint32_t)(w0 + 16u * j + k), lane);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_pkt_v6_walk(const PktBatchArgs& a, bool tx, int cus, hipStream_t s) {
+    if (a.n == 0u) return hipSuccess;
+    if (a.flags_out == nullptr) return hipErrorInvalidValue;
+    const uint64_t blocks = ((uint64_t)a.n + 4095u) / 4096u;
+    const int grid = (int)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 8u);
+    if (tx) {
+        hipLaunchKernelGGL(pkt_v6_walk_kernel<true>, dim3(grid), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(pkt_v6_walk_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace netcsum
