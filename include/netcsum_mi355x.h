@@ -221,13 +221,13 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
  *               the message alone, as the reference does (net_icmpv6.c:2910-2920); other types get no
  *               verdict (the reference rejects them before any checksum, net_icmpv6.c:2945)
  *   Extension headers: Hop-by-Hop (0, first only), Routing (43) and Destination Options (60) are
- *               skipped (up to 4; upper-layer length = payload length - their bytes, net_ipv6.c:5682)
- *               while the chain and the transport fields lie in the first 16*G - (address % 16) bytes
- *               of the packet (G = the launch's lanes per packet: 32 for d_off batches, 8-64 by
- *               pkt_len for strided ones, or NETCSUM_TUNE_GROUP_LANES); a Fragment header (44) gives
- *               FRAGMENT; a header running past the payload gives MALFORMED
- *   EXT_HDR     any other extension header (50, 51, 59, 135, 139, 140, 253, 254), a late Hop-by-Hop
- *               header, or a chain past that window: no transport verdict in the batch. For 50 / 51 /
+ *               skipped, a chain of any length as NetIPv6_RxPktProcessExtHdr walks it
+ *               (net_ipv6.c:8396-8510; upper-layer length = payload length - their bytes,
+ *               net_ipv6.c:5682): the batch kernel walks what its first loads hold, a second pass
+ *               (netcsum_v6walk.hip) the longer chains; a Fragment header (44) gives FRAGMENT; a
+ *               header running past the payload gives MALFORMED
+ *   EXT_HDR     any other extension header (50, 51, 59, 135, 139, 140, 253, 254) or a late
+ *               Hop-by-Hop header: no transport verdict in the batch. For 50 / 51 /
  *               59 / 135 this is also the reference's outcome: it never reaches a transport checksum
  *               (ESP and Mobility: NET_IPv6_ERR_INVALID_EH, net_ipv6.c:8837-8846, :8956-8965; AH: the
  *               next header is read from the IPv6 header's first octet, 0x6X, and rejected as
