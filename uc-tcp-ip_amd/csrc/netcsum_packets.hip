@@ -147,9 +147,10 @@ __device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 
 // them and the pseudo-header length is the payload length minus their bytes (IP_DatagramLen =
 // IP_TotLen - IPv6_ExtHdrLen, net_ipv6.c:5682). A Fragment header (44) means FRAGMENT: the
 // transport checksum covers the reassembled datagram. Any other extension header (AH, ESP,
-// Mobility, No Next Header, experimental values), a chain past that window or a Hop-by-Hop header
-// after the first gets EXT_HDR and no transport verdict; an extension header running past the
-// payload is MALFORMED (INVALID_EH_LEN).
+// Mobility, No Next Header, experimental values) or a Hop-by-Hop header after the first gets EXT_HDR
+// and no transport verdict; so does a chain past that window, which the walk pass
+// (netcsum_v6walk.hip) then finishes; an extension header running past the payload is MALFORMED
+// (INVALID_EH_LEN).
 __device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
     return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 59u || nh == 60u ||
            nh == 135u || nh == 139u || nh == 140u || nh == 253u || nh == 254u;

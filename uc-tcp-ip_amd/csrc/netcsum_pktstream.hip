@@ -28,8 +28,8 @@
 // header words of the 40-B pseudo-header are added in registers; ICMPv6 types 1/3/4 on Rx subtract
 // all of [0, transport start) (no pseudo-header, net_icmpv6.c:2910-2920). Hop-by-Hop / Routing /
 // Destination Options headers are walked inside the lane's window: the first 96 - lead bytes of the
-// datagram (lead = its address mod 16), the window(lead) of oracle_packets._parse6; a chain beyond it
-// gets EXT_HDR, exactly as the lane-group kernel does beyond its 16 G - lead bytes.
+// datagram (lead = its address mod 16); a chain beyond it gets EXT_HDR, as the lane-group kernel's
+// beyond its 16 G - lead bytes, and the walk pass (netcsum_v6walk.hip) finishes it.
 //
 // Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64, gap <= 64 B).
 #include <hip/hip_runtime.h>
