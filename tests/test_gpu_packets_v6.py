@@ -303,3 +303,84 @@ def test_v6_extreme_sizes(group):
         want_pkt, want_f = op.tx_finalize_v6(bytes(stale[o:o + n]), True)
         assert bytes(out[o:o + n]) == want_pkt, i
         assert f.cpu().numpy()[i] == want_f, i
+
+
+_TAILS = ["tcp", "udp", "udp0", "udp_badlen", "tcp_short", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other",
+          "corrupt_l4", "frag", "esp", "hbh_late", "overrun", "trunc"]
+
+
+def _long_prefix_pkt(rng, tail, big):
+    """An IPv6 datagram whose chain starts with a Destination Options header of `big` 8-B units (past
+    every batch kernel's window) and ends in `tail`: every transport outcome, Fragment, an opaque
+    header, a late Hop-by-Hop, a header running past the payload, a chain cut at the payload end."""
+    from packets import _ext_chain
+    if tail in ("frag", "esp", "hbh_late", "overrun", "trunc"):
+        inner = make_packet_v6(rng, "tcp", payload=rng.randint(0, 200))
+        chain = {"frag": [(60, big), (44, 1)], "esp": [(60, big)], "hbh_late": [(60, big), (0, 1)],
+                 "overrun": [(60, big), (43, 1)], "trunc": [(60, big)]}[tail]
+        final = {"esp": 50, "trunc": 43}.get(tail, 6)
+        nh, ext = _ext_chain(rng, chain, final)
+        body = ext + (b"" if tail == "trunc" else inner[40:])
+    else:
+        inner = make_packet_v6(rng, "tcp" if tail == "corrupt_l4" else tail, payload=rng.randint(0, 300))
+        nh, ext = _ext_chain(rng, [(60, big)] + [(43, 1)] * rng.randint(0, 5), inner[6])
+        body = ext + inner[40:]
+    p = bytearray(inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40] + body)
+    if tail == "overrun":
+        p[40 + 8 * big + 1] = 255
+    if tail not in ("overrun", "trunc", "frag", "esp", "hbh_late"):
+        p = bytearray(op.tx_finalize_v6(bytes(p), udp_tx_csum=(tail != "udp0"))[0])
+    if tail == "corrupt_l4":
+        k = rng.randint(40 + 8 * big, len(p) - 1)
+        p[k] ^= 1 << rng.randint(0, 7)
+    return bytes(p)
+
+
+@pytest.mark.parametrize("form", ["varlen8", "varlen64", "strided"])
+def test_v6_long_chain_outcomes_vs_oracle(form):
+    """Every outcome behind a chain the batch kernels cannot hold (the walk pass decides them all):
+    Rx verdicts and Tx bytes + flags (stale fields, UDP checksums on) equal the oracle's, in the
+    lane-group kernel (G = 8 / 64, packed odd offsets) and the run-stream kernel (strided)."""
+    rng = random.Random({"varlen8": 1, "varlen64": 2, "strided": 3}[form] + 4400)
+    pkts = [_long_prefix_pkt(rng, t, rng.choice([17, 40, 129, 140])) for t in _TAILS for _ in range(4)]
+    rng.shuffle(pkts)
+    want_rx = np.array([op.rx_validate_v6(p) for p in pkts], np.uint8)
+    want_tx = [op.tx_finalize_v6(p, True) for p in pkts]
+    assert (want_rx & op.MALFORMED).any() and (want_rx & op.FRAGMENT).any() and (want_rx & op.EXT_HDR).any()
+    assert (want_rx & op.L4_MALFORMED).any() and (want_rx & op.UDP_NO_CSUM).any()
+    assert ((want_rx & (op.L4_CHECKED | op.L4_OK)) == op.L4_CHECKED).any() and (want_rx & op.L4_OK).any()
+    n = len(pkts)
+    if form == "strided":
+        L = 2048
+        buf = np.frombuffer(rng.randbytes(n * L + 64), np.uint8).copy()
+        for i, p in enumerate(pkts):
+            buf[i * L:i * L + len(p)] = np.frombuffer(p, np.uint8)
+        want_buf = buf.copy()
+        for i, (q, _f) in enumerate(want_tx):
+            want_buf[i * L:i * L + len(q)] = np.frombuffer(q, np.uint8)
+        b = torch.from_numpy(buf).to(DEV)
+        f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.rx_validate_ipv6(b, n, f, stride=L, pkt_len=L)
+        torch.cuda.synchronize()
+        assert netcsum.last_launch().startswith("pkt_stream_kernel")
+        rx = f.cpu().numpy()
+        ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.tx_finalize_ipv6(b, n, ft, stride=L, pkt_len=L)
+    else:
+        netcsum.tune(netcsum.TUNE_GROUP_LANES, 8 if form == "varlen8" else 64)
+        buf, offs, lens = packed_batch(pkts, rng)
+        want_buf = buf.copy()
+        for o, (q, _f) in zip(offs.tolist(), want_tx):
+            want_buf[o:o + len(q)] = np.frombuffer(q, np.uint8)
+        b, o, ln = _dev(buf, offs, lens)
+        f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.rx_validate_ipv6(b, n, f, off=o, lens=ln)
+        torch.cuda.synchronize()
+        rx = f.cpu().numpy()
+        ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.tx_finalize_ipv6(b, n, ft, off=o, lens=ln)
+    torch.cuda.synchronize()
+    bad = np.nonzero(rx != want_rx)[0]
+    assert bad.size == 0, [(int(i), int(rx[i]), int(want_rx[i])) for i in bad[:6]]
+    assert np.array_equal(ft.cpu().numpy(), np.array([fl for _q, fl in want_tx], np.uint8))
+    assert np.array_equal(b.cpu().numpy(), want_buf)
