@@ -332,10 +332,21 @@ __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u3
     return p;
 }
 
+#ifndef NETCSUM_TX_FIELD_STORE   // experiment builds: 1 non-temporal field stores, 2 system-scope
+#define NETCSUM_TX_FIELD_STORE 0 // (write-through) field stores, in the one-pass Tx (TUNE_TX_PASSES 1)
+#endif
 __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memcpy of a host-order u16
     __attribute__((address_space(1))) uint8_t* q = (__attribute__((address_space(1))) uint8_t*)p;
-    q[0] = (uint8_t)(v & 0xFFu);
-    q[1] = (uint8_t)(v >> 8);
+    if constexpr (NETCSUM_TX_FIELD_STORE == 1) {
+        __builtin_nontemporal_store((uint8_t)(v & 0xFFu), &q[0]);
+        __builtin_nontemporal_store((uint8_t)(v >> 8), &q[1]);
+    } else if constexpr (NETCSUM_TX_FIELD_STORE == 2) {
+        __hip_atomic_store(p, (uint8_t)(v & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 1, (uint8_t)(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        q[0] = (uint8_t)(v & 0xFFu);
+        q[1] = (uint8_t)(v >> 8);
+    }
 }
 
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
