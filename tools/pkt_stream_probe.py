@@ -34,6 +34,9 @@ def main():
     if ver in ("6", "mix"):
         v[:, 0:8] = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8, device=dev)
         rx_fn, tx_fn = netcsum.rx_validate_ipv6, netcsum.tx_finalize_ipv6
+        if os.environ.get("PS_CHAIN"):   # every datagram: a 200-B Destination Options header before TCP
+            v[:, 6] = 60                  # (past every batch kernel's window: the walk pass's worst case)
+            v[:, 40:42] = torch.tensor([6, 24], dtype=torch.uint8, device=dev)
         if ver == "mix":
             v[0::2, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8,
                                          device=dev)

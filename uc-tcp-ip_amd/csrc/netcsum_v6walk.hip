@@ -7,7 +7,7 @@
 // NetIPv6_RxOptHdr, Routing via NetIPv6_RxRoutingHdr, length (HdrExtLen + 1) * 8, net_ipv6.c:8601,
 // until the next header is not an extension header), so this pass finishes exactly those datagrams:
 //
-//   one wave per 1024 flags; the datagrams whose flag has EXT_HDR are found by a ballot, and the whole wave
+//   one wave per 64 flags; the datagrams whose flag has EXT_HDR are found by a ballot, and the whole wave
 //   takes each of them in turn: the chain is walked with wave-uniform loads (no window, no header
 //   count), then the transport part [off, tot) and the addresses [8, 40) are summed with the wave's
 //   64 lanes reading half-words in parallel, and the verdict (Rx) or the checksum field (Tx) and the
@@ -175,39 +175,20 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
     }
 }
 
-// Each lane scans 16 flags (one 16-B load when the flags are 16-B aligned): a wave covers 1024
-// datagrams, so 1 M datagrams take 256 workgroups.
+// One flag per lane, one wave per 64 datagrams: a batch in which every datagram needs the walk (an
+// adversarial ring of long chains) spreads over n / 64 waves instead of queueing behind a few (a
+// 16-flags-per-lane scan read the flags no faster: 4.8 us per 1 M either way, profiles/r2zt_*).
 template <bool TX>
 __global__ void __launch_bounds__(256) pkt_v6_walk_kernel(PktBatchArgs A) {
-    constexpr uint64_t kPerWave = 64u * 16u;
     const uint32_t lane = threadIdx.x & 63u;
-    const bool vec = (((uintptr_t)A.flags_out) & 15u) == 0u;
-    for (uint64_t w0 = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * kPerWave; w0 < A.n;
-         w0 += (uint64_t)gridDim.x * 4u * kPerWave) {
-        const uint64_t b0 = w0 + 16u * lane;
-        uint32_t hit = 0u;                          // bit k: datagram b0 + k has EXT_HDR
-        if (vec && b0 + 16u <= A.n) {
-            const uint4 v = *reinterpret_cast<const uint4*>(A.flags_out + b0);
-            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                hit |= ((d[k >> 2] >> (8 * (k & 3) + 7)) & 1u) << k;
-            }
-        } else {
-            for (uint32_t k = 0; k < 16u && b0 + k < A.n; ++k) {
-                hit |= ((A.flags_out[b0 + k] & W_EXT_HDR) ? 1u : 0u) << k;
-            }
-        }
-        uint64_t m = __ballot(hit != 0u);           // wave-uniform
+    for (uint64_t w0 = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); w0 < A.n; w0 += (uint64_t)gridDim.x * 256u) {
+        const uint64_t i = w0 + lane;
+        const bool need = i < A.n && (A.flags_out[i] & W_EXT_HDR) != 0u;
+        uint64_t m = __ballot(need);                // wave-uniform
         while (m != 0u) {
             const uint32_t j = (uint32_t)__builtin_ctzll(m);
             m &= m - 1u;
-            uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hit, (int)j);
-            while (h != 0u) {
-                const uint32_t k = (uint32_t)__builtin_ctz(h);
-                h &= h - 1u;
-                walk_one<TX>(A, (uint32_t)(w0 + 16u * j + k), lane);
-            }
+            walk_one<TX>(A, (uint32_t)w0 + j, lane);
         }
     }
 }
@@ -217,8 +198,8 @@ __global__ void __launch_bounds__(256) pkt_v6_walk_kernel(PktBatchArgs A) {
 hipError_t launch_pkt_v6_walk(const PktBatchArgs& a, bool tx, int cus, hipStream_t s) {
     if (a.n == 0u) return hipSuccess;
     if (a.flags_out == nullptr) return hipErrorInvalidValue;
-    const uint64_t blocks = ((uint64_t)a.n + 4095u) / 4096u;
-    const int grid = (int)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 8u);
+    const uint64_t blocks = ((uint64_t)a.n + 255u) / 256u;
+    const int grid = (int)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 64u);
     if (tx) {
         hipLaunchKernelGGL(pkt_v6_walk_kernel<true>, dim3(grid), dim3(256), 0, s, a);
     } else {
