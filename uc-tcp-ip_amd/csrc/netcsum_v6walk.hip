@@ -7,11 +7,11 @@
 // NetIPv6_RxOptHdr, Routing via NetIPv6_RxRoutingHdr, length (HdrExtLen + 1) * 8, net_ipv6.c:8601,
 // until the next header is not an extension header), so this pass finishes exactly those datagrams:
 //
-//   one wave per 64 flags; the datagrams whose flag has EXT_HDR are found by a ballot, and the whole wave
-//   takes each of them in turn: the chain is walked with wave-uniform loads (no window, no header
-//   count), then the transport part [off, tot) and the addresses [8, 40) are summed with the wave's
-//   64 lanes reading half-words in parallel, and the verdict (Rx) or the checksum field (Tx) and the
-//   flag are written by lane 0 (vector stores).
+//   one wave per 64 flags; the datagrams whose flag has EXT_HDR are found by a ballot, and a 16-lane
+//   group of the wave takes each of them (four at a time): the chain is walked with group-uniform loads (no window, no header
+//   count), then the transport part [off, tot) and the addresses [8, 40) are summed with the group's
+//   16 lanes reading half-words in parallel, and the verdict (Rx) or the checksum field (Tx) and the
+//   flag are written by the group's lane 0 (vector stores).
 //
 // Datagrams are rare on this path (chains of more than 4 headers or longer than ~50 bytes), so the
 // pass costs one launch that reads the n flag bytes (1 MB for 1 M datagrams) when no datagram needs
@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "netcsum_device.h"
 #include "netcsum_kernels.h"
 
 namespace netcsum {
@@ -44,19 +45,32 @@ __device__ __forceinline__ uint32_t be16(const uint8_t* p, uint32_t k) {
     return ((uint32_t)p[k] << 8) | (uint32_t)p[k + 1u];
 }
 
-// Big-endian half-word sum of packet bytes [lo, hi) (lo even; an odd last octet padded with zero),
-// the half-word at `skip` (even, or ~0u) counted as zero; the wave's lanes take every 64th half-word.
-__device__ __forceinline__ uint32_t wave_sum(const uint8_t* p, uint32_t lo, uint32_t hi, uint32_t skip, uint32_t lane) {
+// A datagram is finished by a group of kLanes lanes (a wave takes 4 datagrams at a time).
+constexpr uint32_t kLanes = 16u;
+
+// Ones'-complement sum, in big-endian half-words of the datagram, of its bytes [lo, hi) (lo even; an
+// odd last octet padded with zero), the half-word at `skip` (even, or ~0u) counted as zero, folded to
+// 16 bits (0 iff every counted octet is 0). The group's lanes read whole aligned 16-B chunks (bytes
+// outside [lo, hi) masked; a chunk never leaves the 16-B block, hence the page, of a datagram byte)
+// and add their little-endian half-words with v_sad_u16: with the datagram at an even address those
+// are the big-endian ones byte-swapped, at an odd address they ARE the big-endian ones (RFC 1071 §2).
+__device__ __forceinline__ uint32_t group_sum(const uint8_t* p, uint32_t lo, uint32_t hi, uint32_t skip, uint32_t lane) {
+    const uintptr_t s0 = (uintptr_t)p + lo, e0 = (uintptr_t)p + hi;
     uint32_t s = 0u;
-    for (uint32_t k = lo + 2u * lane; k < hi; k += 128u) {
-        const uint32_t w = ((uint32_t)p[k] << 8) | ((k + 1u < hi) ? (uint32_t)p[k + 1u] : 0u);
-        s += (k == skip) ? 0u : w;                  // <= 512 half-words per lane: no overflow
-    }
+    for (uintptr_t c = (s0 & ~(uintptr_t)15u) + 16u * lane; c < e0; c += 16u * kLanes) {
+        const u32x4 v = *reinterpret_cast<gu32x4*>(c);
+        s = sum4(mask_chunk(v, (int)((intptr_t)s0 - (intptr_t)c), (int)((intptr_t)e0 - (intptr_t)c)), s);
+    }                                               // <= 258 chunks of 8 half-words per lane
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s += (uint32_t)__shfl_xor((int)s, o, 64);
+    for (int o = (int)kLanes / 2; o > 0; o >>= 1) {
+        s += (uint32_t)__shfl_xor((int)s, o, (int)kLanes);
+    }                                               // < 2^31 for a 65 575-byte datagram
+    const uint32_t odd = (uint32_t)((uintptr_t)p & 1u);
+    if (skip != ~0u) {                              // exact: those two octets were added above
+        s -= ((uint32_t)p[skip] << (8u * odd)) + ((uint32_t)p[skip + 1u] << (8u * (odd ^ 1u)));
     }
-    return s;                                       // < 2^31 for a 65 575-byte datagram
+    const uint32_t r = fold16(s);
+    return odd ? r : rot8(r);
 }
 
 __device__ __forceinline__ uint32_t fold(uint32_t s) {
@@ -65,7 +79,7 @@ __device__ __forceinline__ uint32_t fold(uint32_t s) {
     return s;                                       // 0 iff every summed half-word was 0
 }
 
-// The whole wave finishes datagram i (all values below are wave-uniform).
+// A lane group finishes datagram i (all values below are uniform in the group; lane = its lane).
 template <bool TX>
 __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
     uint64_t off64;
@@ -151,10 +165,10 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
         }
     }
     if (check) {
-        uint32_t s = wave_sum(p, off, tot, TX ? csum_off : ~0u, lane);
+        uint32_t s = group_sum(p, off, tot, TX ? csum_off : ~0u, lane);
         if (pseudo) {
-            s += wave_sum(p, 8u, 40u, ~0u, lane) + (tot - off) + nh;   // addresses, length, next header
-        }
+            s += group_sum(p, 8u, 40u, ~0u, lane) + (tot - off) + nh;   // addresses, length, next header
+        }                                           // (folded values: no overflow)
         const uint32_t r = fold(s);
         if constexpr (TX) {
             uint32_t c = (~r) & 0xFFFFu;
@@ -177,18 +191,29 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
 
 // One flag per lane, one wave per 64 datagrams: a batch in which every datagram needs the walk (an
 // adversarial ring of long chains) spreads over n / 64 waves instead of queueing behind a few (a
-// 16-flags-per-lane scan read the flags no faster: 4.8 us per 1 M either way, profiles/r2zt_*).
+// 16-flags-per-lane scan read the flags no faster: 4.8 us per 1 M either way, profiles/r2zt_*), and
+// the wave's four 16-lane groups take the next four flagged datagrams at a time (their dependent
+// chain loads overlap).
 template <bool TX>
 __global__ void __launch_bounds__(256) pkt_v6_walk_kernel(PktBatchArgs A) {
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t grp = lane / kLanes;
     for (uint64_t w0 = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); w0 < A.n; w0 += (uint64_t)gridDim.x * 256u) {
         const uint64_t i = w0 + lane;
         const bool need = i < A.n && (A.flags_out[i] & W_EXT_HDR) != 0u;
         uint64_t m = __ballot(need);                // wave-uniform
-        while (m != 0u) {
-            const uint32_t j = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1u;
-            walk_one<TX>(A, (uint32_t)w0 + j, lane);
+        while (m != 0u) {                           // group g takes the g-th lowest set bit
+            uint32_t j = ~0u;
+#pragma unroll
+            for (uint32_t g = 0; g < 64u / kLanes; ++g) {
+                if (m != 0u) {
+                    j = (g == grp) ? (uint32_t)__builtin_ctzll(m) : j;
+                    m &= m - 1u;
+                }
+            }
+            if (j != ~0u) {
+                walk_one<TX>(A, (uint32_t)w0 + j, lane % kLanes);
+            }
         }
     }
 }
