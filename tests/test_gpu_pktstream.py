@@ -244,6 +244,7 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     rx, tx, txf, d_rx, d_tx = _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
     tag = "v6" if ver == 6 else "mixed"
     assert d_rx.startswith("pkt_stream_kernel") and f",rx,{tag}>" in d_rx and f",tx,{tag}>" in d_tx, (d_rx, d_tx)
+    assert d_rx.endswith(" +pkt_v6_walk_kernel") and d_tx.endswith(" +pkt_v6_walk_kernel"), (d_rx, d_tx)
     bad = np.nonzero(rx != rx_w)[0]
     assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
     bad = np.nonzero(tx != tx_w)[0]

@@ -775,9 +775,10 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
         const bool two = tx && g_tune_tx_passes.load() != 1;
-        char desc[112];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s", d, snt ? ",nt" : "",
-                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "");
+        char desc[136];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s", d, snt ? ",nt" : "",
+                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
+                 walk ? " +pkt_v6_walk_kernel" : "");
         netcsum::set_last_launch(desc);
         if (two) {
             // the records live in this stream's scratch buffer (stream_scratch)
@@ -798,9 +799,9 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         return NET_UTIL_ERR_NONE;
     }
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
-    char desc[96];
-    snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u", c.group_lanes,
-             c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile);
+    char desc[120];
+    snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u%s", c.group_lanes,
+             c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile, walk ? " +pkt_v6_walk_kernel" : "");
     netcsum::set_last_launch(desc);
     if (own_flags) {
         void* fl = nullptr;
