@@ -64,19 +64,13 @@ __device__ __forceinline__ uint32_t group_sum(const uint8_t* p, uint32_t lo, uin
 #pragma unroll
     for (int o = (int)kLanes / 2; o > 0; o >>= 1) {
         s += (uint32_t)__shfl_xor((int)s, o, (int)kLanes);
-    }                                               // < 2^31 for a 65 575-byte datagram
+    }                                               // < 2^32: 32 788 half-words at most
     const uint32_t odd = (uint32_t)((uintptr_t)p & 1u);
     if (skip != ~0u) {                              // exact: those two octets were added above
         s -= ((uint32_t)p[skip] << (8u * odd)) + ((uint32_t)p[skip + 1u] << (8u * (odd ^ 1u)));
     }
     const uint32_t r = fold16(s);
     return odd ? r : rot8(r);
-}
-
-__device__ __forceinline__ uint32_t fold(uint32_t s) {
-    s = (s & 0xFFFFu) + (s >> 16);
-    s = (s & 0xFFFFu) + (s >> 16);
-    return s;                                       // 0 iff every summed half-word was 0
 }
 
 // A lane group finishes datagram i (all values below are uniform in the group; lane = its lane).
@@ -169,7 +163,7 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
         if (pseudo) {
             s += group_sum(p, 8u, 40u, ~0u, lane) + (tot - off) + nh;   // addresses, length, next header
         }                                           // (folded values: no overflow)
-        const uint32_t r = fold(s);
+        const uint32_t r = fold16(s);
         if constexpr (TX) {
             uint32_t c = (~r) & 0xFFFFu;
             if (nh == 17u && c == 0u) {
