@@ -148,3 +148,37 @@ def test_mixed_dispatch_follows_the_version_nibble():
         assert op.rx_validate_ip(swapped) == op.rx_validate_v6(swapped)
         assert op.tx_finalize_ip(p6) == op.tx_finalize_v6(p6)
     assert op.rx_validate_ip(b"") == op.MALFORMED
+
+
+def test_chains_of_any_length_and_their_outcomes():
+    """The oracle walks Hop-by-Hop / Routing / Destination Options chains of any length and header
+    count (net_ipv6.c:8411-8418): 1..20 headers of 1..140 units reach the transport header; a chain
+    cut at the payload end or running past it is MALFORMED; Fragment / an opaque header / a late
+    Hop-by-Hop after a long chain keep their outcomes."""
+    from packets import _ext_chain
+    rng = random.Random(69)
+    for _ in range(200):
+        inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(0, 200))
+        kinds = [(rng.choice([43, 60]), rng.randint(1, 140 if k == 0 else 3)) for k in range(rng.randint(1, 20))]
+        if rng.random() < 0.3:
+            kinds = [(0, rng.randint(1, 4))] + kinds                 # Hop-by-Hop first: allowed
+        nh, ext = _ext_chain(rng, kinds, inner[6])
+        body = ext + inner[40:]
+        pkt, ft = op.tx_finalize_v6(inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40] + body)
+        assert ft == op.IP_OK | op.L4_CHECKED | op.L4_OK
+        assert op.rx_validate_v6(pkt) == op.IP_OK | op.L4_CHECKED | op.L4_OK
+        fx, off, ulen, nh2, _ = op._parse6(pkt)
+        assert fx == 0 and off == 40 + len(ext) and ulen == len(inner) - 40 and nh2 == inner[6]
+    for tail, want in ((44, op.IP_OK | op.FRAGMENT), (50, op.IP_OK | op.EXT_HDR), (0, op.IP_OK | op.EXT_HDR)):
+        kinds = [(60, 100), (43, 2)] + ([(44, 1)] if tail == 44 else [(0, 1)] if tail == 0 else [])
+        nh, ext = _ext_chain(rng, kinds, 6 if tail != 50 else 50)
+        body = ext + bytes(40)
+        pkt = struct.pack("!IHBB32s", 6 << 28, len(body), nh, 64, bytes(32)) + body
+        assert op.rx_validate_v6(pkt) == want, tail
+    nh, ext = _ext_chain(rng, [(60, 100)], 43)                        # next header 43, no bytes left
+    pkt = struct.pack("!IHBB32s", 6 << 28, len(ext), nh, 64, bytes(32)) + ext
+    assert op.rx_validate_v6(pkt) == op.MALFORMED
+    nh, ext = _ext_chain(rng, [(60, 100), (43, 1)], 6)
+    b = bytearray(struct.pack("!IHBB32s", 6 << 28, len(ext) + 20, nh, 64, bytes(32)) + ext + bytes(20))
+    b[40 + 800 + 1] = 200                                             # the Routing header runs past the payload
+    assert op.rx_validate_v6(bytes(b)) == op.MALFORMED
