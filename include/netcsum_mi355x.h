@@ -279,6 +279,96 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIP       (void            *d_base,
                                             void            *hip_stream);
 
 /* ============================================================================================
+ * (2b'') Burst adapters for the reference's own checksum-offload seam.
+ *
+ * The reference builds with NET_{IPV4,ICMP,UDP,TCP}_CFG_CHK_SUM_OFFLOAD_{RX,TX}_EN
+ * (Cfg/Template/net_cfg.h:669-682, mapped to NET_*_CHK_SUM_OFFLOAD_{RX,TX} at
+ * Source/net_cfg_net.h:174-190, 305-366) when "the controller" computes the checksums: the stack
+ * then skips those calls. These two entry points ARE that controller, one launch per NIC burst:
+ *
+ * RxBurst — run before the burst is handed to the stack (NetIF_Rx). d_action[i] is one of
+ *   NETCSUM_RX_* below. With the Rx offload flags enabled the stack assumes every checksum valid
+ *   (net_ipv4.c:5243-5244, net_tcp.c:7847-7848 / :7868-7869, net_udp.c:1925-1927 / :1944-1946,
+ *   net_icmpv4.c:1673-1674 / :1683-1684, net_icmpv6.c:2931-2932), so a frame whose checksum fails
+ *   must be dropped HERE; a frame the reference would reject for any other reason (header shape,
+ *   lengths, types, addresses, ports) is delivered and the stack's own checks, which the offload
+ *   flags do not remove, reject it. Decisions therefore equal the reference's with the flags off:
+ *   a frame is delivered iff its checksums pass (or it carries none), and every frame the
+ *   reference drops at a checksum check is dropped. The DROP code names the counter the reference
+ *   increments at that check; for a frame that ALSO fails an earlier non-checksum check (an
+ *   ICMPv4 type/code/length, net_icmpv4.c:1500-1659) the reference counts that check instead.
+ *   IPv4 fragments: the transport checksum covers the reassembled datagram (net_ipv4.c:6523), which
+ *   a per-frame burst does not hold; they are verified at the IP header only (DELIVER_L4_UNVERIFIED,
+ *   what any offloading NIC does; ChkSumBatchChains verifies reassembled datagrams).
+ *   IGMP (net_igmp.c:1332) and ICMPv6 types 1/3/4 (net_icmpv6.c:2913) have no offload flag; the
+ *   adapter drops their checksum failures too (same decision, same counter), so the stack's own
+ *   per-packet call only ever sees valid ones.
+ *   rx_cfg: NETCSUM_RXCFG_UDP_DISCARD_NO_CHK_SUM = the stack's NET_UDP_CFG_RX_CHK_SUM_DISCARD_EN
+ *   (net_udp.c:1972-1977: UDP datagrams without a checksum are dropped); 0 = the template default.
+ *   d_flags (optional, NULL allowed) receives the NETCSUM_PKT_* verdicts of RxValidateIP.
+ *
+ * TxBurst — run on frames the stack built with the Tx offload flags, before they go to the NIC:
+ *   the stack left 0 in the IPv4 header checksum (net_ipv4.c:9575-9586, :10160-10171), 0 in TCP
+ *   (net_tcp.c:29813-29815, :29845-29847) and ICMPv4 (net_icmpv4.c:1046, :2225, :2245, :3093,
+ *   :3124), and in UDP the placeholder 0xFFFF: its own 0 -> 0xFFFF mapping (net_udp.c:2929-2931)
+ *   runs on the offload's 0 (:2877-2878, :2901-2902). A UDP field of 0 means "no checksum"
+ *   (NET_UDP_CFG_TX_CHK_SUM_EN / NET_UDP_FLAG_TX_CHK_SUM_DIS, net_udp.c:2863-2867, :2934-2935) and
+ *   is left 0. Every other checksum field is computed as if zero and written in place (as
+ *   TxFinalizeIP, UDP 0 -> 0xFFFF). Fields the stack computed itself — ICMPv6 and ICMPv4 echo
+ *   requests, whose guards test the never-defined NET_ICMP_CFG_CHK_SUM_OFFLOAD_TX
+ *   (net_icmpv6.c:1439, :1521, :2224, :2273, :2322, :2354; net_icmpv4.c:2201), and IGMP, which has
+ *   no flag (net_igmp.c:1692) — are rewritten with the value they already hold. Frames starting at
+ *   the IP header, mixed IPv4 / IPv6 as RxValidateIP / TxFinalizeIP.
+ * ============================================================================================ */
+#define NETCSUM_RX_DELIVER                 0u  /* hand to the stack                                  */
+#define NETCSUM_RX_DROP_IPV4_CHK_SUM       1u  /* IPv4.RxInvChkSumCtr      net_ipv4.c:5251-5254        */
+#define NETCSUM_RX_DROP_TCP_CHK_SUM        2u  /* TCP.RxHdrChkSumCtr       net_tcp.c:7886-7889         */
+#define NETCSUM_RX_DROP_UDP_CHK_SUM        3u  /* UDP.RxHdrChkSumCtr       net_udp.c:1963-1967         */
+#define NETCSUM_RX_DROP_UDP_NO_CHK_SUM     4u  /* UDP.RxHdrChkSumCtr       net_udp.c:1973-1977         */
+#define NETCSUM_RX_DROP_ICMPV4_CHK_SUM     5u  /* ICMPv4.RxInvChkSumCtr    net_icmpv4.c:1697-1700      */
+#define NETCSUM_RX_DROP_IGMP_CHK_SUM       6u  /* IGMP.RxHdrChkSumCtr      net_igmp.c:1335-1339        */
+#define NETCSUM_RX_DROP_ICMPV6_CHK_SUM     7u  /* ICMPv6.RxHdrChkSumCtr    net_icmpv6.c:2952-2955      */
+#define NETCSUM_RX_DELIVER_L4_UNVERIFIED   8u  /* IPv4 / IPv6 fragment: IP layer verified only       */
+#define NETCSUM_RX_NBR_ACTIONS             9u
+
+#define NETCSUM_RXCFG_UDP_DISCARD_NO_CHK_SUM  0x1u
+
+NET_ERR  NetUtil_MI355X_RxBurst            (const void      *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint32_t         rx_cfg,
+                                            uint8_t         *d_action,
+                                            uint8_t         *d_flags,
+                                            void            *hip_stream);
+
+NET_ERR  NetUtil_MI355X_TxBurst            (void            *d_base,
+                                            const uint64_t  *d_off,
+                                            const uint16_t  *d_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *d_flags,
+                                            void            *hip_stream);
+
+/* The action of one datagram from its RxValidateIP verdict `flags` (NETCSUM_PKT_*), the transport
+ * protocol its checksum verdict covers (6, 17, 1, 2, 58) and its IP version: the function the Rx
+ * burst kernels apply per frame, as host logic (no device work). */
+uint8_t  NetUtil_MI355X_RxAction           (uint8_t          flags,
+                                            uint8_t          proto,
+                                            int              ipv6,
+                                            uint32_t         rx_cfg);
+
+/* Host tally of a burst's actions (after copying d_action to the host): ctr[a] += number of frames
+ * with action a, a < NETCSUM_RX_NBR_ACTIONS — the increments the stack's Net_ErrCtrs would have seen
+ * (NET_CTR_ERR_INC at the lines above). Host logic, no device work. */
+NET_ERR  NetUtil_MI355X_RxBurstTally       (const uint8_t   *h_action,
+                                            uint32_t         n_pkt,
+                                            uint32_t        *ctr);
+
+/* ============================================================================================
  * (2c) Batched NET_BUF chains. Chain i = its pseudo-header
  * (d_pseudo + i*pseudo_stride, pseudo_len bytes; none if pseudo_len = 0) followed by pieces
  * [d_chain_first[i], d_chain_first[i+1]) in order, piece j = d_base + d_piece_off[j] with

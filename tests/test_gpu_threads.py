@@ -116,3 +116,66 @@ def test_thread_contexts_released():
     assert netcsum.thread_release() == 200
     assert netcsum.DataCalc(ch.ptr, None, 0) == want
     assert netcsum.thread_release() == 200
+
+
+def test_scratch_buffers_many_threads_many_streams():
+    """The packet / varlen scratch (two-pass Tx records, the varlen run word) is per thread and per
+    stream (netcsum_abi.hip ScratchLease): 4 threads x 24 streams each — more streams than a
+    thread's 16 slots, so slots are evicted and re-created while launches on other streams are in
+    flight — run two-pass Tx finalize and adaptive-run varlen batches at once; every result equals
+    the oracle's."""
+    import numpy as np
+    import oracle_packets as op
+    from packets import make_packet, packed_batch
+
+    rng = random.Random(77)
+    stride, n_pkt = 1500, 96
+    tx_in = np.zeros(n_pkt * stride + 64, np.uint8)
+    tx_want = tx_in.copy()
+    for i in range(n_pkt):
+        p = make_packet(rng, rng.choice(["tcp", "udp", "icmp"]), payload=rng.randint(100, 1300))[:stride]
+        tx_in[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
+        q, _ = op.tx_finalize(bytes(tx_in[i * stride:(i + 1) * stride]))
+        tx_want[i * stride:(i + 1) * stride] = np.frombuffer(q, np.uint8)
+    segs = [rng.randbytes(rng.randint(40, 3000)) for _ in range(400)]
+    vbuf, voff, vlen = packed_batch(segs, rng, trailer=False)
+    vwant = oracle.batch_varlen(vbuf, voff, vlen, None, 0, 0)
+    errors = []
+
+    def worker(seed):
+        try:
+            torch.cuda.set_device(0)
+            streams = [torch.cuda.Stream() for _ in range(24)]
+            with torch.cuda.stream(streams[0]):
+                vb = torch.from_numpy(vbuf).cuda()
+                vo = torch.from_numpy(voff.astype(np.int64)).cuda()
+                vl = torch.from_numpy(vlen.view(np.int16)).cuda()
+            streams[0].synchronize()
+            for rnd in range(3):
+                bufs, outs = [], []
+                for s in streams:
+                    with torch.cuda.stream(s):
+                        b = torch.from_numpy(tx_in).cuda()
+                        o = torch.empty(len(segs), dtype=torch.int16, device="cuda")
+                        netcsum.tx_finalize_ipv4(b, n_pkt, stride=stride, pkt_len=stride, stream=s)
+                        netcsum.batch_varlen(vb, vo, vl, None, 0, 0, len(segs), o, stream=s)
+                        bufs.append(b)
+                        outs.append(o)
+                for s, b, o in zip(streams, bufs, outs):
+                    s.synchronize()
+                    if not np.array_equal(b.cpu().numpy(), tx_want):
+                        errors.append((seed, rnd, "tx"))
+                    if not np.array_equal(o.cpu().numpy().view(np.uint16), vwant):
+                        errors.append((seed, rnd, "varlen"))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+        finally:
+            netcsum.thread_release()
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ths)
+    assert errors == []

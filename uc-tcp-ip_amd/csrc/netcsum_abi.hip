@@ -15,6 +15,7 @@
 #include <mutex>
 
 #include "../../include/netcsum_mi355x.h"
+#include "netcsum_device.h"
 #include "netcsum_kernels.h"
 
 namespace {
@@ -282,67 +283,130 @@ NET_ERR check_op(NETCSUM_OP op, const void* d_pseudo, CPU_INT16U pseudo_len) {
     return NET_UTIL_ERR_NONE;
 }
 
-// Scratch of the two-pass Tx (8-B records between its two kernels): plain hipMalloc device memory,
-// one buffer per (device, stream) — launches on one stream are ordered, so a stream's buffer is never
-// in use by two launches at once. Memory from the stream-ordered allocator measured ~70 us slower
-// for the record stores on 1 M packets (profiles/r2tx_*), so it is not used. Up to kScratchSlots
-// buffers are kept; the least recently used is freed (after a device synchronisation) beyond that.
+// Device scratch of the packet batches (two-pass Tx records, the walk pass's flags when the caller
+// passes none) and of the varlen run word: plain hipMalloc memory (memory from the stream-ordered
+// allocator measured ~70 us slower for the record stores on 1 M packets, profiles/r2tx_*), one buffer
+// per (device, stream), kept PER HOST THREAD: only the calling thread hands a buffer out, launches on
+// it and evicts it, so no other thread can free it between the hand-out and the launches that use it.
+// A lease records an event on the stream after the launches that use its buffer; evicting (least
+// recently used, beyond kScratchSlots) or growing a buffer waits for that event — never for the whole
+// device — and a new lease whose earlier launches are still pending makes the stream wait for it, so
+// a stream created with the handle of a destroyed one whose work is still running cannot overtake it. Under stream capture no event is recorded and the
+// slot is pinned (the captured graph keeps its address): capture needs one uncaptured call first.
 constexpr int kScratchSlots = 16;
 struct ScratchSlot {
-    int dev = -1;
-    hipStream_t stream = nullptr;
-    void* p = nullptr;
-    size_t cap = 0;
-    uint64_t used = 0;
+    int                dev = -1;
+    hipStream_t        stream = nullptr;
+    void*              p = nullptr;
+    size_t             cap = 0;
+    uint64_t           used = 0;
+    hipEvent_t         ev = nullptr;  // recorded after the last launches that used p
+    bool               ev_live = false;
+    bool               pinned = false;  // used under stream capture: never freed while the thread runs
 };
 
-hipError_t stream_scratch(int dev, hipStream_t st, size_t bytes, void** out) {
-    static std::mutex mu;
-    static ScratchSlot slots[kScratchSlots];
-    static uint64_t tick = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    ScratchSlot* hit = nullptr;
-    ScratchSlot* lru = &slots[0];
-    for (ScratchSlot& sl : slots) {
-        if (sl.dev == dev && sl.stream == st && sl.p != nullptr) {
-            hit = &sl;
-            break;
-        }
-        if (sl.p == nullptr || sl.used < lru->used) lru = &sl;
+hipError_t slot_wait(ScratchSlot& sl) {                // all launches that used sl.p have finished
+    if (!sl.ev_live) return hipSuccess;
+    const hipError_t e = hipEventSynchronize(sl.ev);
+    sl.ev_live = false;
+    return e;
+}
+
+struct ScratchCache {
+    ScratchSlot slots[kScratchSlots];
+    uint64_t    tick = 0;
+
+    void drop(ScratchSlot& sl) {                       // free a slot's buffer and event (its device)
+        int cur = -1;
+        const bool have = hipGetDevice(&cur) == hipSuccess;
+        if (sl.dev >= 0) (void)hipSetDevice(sl.dev);
+        (void)slot_wait(sl);
+        if (sl.p) (void)hipFree(sl.p);
+        if (sl.ev) (void)hipEventDestroy(sl.ev);
+        if (have && cur >= 0 && cur != sl.dev) (void)hipSetDevice(cur);
+        sl = ScratchSlot{};
     }
-    if (hit == nullptr) {
-        hit = lru;
-        if (hit->p != nullptr) {                       // evict: nothing may still use it
-            hipError_t e = hipDeviceSynchronize();
-            if (e != hipSuccess) return e;
-            (void)hipSetDevice(hit->dev);
-            (void)hipFree(hit->p);
-            (void)hipSetDevice(dev);
-            *hit = ScratchSlot{};
+    void release_all() {
+        for (ScratchSlot& sl : slots) {
+            if (sl.p || sl.ev) drop(sl);
         }
-        hit->dev = dev;
-        hit->stream = st;
     }
-    if (hit->cap < bytes) {                            // grow: the stream's earlier work may use it
-        if (hit->p != nullptr) {
-            hipError_t e = hipStreamSynchronize(st);
+    ~ScratchCache() { release_all(); }
+};
+
+thread_local ScratchCache tls_scratch;
+
+// A buffer of >= `bytes` for launches on stream `st` of device `dev`; end() (or the destructor) after
+// the last launch that uses it records the slot's event.
+class ScratchLease {
+public:
+    hipError_t acquire(int dev, hipStream_t st, size_t bytes) {
+        stream_ = st;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (st != nullptr && hipStreamIsCapturing(st, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+        capturing_ = cs != hipStreamCaptureStatusNone;
+        ScratchCache& c = tls_scratch;
+        ScratchSlot* hit = nullptr;
+        ScratchSlot* lru = nullptr;
+        for (ScratchSlot& sl : c.slots) {
+            if (sl.p != nullptr && sl.dev == dev && sl.stream == st) {
+                hit = &sl;
+                break;
+            }
+            if (sl.pinned) continue;
+            if (lru == nullptr || sl.p == nullptr || (lru->p != nullptr && sl.used < lru->used)) lru = &sl;
+        }
+        if (hit == nullptr) {
+            if (lru == nullptr) return hipErrorOutOfMemory;           // every slot pinned by captures
+            if (lru->p != nullptr || lru->ev != nullptr) c.drop(*lru);  // evict: waits for its event
+            hit = lru;
+            hit->dev = dev;
+            hit->stream = st;
+        }
+        if (hit->cap < bytes) {
+            if (capturing_ || hit->pinned) return hipErrorStreamCaptureUnsupported;   // no allocation under capture
+            hipError_t e = slot_wait(*hit);                // the stream's earlier launches may use it
             if (e != hipSuccess) return e;
-            (void)hipFree(hit->p);
+            if (hit->p) (void)hipFree(hit->p);
             hit->p = nullptr;
             hit->cap = 0;
+            const size_t cap = std::max<size_t>(bytes, (size_t)1 << 20);
+            e = hipMalloc(&hit->p, cap);
+            if (e != hipSuccess) {
+                hit->p = nullptr;
+                return e;
+            }
+            hit->cap = cap;
         }
-        const size_t cap = std::max<size_t>(bytes, (size_t)1 << 20);
-        hipError_t e = hipMalloc(&hit->p, cap);
-        if (e != hipSuccess) {
-            hit->p = nullptr;
-            return e;
+        if (hit->ev_live && !capturing_ && hipEventQuery(hit->ev) == hipErrorNotReady) {
+            hipError_t e = hipStreamWaitEvent(st, hit->ev, 0);
+            if (e != hipSuccess) return e;
         }
-        hit->cap = cap;
+        if (hit->ev == nullptr && !capturing_) {
+            hipError_t e = hipEventCreateWithFlags(&hit->ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        hit->used = ++c.tick;
+        if (capturing_) hit->pinned = true;
+        slot_ = hit;
+        return hipSuccess;
     }
-    hit->used = ++tick;
-    *out = hit->p;
-    return hipSuccess;
-}
+    void* ptr() const { return slot_ ? slot_->p : nullptr; }
+    hipError_t end() {
+        ScratchSlot* sl = slot_;
+        slot_ = nullptr;
+        if (sl == nullptr || capturing_) return hipSuccess;
+        const hipError_t e = hipEventRecord(sl->ev, stream_);
+        sl->ev_live = e == hipSuccess;
+        return e;
+    }
+    ~ScratchLease() { (void)end(); }
+
+private:
+    ScratchSlot* slot_ = nullptr;
+    hipStream_t  stream_ = nullptr;
+    bool         capturing_ = false;
+};
 
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStream_t s) {
     int dev = 0;
@@ -353,11 +417,14 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         // adaptive varlen runs: a one-block kernel samples the lengths and leaves the run length in
         // this stream's scratch word, which the batch kernel reads (stream order; any value is safe:
         // the kernel never runs shorter runs than its grid covers)
-        void* word = nullptr;
-        NC_HIP(stream_scratch(dev, s, 256u, &word));
+        ScratchLease word;
+        NC_HIP(word.acquire(dev, s, 256u));
         NC_HIP(netcsum::launch_varlen_runlen(a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
-                                             c.stream_spw, static_cast<uint32_t*>(word), s));
-        a.run_dev = static_cast<const uint32_t*>(word);
+                                             c.stream_spw, static_cast<uint32_t*>(word.ptr()), s));
+        a.run_dev = static_cast<const uint32_t*>(word.ptr());
+        NC_HIP(netcsum::launch_seg_batch(a, c, s));
+        NC_HIP(word.end());
+        return NET_UTIL_ERR_NONE;
     }
     NC_HIP(netcsum::launch_seg_batch(a, c, s));
     return NET_UTIL_ERR_NONE;
@@ -587,6 +654,7 @@ NET_ERR NetUtil_MI355X_ThreadRelease(void) {
     for (int d = 0; d < kMaxDev; ++d) {
         tls_ctx[d].release();
     }
+    tls_scratch.release_all();
     return NET_UTIL_ERR_NONE;
 }
 
@@ -709,12 +777,13 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
     return NET_UTIL_ERR_NONE;
 }
 
+// udp_mode: PktBatchArgs::udp_tx_csum (Tx); d_action / rx_cfg: the Rx burst actions (Rx, optional).
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
-                         CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum, bool tx,
-                         int ip_ver, void* hip_stream) {
+                         CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, uint32_t udp_mode, bool tx,
+                         int ip_ver, void* hip_stream, uint8_t* d_action = nullptr, uint32_t rx_cfg = 0u) {
     if (n_pkt == 0) return NET_UTIL_ERR_NONE;
     if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
-    if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr)) {
+    if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr && d_action == nullptr)) {
         return NET_ERR_FAULT_NULL_PTR;
     }
     int dev = 0;
@@ -727,7 +796,9 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     a.len_u = pkt_len;
     a.n = n_pkt;
     a.flags_out = d_flags;
-    a.udp_tx_csum = udp_tx_csum ? 1u : 0u;
+    a.udp_tx_csum = udp_mode;
+    a.action_out = tx ? nullptr : d_action;
+    a.rx_cfg = rx_cfg;
     netcsum::LaunchCfg c{};
     const uint32_t chunks = d_off ? 288u : ((uint32_t)pkt_len + 30u) / 16u;
     int g = g_tune_group.load();
@@ -764,6 +835,8 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // IPv6 / mixed batches: a second pass walks the extension-header chains the batch kernel left as
     // EXT_HDR (netcsum_v6walk.hip). It reads the flags, so a Tx batch without d_flags gets them in the
     // stream's scratch buffer (after the two-pass records when there are records).
+    // (an Rx burst without d_flags keeps them there too, or nowhere for IPv4, whose kernels write
+    // each action directly)
     const bool walk = ip_ver != 4;
     const bool own_flags = walk && d_flags == nullptr;
     hipStream_t hs = static_cast<hipStream_t>(hip_stream);
@@ -780,22 +853,16 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
                  tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
                  walk ? " +pkt_v6_walk_kernel" : "");
         netcsum::set_last_launch(desc);
-        if (two) {
-            // the records live in this stream's scratch buffer (stream_scratch)
-            const size_t rec_bytes = (size_t)n_pkt * sizeof(netcsum::PktTxRecord);
-            void* rec = nullptr;
-            NC_HIP(stream_scratch(dev, hs, rec_bytes + (own_flags ? n_pkt : 0u), &rec));
-            if (own_flags) a.flags_out = static_cast<uint8_t*>(rec) + rec_bytes;
-            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs, static_cast<netcsum::PktTxRecord*>(rec)));
-        } else {
-            if (own_flags) {
-                void* fl = nullptr;
-                NC_HIP(stream_scratch(dev, hs, n_pkt, &fl));
-                a.flags_out = static_cast<uint8_t*>(fl);
-            }
-            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs));
+        ScratchLease scratch;                             // records (two-pass Tx) and / or flags
+        const size_t rec_bytes = two ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
+        if (two || own_flags) {
+            NC_HIP(scratch.acquire(dev, hs, rec_bytes + (own_flags ? n_pkt : 0u)));
+            if (own_flags) a.flags_out = static_cast<uint8_t*>(scratch.ptr()) + rec_bytes;
         }
+        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs,
+                                          two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
+        NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
@@ -803,13 +870,14 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u%s", c.group_lanes,
              c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile, walk ? " +pkt_v6_walk_kernel" : "");
     netcsum::set_last_launch(desc);
+    ScratchLease scratch;
     if (own_flags) {
-        void* fl = nullptr;
-        NC_HIP(stream_scratch(dev, hs, n_pkt, &fl));
-        a.flags_out = static_cast<uint8_t*>(fl);
+        NC_HIP(scratch.acquire(dev, hs, n_pkt));
+        a.flags_out = static_cast<uint8_t*>(scratch.ptr());
     }
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, hs));
     if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
+    NC_HIP(scratch.end());
     return NET_UTIL_ERR_NONE;
 }
 
@@ -858,7 +926,7 @@ NET_ERR NetUtil_MI355X_RxValidateIPv4(const void* d_base, const uint64_t* d_off,
 NET_ERR NetUtil_MI355X_TxFinalizeIPv4(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                       CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 4, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum ? 1u : 0u, true, 4, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_RxValidateIPv6(const void* d_base, const uint64_t* d_off, const uint16_t* d_len,
@@ -876,13 +944,33 @@ NET_ERR NetUtil_MI355X_RxValidateIP(const void* d_base, const uint64_t* d_off, c
 NET_ERR NetUtil_MI355X_TxFinalizeIPv6(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                       CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
                                       void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 6, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum ? 1u : 0u, true, 6, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_TxFinalizeIP(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                     CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, int udp_tx_csum,
                                     void* hip_stream) {
-    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum, true, 0, hip_stream);
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, udp_tx_csum ? 1u : 0u, true, 0, hip_stream);
+}
+
+// Burst adapters of the reference's checksum-offload seam (include/netcsum_mi355x.h (2b'')): the mixed
+// IPv4 / IPv6 kernels with the action written beside each verdict (Rx) and the per-datagram UDP policy
+// of the offload's 0xFFFF placeholder (Tx).
+NET_ERR NetUtil_MI355X_RxBurst(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
+                               CPU_INT16U pkt_len, uint32_t n_pkt, uint32_t rx_cfg, uint8_t* d_action, uint8_t* d_flags,
+                               void* hip_stream) {
+    if (n_pkt != 0 && d_action == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    if (rx_cfg & ~(uint32_t)NETCSUM_RXCFG_UDP_DISCARD_NO_CHK_SUM) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 1u, false, 0, hip_stream, d_action, rx_cfg);
+}
+
+uint8_t NetUtil_MI355X_RxAction(uint8_t flags, uint8_t proto, int ipv6, uint32_t rx_cfg) {
+    return (uint8_t)netcsum::rx_action(flags, proto, ipv6 != 0, rx_cfg);
+}
+
+NET_ERR NetUtil_MI355X_TxBurst(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
+                               CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, void* hip_stream) {
+    return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 2u, true, 0, hip_stream);
 }
 
 NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern,

@@ -237,17 +237,6 @@ __device__ __forceinline__ uint32_t apply_wide(const uint32_t* W, uint32_t c) {
     return W[c & 0x7FFu] ^ W[2048u + ((c >> 11) & 0x7FFu)] ^ W[4096u + (c >> 22)];
 }
 
-#ifndef NETCSUM_CRC_L1_SPLIT   // experiment builds: of the three 11-bit lookups, this many (1: the
-#define NETCSUM_CRC_L1_SPLIT 0 // [22, 32) one, 2: also [11, 22)) come from the global copy of the map
-#endif                         // (vector-memory path / L1) instead of LDS, to share the lookup load
-template <int N>
-__device__ __forceinline__ uint32_t apply_wide_split(const uint32_t* W, const uint32_t* Gm, uint32_t c) {
-    const uint32_t a = W[c & 0x7FFu];
-    const uint32_t b = N >= 2 ? Gm[2048u + ((c >> 11) & 0x7FFu)] : W[2048u + ((c >> 11) & 0x7FFu)];
-    const uint32_t d = N >= 1 ? Gm[4096u + (c >> 22)] : W[4096u + (c >> 22)];
-    return a ^ b ^ d;
-}
-
 __device__ __forceinline__ uint32_t apply(const uint32_t (*S)[256], uint32_t c) {
     return S[0][c & 0xFFu] ^ S[1][(c >> 8) & 0xFFu] ^ S[2][(c >> 16) & 0xFFu] ^ S[3][c >> 24];
 }
@@ -510,10 +499,6 @@ __global__ void __launch_bounds__(ilv_block(W)) crc_ilv_kernel(CrcBatchArgs A) {
         if constexpr (W == 2) {
             return apply_k6(last ? RT : RZ, c ^ w);
         } else if constexpr (W == 1) {
-            if constexpr (NETCSUM_CRC_L1_SPLIT > 0) {
-                return apply_wide_split<NETCSUM_CRC_L1_SPLIT>(last ? LW[0] : LW[1],
-                                                               last ? kWideTabs.w[kWideT] : kWideTabs.w[kZwide], c ^ w);
-            }
             return apply_wide(last ? LW[0] : LW[1], c ^ w);
         } else {
             return crc_word(last ? L[0] : L[kZ], c, w);
@@ -523,9 +508,6 @@ __global__ void __launch_bounds__(ilv_block(W)) crc_ilv_kernel(CrcBatchArgs A) {
         if constexpr (W == 2) {
             return apply_k6(RT, c ^ w);
         } else if constexpr (W == 1) {
-            if constexpr (NETCSUM_CRC_L1_SPLIT > 0) {
-                return apply_wide_split<NETCSUM_CRC_L1_SPLIT>(LW[0], kWideTabs.w[kWideT], c ^ w);
-            }
             return apply_wide(LW[0], c ^ w);
         } else {
             return crc_word(L[0], c, w);

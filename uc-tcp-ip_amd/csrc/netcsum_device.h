@@ -24,6 +24,29 @@ __device__ __forceinline__ uint32_t rot8(uint32_t s16) {   // x * 256 mod 65535 
     return ((s16 << 8) | (s16 >> 8)) & 0xFFFFu;
 }
 
+// Rx burst action (NetUtil_MI355X_RxBurst, include/netcsum_mi355x.h (2b'')) of a datagram from its
+// NETCSUM_PKT_* verdict `f` and the transport protocol whose checksum the verdict covers. The order
+// of the tests is the reference's order of checks: the IPv4 header's shape (MALFORMED, delivered: the
+// stack rejects it itself), the IPv4 header checksum (net_ipv4.c:5243-5254), fragments (transport
+// verified after reassembly, net_ipv4.c:6523), transport shape (delivered), then the transport
+// checksum of each protocol.
+__host__ __device__ __forceinline__ uint32_t rx_action(uint32_t f, uint32_t proto, bool v6, uint32_t rx_cfg) {
+    if (f & 0x10u) return 0u;                                    // MALFORMED: NETCSUM_RX_DELIVER
+    if (!v6 && !(f & 0x01u)) return 1u;                          // IPv4 header checksum failed
+    if (f & 0x20u) return 8u;                                    // FRAGMENT: DELIVER_L4_UNVERIFIED
+    if (f & 0xC0u) return 0u;                                    // EXT_HDR / L4_MALFORMED: the stack
+    if (f & 0x08u) return (rx_cfg & 1u) ? 4u : 0u;               // UDP without a checksum (net_udp.c:1971)
+    if ((f & 0x06u) != 0x04u) return 0u;                         // not checked, or checked and valid
+    switch (proto) {
+    case 6u:  return 2u;                                         // TCP
+    case 17u: return 3u;                                         // UDP
+    case 1u:  return v6 ? 0u : 5u;                               // ICMPv4
+    case 2u:  return v6 ? 0u : 6u;                               // IGMP
+    case 58u: return v6 ? 7u : 0u;                               // ICMPv6
+    default:  return 0u;
+    }
+}
+
 template <bool NT>
 __device__ __forceinline__ u32x4 load16(gu32x4* p) {
     if constexpr (NT) {

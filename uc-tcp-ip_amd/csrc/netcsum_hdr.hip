@@ -157,11 +157,7 @@ __global__ void __launch_bounds__(256) seg_hdr_kernel(SegBatchArgs A, uint32_t n
 #pragma unroll
         for (int hh = 0; hh < H; ++hh) {
             const uint32_t j = 64u * (uint32_t)hh + lane;
-#if defined(NETCSUM_HDR_DROP_STORES)   // experiment builds: every store out of range
-            const uint32_t h = h0 + j + 0x40000000u;
-#else
             const uint32_t h = h0 + j;
-#endif
             const uint32_t s = sres[hh];
             if (verify) {
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(s == 0xFFFFu ? 1u : 0u), ro,

@@ -56,9 +56,17 @@ struct PktBatchArgs {
     uint32_t        n;
     uint8_t*        flags_out;     // NETCSUM_PKT_* per packet (optional for Tx)
     uint32_t        tile;          // segments (packets) per group per block tile (0 = grid-stride)
-    uint32_t        udp_tx_csum;   // Tx: 1 = compute UDP checksums, 0 = transmit none
+    uint32_t        udp_tx_csum;   // Tx UDP checksums: 1 = compute, 0 = transmit none (write 0), 2 = per
+                                   // datagram: a field of 0 is left 0 (no checksum), any other computed
     uint32_t        touch;         // run-stream form: row-touch prologue (set by the launcher)
+    uint8_t*        action_out;    // Rx: NETCSUM_RX_* action per packet (optional; rx_action)
+    uint32_t        rx_cfg;        // Rx: NETCSUM_RXCFG_* bits for the actions
 };
+
+// Tx UDP checksum policy of a datagram whose checksum field holds `field` (PktBatchArgs::udp_tx_csum).
+__host__ __device__ __forceinline__ bool udp_tx_compute(uint32_t mode, uint32_t field) {
+    return mode == 1u || (mode == 2u && field != 0u);
+}
 
 // Two-pass Tx (run-stream form): one record per packet between the checksum pass and the scatter pass,
 // written and read as ONE little-endian uint64 (vals | l4_off << 32 | flags << 48 | store << 56).

@@ -64,7 +64,7 @@ __device__ __forceinline__ void pin_chunks(u32x4 (&v)[K]) {
 
 // The packet's frame starts at the 16-B boundary below it; chunk c of the frame is
 // [q0 + 16c, q0 + 16c + 16).
-template <int G, int K, bool NT, bool NT_TAIL = NT>   // NT_TAIL: policy of the chunks past slot 0
+template <int G, int K, bool NT>
 __device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t avail, int lane) {
     st.a = a;
     st.lead = (uint32_t)(a & 15u);
@@ -76,7 +76,7 @@ __device__ __forceinline__ void pkt_issue(PktStage<K>& st, uintptr_t a, uint32_t
     for (int k = 0; k < K; ++k) {
         const uint32_t c = (uint32_t)(k * G + lane);
         gu32x4* src = reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z);
-        st.v[k] = (k == 0) ? load16<NT>(src) : load16<NT_TAIL>(src);
+        st.v[k] = load16<NT>(src);
     }
 }
 
@@ -157,7 +157,7 @@ __device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
 }
 
 template <int G, bool TX>
-__device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum,
+__device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, uint32_t udp_mode,
                                                 uint32_t d0, uint32_t d1) {   // packet dwords 0 and 1
     PktInfo p{};
     p.l4_csum_off = ~0u;
@@ -227,7 +227,7 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
             p.flags |= F_UDP_NO_CSUM | F_L4_OK;
             return p;
         }
-        if (TX && !udp_tx_csum) {
+        if (TX && !udp_tx_compute(udp_mode, du >> 16)) {
             p.flags |= F_UDP_NO_CSUM;
             return p;
         }
@@ -262,7 +262,7 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
 }
 
 template <bool TX>
-__device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, bool udp_tx_csum,
+__device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t avail, int gbase, uint32_t udp_mode,
                                              uint32_t d0, uint32_t d1) {      // packet dwords 0 and 1
     PktInfo p{};
     p.l4_csum_off = ~0u;
@@ -313,7 +313,7 @@ __device__ __forceinline__ PktInfo pkt_parse(u32x4 v0, uint32_t lead, uint32_t a
             p.flags |= F_UDP_NO_CSUM | F_L4_OK;
             return p;
         }
-        if (TX && !udp_tx_csum) {
+        if (TX && !udp_tx_compute(udp_mode, du >> 16)) {
             p.flags |= F_UDP_NO_CSUM;                            // write 0 (NET_UDP_HDR_CHK_SUM_NONE)
             p.check_l4 = false;
             return p;
@@ -353,15 +353,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t byte_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
 }
 
-// Cache policy of the Tx checksum-field stores (buffer-instruction cpol bits: 1 = sc0, 2 = nt,
-// 16 = sc1). Compile-time knob for store-policy experiments (tools/tx_store_policy.sh); 0 = default.
-#ifndef NETCSUM_TX_STORE_AUX
-#define NETCSUM_TX_STORE_AUX 0
-#endif
-
-template <int AUX = 0>
 __device__ __forceinline__ void store_byte(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xFFu), r, (int)off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xFFu), r, (int)off, 0, 0);
 }
 
 // A packet's stores, deferred: the kernel issues them right AFTER the next stage's loads, so no
@@ -371,7 +364,8 @@ __device__ __forceinline__ void store_byte(__amdgpu_buffer_rsrc_t r, uint32_t v,
 struct PktStore {
     uintptr_t a;       // packet address
     uint32_t  vals;    // Tx: IP checksum | transport checksum << 16 (host order)
-    uint32_t  meta;    // transport field offset | flags << 16 | store IP << 24 | store L4 << 25 | lane stores << 26
+    uint32_t  meta;    // Tx: transport field offset, Rx: action | flags << 16 | store IP << 24 | store L4 << 25 |
+                       // lane stores << 26
     uint32_t  idx;     // packet index (flags)
 };
 
@@ -392,18 +386,18 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ps.a);
         const uint32_t o = (uint32_t)(ps.a - wb);
         if constexpr (TX) {
-#ifdef NETCSUM_TX_DROP_STORES   // experiment builds only: same instructions, every field store out of range
-            const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0u);
-#else
             const __amdgpu_buffer_rsrc_t rp = byte_rsrc(reinterpret_cast<const void*>(wb), 0xFFFFFFFFu);
-#endif
-            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
-            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 8, si ? o + 11u : kOOB);
-            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
-            store_byte<NETCSUM_TX_STORE_AUX>(rp, ps.vals >> 24, sl ? o + l4off + 1u : kOOB);
+            store_byte(rp, ps.vals, si ? o + 10u : kOOB);        // memcpy of the host-order values
+            store_byte(rp, ps.vals >> 8, si ? o + 11u : kOOB);
+            store_byte(rp, ps.vals >> 16, sl ? o + l4off : kOOB);
+            store_byte(rp, ps.vals >> 24, sl ? o + l4off + 1u : kOOB);
         }
         const __amdgpu_buffer_rsrc_t rf = byte_rsrc(A.flags_out, A.flags_out ? A.n : 0u);
         store_byte(rf, f, me ? ps.idx : kOOB);
+        if constexpr (!TX) {
+            const __amdgpu_buffer_rsrc_t ra = byte_rsrc(A.action_out, A.action_out ? A.n : 0u);
+            store_byte(ra, l4off, me ? ps.idx : kOOB);
+        }
     } else {
         if (!me) {
             return;
@@ -416,6 +410,9 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
         }
         if (A.flags_out) {
             A.flags_out[ps.idx] = (uint8_t)f;
+        }
+        if (!TX && A.action_out) {
+            A.action_out[ps.idx] = (uint8_t)l4off;
         }
     }
 }
@@ -440,8 +437,8 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     const uint32_t d0 = pkt_dword(st.v[0], lead, 0u, gbase);
     const uint32_t d1 = pkt_dword(st.v[0], lead, 4u, gbase);
     const bool is6 = (VER == 6) || (VER == 0 && ((d0 >> 4) & 0xFu) == 6u);
-    PktInfo p = is6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u, d0, d1)
-                   : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum != 0u, d0, d1);
+    PktInfo p = is6 ? pkt_parse_v6<G, TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum, d0, d1)
+                   : pkt_parse<TX>(st.v[0], lead, st.avail, gbase, A.udp_tx_csum, d0, d1);
     const uint32_t end = p.check_l4 ? p.l4_end : p.hlen;
     const uint32_t rend = lead + end;
     const uint32_t nch = (rend + 15u) >> 4;
@@ -532,7 +529,8 @@ __device__ __forceinline__ PktStore pkt_consume(const PktStage<K>& st, const Pkt
     PktStore ps;
     ps.a = st.a;
     ps.vals = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
-    ps.meta = (p.l4_csum_off & 0xFFFFu) | ((f & 0xFFu) << 16) | (cip != ~0u ? 1u << 24 : 0u) |
+    const uint32_t low = TX ? (p.l4_csum_off & 0xFFFFu) : rx_action(f, p.proto, is6, A.rx_cfg);
+    ps.meta = low | ((f & 0xFFu) << 16) | (cip != ~0u ? 1u << 24 : 0u) |
               (cl4 != ~0u ? 1u << 25 : 0u) | ((valid && lane == 0) ? 1u << 26 : 0u);
     ps.idx = idx;
     return ps;
@@ -555,10 +553,6 @@ __device__ __forceinline__ void pkt_desc(const PktBatchArgs& A, uint32_t i, uint
 template <int G, int K, bool VARLEN, bool NT, bool TX, int VER>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) pkt_batch_kernel(PktBatchArgs A) {
     static_assert(G >= 8, "header extraction needs the first 6 chunks in slot 0");
-#ifndef NETCSUM_TX_SPLIT_NT      // experiment: Tx reads the header slot plain, the rest non-temporal
-#define NETCSUM_TX_SPLIT_NT 0
-#endif
-    constexpr bool kNtTail = NT || (TX && NETCSUM_TX_SPLIT_NT);
     const int lane = (int)(threadIdx.x & (G - 1));
     const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
     const uint32_t gpb = blockDim.x / G;
@@ -587,13 +581,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
     uint32_t i = first;
     bool v0 = cnt != 0u, v1 = false;
     pkt_desc<VARLEN>(A, i, off, avail);
-    pkt_issue<G, K, NT, kNtTail>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+    pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
     PktStore pend{z, 0u, 0u, 0u};                                // nothing to store yet
     for (uint32_t j = 0u; j < iters; j += 2u) {                  // one scalar exit (see seg_pipe_kernel)
         uint32_t nx = i + step;
         v1 = j + 1u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT, kNtTail>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
+        pkt_issue<G, K, NT>(S1, v1 ? base + off : z, v1 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);                      // previous packet's stores, after the loads
         pin_chunks<K>(S0.v);
         pend = pkt_consume<G, K, NT, TX, VER>(S0, A, i, v0, lane, gbase);
@@ -601,7 +595,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) p
         nx = i + step;
         v0 = j + 2u < cnt;
         pkt_desc<VARLEN>(A, nx, off, avail);
-        pkt_issue<G, K, NT, kNtTail>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
+        pkt_issue<G, K, NT>(S0, v0 ? base + off : z, v0 ? avail : 0u, lane);
         pkt_store<G, TX, !VARLEN>(pend, A);
         pin_chunks<K>(S1.v);
         pend = pkt_consume<G, K, NT, TX, VER>(S1, A, i, v1, lane, gbase);

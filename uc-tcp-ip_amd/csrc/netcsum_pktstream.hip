@@ -136,7 +136,7 @@ __device__ __forceinline__ bool ipv6_ext(uint32_t nh) {
 // 5682; net_tcp.c:7871-7879; net_udp.c:1947-1957; net_icmpv6.c:2910-2948).
 template <bool TX>
 __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
-                                               uint32_t avail, bool odd, bool udp_tx_csum, uint32_t d0, uint32_t d1) {
+                                               uint32_t avail, bool odd, uint32_t udp_mode, uint32_t d0, uint32_t d1) {
     LanePkt p{};
     p.l4_csum_off = ~0u;
     p.v6 = true;
@@ -199,7 +199,7 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
             p.flags = NETCSUM_PKT_UDP_NO_CSUM | NETCSUM_PKT_L4_OK;
             return p;
         }
-        if (TX && !udp_tx_csum) {
+        if (TX && !udp_tx_compute(udp_mode, du >> 16)) {
             p.flags = NETCSUM_PKT_UDP_NO_CSUM;
             return p;
         }
@@ -243,7 +243,7 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
 // IPv4 parse of pkt_parse (netcsum_packets.hip) from the lane's own window; `avail` bytes present.
 template <bool TX>
 __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
-                                              uint32_t avail, bool odd, bool udp_tx_csum) {
+                                              uint32_t avail, bool odd, uint32_t udp_mode) {
     LanePkt p{};
     p.l4_csum_off = ~0u;
     const uint32_t d0 = pkt_dword_fixed<0>(wd, lead);
@@ -304,7 +304,7 @@ __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u3
             p.flags = NETCSUM_PKT_UDP_NO_CSUM | NETCSUM_PKT_L4_OK;
             return p;
         }
-        if (TX && !udp_tx_csum) {
+        if (TX && !udp_tx_compute(udp_mode, fd >> 16)) {
             p.flags = NETCSUM_PKT_UDP_NO_CSUM;                   // write 0 (NET_UDP_HDR_CHK_SUM_NONE)
             return p;
         }
@@ -332,37 +332,26 @@ __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u3
     return p;
 }
 
-#ifndef NETCSUM_TX_FIELD_STORE   // experiment builds: 1 non-temporal field stores, 2 system-scope
-#define NETCSUM_TX_FIELD_STORE 0 // (write-through) field stores, in the one-pass Tx (TUNE_TX_PASSES 1)
-#endif
 __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memcpy of a host-order u16
     __attribute__((address_space(1))) uint8_t* q = (__attribute__((address_space(1))) uint8_t*)p;
-    if constexpr (NETCSUM_TX_FIELD_STORE == 1) {
-        __builtin_nontemporal_store((uint8_t)(v & 0xFFu), &q[0]);
-        __builtin_nontemporal_store((uint8_t)(v >> 8), &q[1]);
-    } else if constexpr (NETCSUM_TX_FIELD_STORE == 2) {
-        __hip_atomic_store(p, (uint8_t)(v & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(p + 1, (uint8_t)(v >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-        q[0] = (uint8_t)(v & 0xFFu);
-        q[1] = (uint8_t)(v >> 8);
-    }
+    q[0] = (uint8_t)(v & 0xFFu);
+    q[1] = (uint8_t)(v >> 8);
 }
 
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
 template <int VER, bool TX>
 __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], const u32x4 (&h)[6], uint32_t lead,
-                                                  uint32_t avail, bool odd, bool udp_tx_csum) {
+                                                  uint32_t avail, bool odd, uint32_t udp_mode) {
     if constexpr (VER == 4) {
-        return lane_parse<TX>(wd, h, lead, avail, odd, udp_tx_csum);
+        return lane_parse<TX>(wd, h, lead, avail, odd, udp_mode);
     } else {
         const uint32_t d0 = pkt_dword_fixed<0>(wd, lead);
         const uint32_t d1 = pkt_dword_fixed<4>(wd, lead);
         if (VER == 6 || ((d0 >> 4) & 0xFu) == 6u) {
-            return lane_parse6<TX>(wd, h, lead, avail, odd, udp_tx_csum, d0, d1);
+            return lane_parse6<TX>(wd, h, lead, avail, odd, udp_mode, d0, d1);
         }
-        return lane_parse<TX>(wd, h, lead, avail, odd, udp_tx_csum);
+        return lane_parse<TX>(wd, h, lead, avail, odd, udp_mode);
     }
 }
 
@@ -413,7 +402,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         wd[4 * c + 3] = h[c].w;
     }
     const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
-    const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, L, odd, A.udp_tx_csum != 0u);
+    const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, L, odd, A.udp_tx_csum);
     // Row touch (off by default here: the header loads above already touch every datagram) issued
     // after the parse, when the window's registers are free (issued before it, its two VGPRs raised
     // the prologue's peak to 73 = 6 waves/SIMD).
@@ -516,33 +505,6 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         }
     }
     const uint32_t idx = s_begin + lane;
-#if defined(NETCSUM_PKTSTREAM_PROBE)
-    // EXPERIMENT builds (tools/pkt_write_probe.sh): 1 = Rx stores nothing, 2 = Rx stores 8 B per
-    // packet (flags_out must hold 8 B per packet), 4 = the Tx record pass stores nothing
-    if (!TX && NETCSUM_PKTSTREAM_PROBE == 1) return;
-    if (!TX && NETCSUM_PKTSTREAM_PROBE == 2) {
-        reinterpret_cast<uint64_t*>(A.flags_out)[idx] = ((uint64_t)tot_v << 32) | f;
-        return;
-    }
-    if (REC && NETCSUM_PKTSTREAM_PROBE == 4) {
-        if (tot_v == 0x12345678u) rec[0].vals = f;            // keeps the work live, never taken
-        return;
-    }
-    // 5 = the Tx record pass stores its 8-B records into flags_out (the probe's 8-B-per-packet
-    // torch buffer) instead of the scratch buffer; 6 = 4-B records (values only) into the scratch
-    // (run with PS_TX_FLAGS=1 so that Tx gets the 8-B-per-packet flags buffer)
-    if (REC && NETCSUM_PKTSTREAM_PROBE == 5) {
-        if (A.flags_out == nullptr) return;
-        reinterpret_cast<uint64_t*>(A.flags_out)[idx] =
-            (uint64_t)((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16)) | ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) |
-            ((uint64_t)(f & 0xFFu) << 48);
-        return;
-    }
-    if (REC && NETCSUM_PKTSTREAM_PROBE == 6) {
-        reinterpret_cast<uint32_t*>(rec)[idx] = (cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16);
-        return;
-    }
-#endif
     if constexpr (REC) {
         // one 8-B store per packet (a struct assignment compiles to four partial stores, which
         // made this pass ~70 us slower on 1 M packets)
@@ -554,6 +516,9 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     }
     if (A.flags_out) {
         A.flags_out[idx] = (uint8_t)f;
+    }
+    if (!TX && A.action_out) {
+        A.action_out[idx] = (uint8_t)rx_action(f, pk.proto, pk.v6, A.rx_cfg);
     }
     if constexpr (TX) {
         uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)idx * A.stride;

@@ -203,13 +203,6 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
             if (u < s_end && e <= pend) {                      // segment `u` ends in this piece
                 const uint32_t Pe = piece_prefix(v, lane16, e - qb);
                 finish(u, wave_total(a + Pe), (((e - L) & 1u) != 0u) != ph_odd);
-#if defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE == 2
-                // EXPERIMENT: the segment's field writes issued as soon as its last byte is read
-                if (lane < 4u) {
-                    uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)u * A.seg_stride;
-                    p[(lane < 2u ? 10u : 34u) + lane] = (uint8_t)Pe;
-                }
-#endif
                 a = full - Pe;                                 // the next segment starts at e
                 ++u;
                 e += st;
@@ -245,44 +238,6 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     };
 
     const uint32_t rounds = (npieces + (uint32_t)D - 1u) / (uint32_t)D;
-#if defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE >= 4
-    // EXPERIMENT (timing only, results are not checksums): 4 = pieces read in REVERSE order, and after
-    // each piece the field bytes (+10/+36) of the segment starting in it are written (a reversed Tx
-    // reads a packet's header last and writes it right away); 5 = the same writes in forward order
-    // right after the header's piece is read; 6 = as 4 with whole aligned 64-B line writes.
-    constexpr bool kRev = NETCSUM_STREAM_WB_PROBE != 5;
-    for (int j = 0; j < D; ++j) {
-        const uint32_t pq = kRev ? (npieces - 1u - (uint32_t)j) : (uint32_t)j;
-        dv[j] = buf_load16<NT>(rd, (((int)pq >= 0 ? pq : 0x200000u) << 10) + lane16);
-    }
-    for (uint32_t r = 0; r < rounds; ++r) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const uint32_t q = r * (uint32_t)D + (uint32_t)j;
-            consume(q, opaque_tuple(dv[j]));
-            const uint32_t pq = kRev ? npieces - 1u - q : q;       // physical piece just consumed
-            if (q < npieces) {
-                const uint32_t lo = pq << 10, hi = lo + 1024u, lead0 = (uint32_t)(a_first - O);
-                const uint32_t k = lo > lead0 ? (lo - lead0 + st - 1u) / st : 0u;
-                if (k < nres && lead0 + k * st < hi) {
-                    uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)(s_begin + k) * A.seg_stride;
-#if NETCSUM_STREAM_WB_PROBE == 6
-                    if (lane < 8u) {
-                        const uintptr_t line = (((uintptr_t)p + ((lane >> 2) ? 36u : 10u)) & ~(uintptr_t)63) + 16u * (lane & 3u);
-                        *reinterpret_cast<u32x4*>(line) = u32x4{acc, 0u, 0u, 0u};
-                    }
-#else
-                    if (lane < 4u) p[(lane < 2u ? 10u : 34u) + lane] = (uint8_t)acc;
-#endif
-                }
-            }
-            const uint32_t nq = q + (uint32_t)D;
-            const uint32_t npq = kRev ? (nq < npieces ? npieces - 1u - nq : 0x200000u) : nq;
-            dv[j] = buf_load16<NT>(rd, (npq << 10) + lane16);
-            asm volatile("" ::: "memory");
-        }
-    }
-#else
     for (uint32_t r = 0; r < rounds; ++r) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -292,31 +247,12 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
             asm volatile("" ::: "memory");                     // keep the refill here, not sunk to the latch
         }
     }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
     if constexpr (PH == 0) {
         touch_retire(touch);
     }
 
     store_run_results(A, s_begin, nres, lane, res0, res1);
-#if defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE == 1
-    // EXPERIMENT (Tx write cost): 2 x 2-byte in-place field writes per segment at +10 / +36,
-    // issued as one burst by the wave after its run's reads
-    if (lane < nres) {
-        uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)(s_begin + lane) * A.seg_stride;
-        p[10] = (uint8_t)res0; p[11] = (uint8_t)(res0 >> 8); p[36] = (uint8_t)res0; p[37] = (uint8_t)(res0 >> 8);
-    }
-#elif defined(NETCSUM_STREAM_WB_PROBE) && NETCSUM_STREAM_WB_PROBE == 3
-    // EXPERIMENT: the same burst as whole aligned 64-B lines (lines holding +10 and +36), 16-B stores
-    {
-        const uint32_t k = lane >> 3, part = lane & 7u;        // 8 lanes per segment: 2 lines x 4 x 16 B
-        for (uint32_t kk = k; kk < nres; kk += 8u) {
-            uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)(s_begin + kk) * A.seg_stride;
-            const uintptr_t line = (((uintptr_t)p + ((part >> 2) ? 36u : 10u)) & ~(uintptr_t)63) + 16u * (part & 3u);
-            *reinterpret_cast<u32x4*>(line) = u32x4{res0, res1, 0u, 0u};
-        }
-    }
-#endif
 }
 
 // Variable-length batches (offset/length descriptors, config C4). A wave takes a run of segments;

@@ -134,7 +134,7 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
                 csum_off = off + 6u;
                 if (!TX && be16(p, off + 6u) == 0u) {
                     f |= W_UDP_NO_CSUM | W_L4_OK;
-                } else if (TX && !A.udp_tx_csum) {
+                } else if (TX && !udp_tx_compute(A.udp_tx_csum, be16(p, off + 6u))) {
                     f |= W_UDP_NO_CSUM;
                     if (lane == 0u) {
                         p[csum_off] = 0u;           // NET_UDP_HDR_CHK_SUM_NONE (net_udp.c:2935)
@@ -180,6 +180,9 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
     }
     if (lane == 0u) {
         A.flags_out[i] = (uint8_t)f;
+        if (!TX && A.action_out) {
+            A.action_out[i] = (uint8_t)rx_action(f, nh, true, A.rx_cfg);
+        }
     }
 }
 

@@ -49,6 +49,12 @@ DEF_OK, DEF_FAIL = 1, 0
 OP_DATA_CALC, OP_DATA_VERIFY, OP_HDR_CALC, OP_HDR_VERIFY = 0, 1, 2, 3
 PKT_IP_OK, PKT_L4_OK, PKT_L4_CHECKED, PKT_UDP_NO_CSUM = 0x01, 0x02, 0x04, 0x08
 PKT_MALFORMED, PKT_FRAGMENT, PKT_L4_MALFORMED = 0x10, 0x20, 0x40
+PKT_EXT_HDR = 0x80
+# Rx burst actions / config (include/netcsum_mi355x.h (2b''): the reference's checksum-offload seam)
+RX_DELIVER, RX_DROP_IPV4_CHK_SUM, RX_DROP_TCP_CHK_SUM, RX_DROP_UDP_CHK_SUM = 0, 1, 2, 3
+RX_DROP_UDP_NO_CHK_SUM, RX_DROP_ICMPV4_CHK_SUM, RX_DROP_IGMP_CHK_SUM, RX_DROP_ICMPV6_CHK_SUM = 4, 5, 6, 7
+RX_DELIVER_L4_UNVERIFIED, RX_NBR_ACTIONS = 8, 9
+RXCFG_UDP_DISCARD_NO_CHK_SUM = 0x1
 TUNE_GRID_BLOCKS, TUNE_GROUP_LANES, TUNE_NT_LOADS, TUNE_BLOCK_THREADS = 1, 2, 3, 4
 TUNE_KERNEL, TUNE_CHUNKS, TUNE_PROBE, TUNE_GRID_MULT, TUNE_TILE = 5, 6, 7, 8, 9
 TUNE_TX_PASSES = 10
@@ -215,6 +221,14 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_RxValidateIP.restype = i32
     L.NetUtil_MI355X_TxFinalizeIP.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, vp]
     L.NetUtil_MI355X_TxFinalizeIP.restype = i32
+    L.NetUtil_MI355X_RxBurst.argtypes = [vp, vp, vp, u64, u16, u32, u32, vp, vp, vp]
+    L.NetUtil_MI355X_RxBurst.restype = i32
+    L.NetUtil_MI355X_TxBurst.argtypes = [vp, vp, vp, u64, u16, u32, vp, vp]
+    L.NetUtil_MI355X_TxBurst.restype = i32
+    L.NetUtil_MI355X_RxAction.argtypes = [ctypes.c_uint8, ctypes.c_uint8, i32, u32]
+    L.NetUtil_MI355X_RxAction.restype = ctypes.c_uint8
+    L.NetUtil_MI355X_RxBurstTally.argtypes = [vp, u32, vp]
+    L.NetUtil_MI355X_RxBurstTally.restype = i32
     L.NetUtil_32BitCRC_Calc.argtypes = [vp, u32, perr]
     L.NetUtil_32BitCRC_Calc.restype = u32
     L.NetUtil_32BitCRC_CalcCpl.argtypes = [vp, u32, perr]
@@ -526,6 +540,43 @@ def tx_finalize_ip(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0
     if check:
         _check(err, "NetUtil_MI355X_TxFinalizeIP")
     return err
+
+
+def rx_burst(base, n, action, flags=None, off=None, lens=None, stride=0, pkt_len=0, rx_cfg=0, stream=None,
+             check=True):
+    """NetUtil_MI355X_RxBurst: per-frame NETCSUM_RX_* actions of a mixed IPv4 / IPv6 burst."""
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    if n:
+        _require(action, n, "actions")
+    err = lib().NetUtil_MI355X_RxBurst(_p(base), _p(off), _p(lens), stride, pkt_len, n, rx_cfg, _p(action),
+                                       _p(flags), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_RxBurst")
+    return err
+
+
+def tx_burst(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, stream=None, check=True):
+    """NetUtil_MI355X_TxBurst: fill in the checksum fields the stack left to the offload, in place."""
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_TxBurst(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags), _stream(stream))
+    if check:
+        _check(err, "NetUtil_MI355X_TxBurst")
+    return err
+
+
+def rx_action(flags, proto, ipv6, rx_cfg=0):
+    """NetUtil_MI355X_RxAction (host logic): the burst action of one verdict."""
+    return int(lib().NetUtil_MI355X_RxAction(flags, proto, int(bool(ipv6)), rx_cfg))
+
+
+def rx_burst_tally(actions):
+    """NetUtil_MI355X_RxBurstTally over a host uint8 array -> list of RX_NBR_ACTIONS counts."""
+    import numpy as np
+    a = np.ascontiguousarray(actions, dtype=np.uint8)
+    ctr = np.zeros(RX_NBR_ACTIONS, np.uint32)
+    _check(lib().NetUtil_MI355X_RxBurstTally(a.ctypes.data if a.size else None, a.size, ctr.ctypes.data),
+           "NetUtil_MI355X_RxBurstTally")
+    return [int(x) for x in ctr]
 
 
 def fill(buf, n_bytes, seed, pattern=0, stream=None, first_byte=0):
