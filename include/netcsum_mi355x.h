@@ -223,16 +223,21 @@ NET_ERR  NetUtil_MI355X_TxFinalizeIPv4     (void            *d_base,
  *   Extension headers: Hop-by-Hop (0, first only), Routing (43) and Destination Options (60) are
  *               skipped, a chain of any length as NetIPv6_RxPktProcessExtHdr walks it
  *               (net_ipv6.c:8396-8510; upper-layer length = payload length - their bytes,
- *               net_ipv6.c:5682): the batch kernel walks what its first loads hold, a second pass
- *               (netcsum_v6walk.hip) the longer chains; a Fragment header (44) gives FRAGMENT; a
- *               header running past the payload gives MALFORMED
- *   EXT_HDR     any other extension header (50, 51, 59, 135, 139, 140, 253, 254) or a late
- *               Hop-by-Hop header: no transport verdict in the batch. For 50 / 51 /
- *               59 / 135 this is also the reference's outcome: it never reaches a transport checksum
- *               (ESP and Mobility: NET_IPv6_ERR_INVALID_EH, net_ipv6.c:8837-8846, :8956-8965; AH: the
- *               next header is read from the IPv6 header's first octet, 0x6X, and rejected as
- *               NET_IPv6_ERR_INVALID_PROTOCOL, :8885-8894, :8357-8360; No Next Header: no upper
- *               layer, :8460-8462)
+ *               net_ipv6.c:5682), each judged as the reference's handler judges it: the options of
+ *               Hop-by-Hop / Destination Options headers are walked and one whose type & 0x1F is not
+ *               Pad1 / PadN / Router Alert with non-"skip" action bits drops the datagram
+ *               (NetIPv6_RxOptHdr, net_ipv6.c:8604-8672); a routing type > 2 with Segments Left != 0
+ *               drops it (NetIPv6_RxRoutingHdr, :8735-8753). The batch kernel walks accepted Routing
+ *               headers its first loads hold; a second pass (netcsum_v6walk.hip, launched work only
+ *               when the batch deferred a datagram) the option headers and longer chains; a Fragment
+ *               header (44) gives FRAGMENT; a header running past the payload gives MALFORMED (the
+ *               reference does not check this, and reads on past the payload)
+ *   EXT_HDR     a datagram the reference drops in its extension-header processing: a dropping option
+ *               or routing header (above), any other extension header (50, 51, 59, 135, 139, 140, 253,
+ *               254) or a late Hop-by-Hop header: no transport verdict. ESP and Mobility:
+ *               NET_IPv6_ERR_INVALID_EH, net_ipv6.c:8837-8846, :8956-8965; AH: the next header is read
+ *               from the IPv6 header's first octet, 0x6X, and rejected as NET_IPv6_ERR_INVALID_PROTOCOL,
+ *               :8885-8894, :8357-8360; No Next Header: no upper layer, :8460-8462
  * TxFinalizeIPv6 writes the TCP / UDP / ICMPv6 checksum in place (net_tcp.c:29839-29862,
  *   net_udp.c:2909-2937, net_icmpv6.c:1439 and :949-965); UDP 0x0000 -> 0xFFFF, udp_tx_csum = 0
  *   writes 0; no header checksum to write.

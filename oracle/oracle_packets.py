@@ -155,14 +155,43 @@ def tx_finalize(pkt: bytes, udp_tx_csum: bool = True):
 # Extension headers (net_ipv6.c:8290-8360, 8396-8510): Hop-by-Hop (0, first only), Routing (43),
 # Destination Options (60), length (HdrExtLen + 1) * 8 (net_ipv6.c:8601), are skipped -- a chain of
 # any length, as NetIPv6_RxPktProcessExtHdr walks it -- and the upper-layer length becomes payload -
-# extension bytes (net_ipv6.c:5682). Fragment (44) -> FRAGMENT; an extension header running past the
-# payload -> MALFORMED; any other extension header or a Hop-by-Hop header after the first -> EXT_HDR.
-# No transport verdict for those.
+# extension bytes (net_ipv6.c:5682). Each is checked as the reference's handler checks it:
+#   Hop-by-Hop / Destination Options (NetIPv6_RxOptHdr, net_ipv6.c:8604-8672): the options are walked
+#     while the offset into them is < length - 2; an option whose type & 0x1F is not Pad1 (0), PadN (1)
+#     or Router Alert (5) and whose action bits (type & 0xC0) are not "skip" drops the datagram
+#     (NET_IPv6_ERR_INVALID_EH_OPT); Pad1 advances 1 octet, every other option Len + 2;
+#   Routing (NetIPv6_RxRoutingHdr, net_ipv6.c:8735-8753): a routing type other than 0, 1, 2 with
+#     Segments Left != 0 drops the datagram (NET_IPv6_ERR_INVALID_EH_OPT_SEQ).
+# A dropped datagram, any other extension header, or a Hop-by-Hop header after the first -> EXT_HDR:
+# the reference never reaches a transport checksum for them. Fragment (44) -> FRAGMENT. An extension
+# header running past the payload -> MALFORMED: the reference has no such check (its
+# NET_IPv6_ERR_INVALID_EH_LEN, net_ipv6.c:8381, is never raised; it reads on past the payload and its
+# DataLen -= eh_len wraps, net_ipv6.c:8602), so the datagram gets no transport verdict here instead of
+# reading past the bytes present.
 # ---------------------------------------------------------------------------------------------
 EXT_HDR = 128
 IPV6_EXT = {0, 43, 44, 50, 51, 59, 60, 135, 139, 140, 253, 254}
 ICMPV6_PSEUDO_TYPES = {128, 129, 130, 131, 134, 135, 136, 137}
 ICMPV6_NOPSEUDO_TYPES = {1, 3, 4}
+
+
+def opt_hdr_accepts(pkt: bytes, off: int, eh_len: int) -> bool:
+    """NetIPv6_RxOptHdr's option walk (net_ipv6.c:8604-8672) over the header at pkt[off:off+eh_len]."""
+    nto = 0
+    while nto < eh_len - 2:
+        t = pkt[off + 2 + nto]
+        opt, act = t & 0x1F, t & 0xC0
+        if opt not in (0, 1, 5) and act != 0:
+            return False                       # DISCARD, DISCARD_IPPM or DISCARD_IPPM_MC
+        # an option starting at the header's last octet reads its Len one past the header; any value
+        # ends the walk there, so it is not needed
+        nto += 1 if opt == 0 else (pkt[off + 3 + nto] if nto + 3 < eh_len else 0) + 2
+    return True
+
+
+def routing_hdr_accepts(pkt: bytes, off: int) -> bool:
+    """NetIPv6_RxRoutingHdr (net_ipv6.c:8735-8753): types 0-2 pass; others need Segments Left 0."""
+    return pkt[off + 2] <= 2 or pkt[off + 3] == 0
 
 
 def _parse6(pkt: bytes):
@@ -179,9 +208,12 @@ def _parse6(pkt: bytes):
             return EXT_HDR, off, 0, nh, pkt[8:40]
         if off + 8 > tot:                      # the header itself would run past the payload
             return None
-        nh, off = pkt[off], off + (pkt[off + 1] + 1) * 8
-        if off > tot:
+        eh_len = (pkt[off + 1] + 1) * 8
+        if off + eh_len > tot:
             return None
+        if not (routing_hdr_accepts(pkt, off) if nh == 43 else opt_hdr_accepts(pkt, off, eh_len)):
+            return EXT_HDR, off, 0, nh, pkt[8:40]
+        nh, off = pkt[off], off + eh_len
     if nh == 44:
         return FRAGMENT, off, 0, nh, pkt[8:40]
     if nh in IPV6_EXT:

@@ -88,17 +88,78 @@ def packed_batch(pkts, rng: random.Random, trailer=True, lead=1):
 
 KINDS6 = ["tcp", "tcp", "udp", "udp", "udp0", "icmp_echo", "icmp_err", "icmp_nd", "icmp_other", "ext",
           "other", "bad_ver", "bad_plen", "udp_badlen", "tcp_short", "corrupt_l4", "ext_ok", "ext_ok",
-          "ext_frag", "ext_long", "ext_bad", "ext_hbh_late"]
+          "ext_frag", "ext_long", "ext_bad", "ext_hbh_late", "ext_opt_drop", "ext_rt_drop"]
 EXT_OPAQUE = [50, 51, 59, 135, 139, 140, 253, 254]       # extension headers the batch does not walk
 
 
-def _ext_chain(rng: random.Random, kinds, final_nh: int) -> tuple[int, bytes]:
-    """Extension headers of the given types (units of 8 B each) ending in final_nh -> (first nh, bytes)."""
+def _options(rng: random.Random, n: int) -> bytes:
+    """n octets of Hop-by-Hop / Destination Options that NetIPv6_RxOptHdr accepts (net_ipv6.c:8604-
+    8672): Pad1 and PadN, Router Alert, unknown options with the "skip" action, option types whose
+    low 5 bits are 0 / 1 / 5 under any action bits, and a last option whose Len runs past the header
+    (the walk just ends there)."""
+    out = b""
+    while len(out) < n:
+        r = n - len(out)
+        c = rng.random()
+        if r == 1 or c < 0.15:
+            out += bytes([rng.choice([0x00, 0x20, 0x40, 0x80, 0xC0])])                 # Pad1 (any action bits)
+        elif c < 0.4:
+            k = rng.randint(0, min(r - 2, 255))
+            out += bytes([rng.choice([0x01, 0x21, 0xC1]), k]) + bytes(k)             # PadN
+        elif c < 0.55 and r >= 4:
+            out += bytes([rng.choice([0x05, 0x85]), 2]) + rng.randbytes(2)          # Router Alert
+        elif c < 0.9 or r > 256:
+            k = rng.randint(0, min(r - 2, 255))
+            t = rng.choice([x for x in range(2, 32) if x != 5]) | rng.choice([0x00, 0x20])
+            out += bytes([t, k]) + rng.randbytes(k)                                 # unknown, skip
+        else:
+            out += bytes([0x01, rng.randint(r - 1, 255)]) + rng.randbytes(r - 2)    # Len past the end
+    return out[:n]
+
+
+def _ext_chain(rng: random.Random, kinds, final_nh: int, reject: int | None = None) -> tuple[int, bytes]:
+    """Extension headers of the given types (units of 8 B each) ending in final_nh -> (first nh, bytes).
+    Option headers carry options the reference accepts and Routing headers a type / Segments Left it
+    accepts (net_ipv6.c:8735-8753), except header number `reject`, which carries what it drops: an
+    unknown option with a discard action, or a routing type > 2 with Segments Left != 0."""
     out, nh = b"", final_nh
-    for t, units in reversed(kinds):
-        out = struct.pack("!BB", nh, units - 1) + rng.randbytes(units * 8 - 2) + out
+    for j in reversed(range(len(kinds))):
+        t, units = kinds[j]
+        n = units * 8 - 2
+        if t == 43:
+            rt = rng.choice([0, 1, 2]) if rng.random() < 0.6 else rng.randint(3, 255)
+            sl = rng.randint(0, 255) if rt <= 2 else 0
+            if reject == j:
+                rt, sl = rng.randint(3, 255), rng.randint(1, 255)
+            body = bytes([rt, sl]) + rng.randbytes(n - 2)
+        elif t in (0, 60):
+            body = _options(rng, n)
+            if reject == j:
+                k = rng.randint(0, n - 2)                                          # reachable: valid options before
+                pre = _options(rng, k) if k else b""
+                while pre and (len(pre) < k or _ends_walk(pre)):
+                    pre = _options(rng, k)
+                bad = rng.choice([x for x in range(2, 32) if x != 5]) | rng.choice([0x40, 0x80, 0xC0])
+                body = pre + bytes([bad]) + rng.randbytes(n - k - 1)
+        else:
+            body = rng.randbytes(n)
+        out = struct.pack("!BB", nh, units - 1) + body + out
         nh = t
     return nh, out
+
+
+def _ends_walk(opts: bytes) -> bool:
+    """Does the option walk over `opts` (as a prefix of a longer area) end before its last octet?"""
+    i = 0
+    while i < len(opts):
+        t = opts[i]
+        if t & 0x1F == 0:
+            i += 1
+        elif i + 1 < len(opts):
+            i += opts[i + 1] + 2
+        else:
+            return True
+    return i != len(opts)
 
 
 def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) -> bytes:
@@ -143,6 +204,12 @@ def make_packet_v6(rng: random.Random, kind: str, payload: int | None = None) ->
             nh, ext = _ext_chain(rng, [(60, rng.randint(129, 200))], inner_nh)
         elif kind == "ext_hbh_late":
             nh, ext = _ext_chain(rng, [(60, 1), (0, 1)], inner_nh)
+        elif kind == "ext_opt_drop":                           # an option the reference discards on
+            chain = [(rng.choice([0, 60]), rng.choice([1, 1, 2, 3]))] + [(60, 1)] * rng.randint(0, 1)
+            nh, ext = _ext_chain(rng, chain, inner_nh, reject=rng.randrange(len(chain)))
+        elif kind == "ext_rt_drop":                            # routing type > 2, Segments Left != 0
+            chain = [(60, 1)] * rng.randint(0, 1) + [(43, rng.choice([1, 2, 3]))]
+            nh, ext = _ext_chain(rng, chain, inner_nh, reject=len(chain) - 1)
         else:                                                  # ext_bad: length past the payload
             nh, ext = _ext_chain(rng, [(43, 1)], inner_nh)
             ext = ext[:1] + bytes([rng.randint(20, 255)]) + ext[2:]

@@ -182,3 +182,45 @@ def test_chains_of_any_length_and_their_outcomes():
     b = bytearray(struct.pack("!IHBB32s", 6 << 28, len(ext) + 20, nh, 64, bytes(32)) + ext + bytes(20))
     b[40 + 800 + 1] = 200                                             # the Routing header runs past the payload
     assert op.rx_validate_v6(bytes(b)) == op.MALFORMED
+
+
+def test_option_and_routing_header_rules():
+    """Hand-made headers against NetIPv6_RxOptHdr (net_ipv6.c:8604-8672) and NetIPv6_RxRoutingHdr
+    (:8735-8753): an option is judged by type & 0x1F (Pad1 0, PadN 1, Router Alert 5 pass under any
+    action bits) and otherwise by its action bits (0x00 skip passes; 0x40 / 0x80 / 0xC0 drop); the walk
+    only sees options it reaches; a routing type > 2 drops iff Segments Left != 0. A dropped datagram
+    gets EXT_HDR (no transport verdict), its neighbours' verdicts are unchanged."""
+    inner = make_packet_v6(random.Random(70), "tcp", payload=40)
+
+    def dgram(nh, ext):
+        body = ext + inner[40:]
+        return op.tx_finalize_v6(inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40] + body)[0]
+
+    ok = op.IP_OK | op.L4_CHECKED | op.L4_OK
+    rej = op.IP_OK | op.EXT_HDR
+    opts = [  # (6 option octets of an 8-B header, accepted?)
+        (bytes([0, 0, 0, 0, 0, 0]), True),                       # Pad1 x 6
+        (bytes([1, 4, 0, 0, 0, 0]), True),                       # PadN
+        (bytes([5, 2, 0, 0, 1, 4, 0, 0][:6]), True),             # Router Alert, PadN cut by the end
+        (bytes([0x3E, 4, 9, 9, 9, 9]), True),                    # unknown, skip (+ change bit)
+        (bytes([0x1E, 0, 0x01, 2, 0, 0]), True),
+        (bytes([0x7E, 4, 9, 9, 9, 9]), False),                   # unknown, discard
+        (bytes([0xBE, 4, 9, 9, 9, 9]), False),                   # discard + ICMP
+        (bytes([0xFE, 4, 9, 9, 9, 9]), False),                   # discard + ICMP unless multicast
+        (bytes([0, 0, 0, 0, 0, 0xDE]), False),                   # reached at the last octet
+        (bytes([0x40, 0x80, 0xC0, 0x20, 0, 0]), True),           # opt 0 under any action: Pad1
+        (bytes([0xC5, 2, 1, 1, 0xC1, 0]), True),                 # Router Alert / PadN with action bits
+        (bytes([1, 4, 0xDE, 0, 0, 0]), True),                    # the discard option is PadN's data
+        (bytes([0x01, 200, 0xDE, 0, 0, 0]), True),               # a Len past the header ends the walk
+    ]
+    for first in (0, 60):
+        for o, accepted in opts:
+            nh, ext = first, bytes([6, 0]) + o
+            assert op.rx_validate_v6(dgram(nh, ext)) == (ok if accepted else rej), (first, o.hex())
+            # second in a chain behind an accepted Destination Options header
+            nh2, ext2 = 60, bytes([first if first == 60 else 60, 0]) + bytes(6) + ext
+            assert op.rx_validate_v6(dgram(nh2, ext2)) == (ok if accepted else rej), (first, o.hex())
+    for rt, sl, accepted in ((0, 7, True), (1, 1, True), (2, 255, True), (3, 0, True), (3, 1, False),
+                             (4, 2, False), (255, 255, False), (200, 0, True)):
+        ext = bytes([6, 0, rt, sl]) + bytes(4)
+        assert op.rx_validate_v6(dgram(43, ext)) == (ok if accepted else rej), (rt, sl)

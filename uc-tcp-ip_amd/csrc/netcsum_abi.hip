@@ -303,6 +303,7 @@ struct ScratchSlot {
     hipEvent_t         ev = nullptr;  // recorded after the last launches that used p
     bool               ev_live = false;
     bool               pinned = false;  // used under stream capture: never freed while the thread runs
+    uint32_t           seq = 0;         // last tag handed out (ScratchLease::next_tag)
 };
 
 hipError_t slot_wait(ScratchSlot& sl) {                // all launches that used sl.p have finished
@@ -392,6 +393,12 @@ public:
         return hipSuccess;
     }
     void* ptr() const { return slot_ ? slot_->p : nullptr; }
+    // A tag no earlier call on this slot used (a deferral word holding it was written by this call;
+    // after 2^32 calls a stale word may match once, which only repeats an idempotent pass).
+    uint32_t next_tag() {
+        if (++slot_->seq == 0u) slot_->seq = 1u;
+        return slot_->seq;
+    }
     hipError_t end() {
         ScratchSlot* sl = slot_;
         slot_ = nullptr;
@@ -853,14 +860,23 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
                  tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
                  walk ? " +pkt_v6_walk_kernel" : "");
         netcsum::set_last_launch(desc);
-        ScratchLease scratch;                             // records (two-pass Tx) and / or flags
+        // scratch: [deferral word (IPv6 / mixed), 256 B | records (two-pass Tx) | flags (own_flags)]
+        ScratchLease scratch;
+        const size_t word_bytes = walk ? 256u : 0u;
         const size_t rec_bytes = two ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
-        if (two || own_flags) {
-            NC_HIP(scratch.acquire(dev, hs, rec_bytes + (own_flags ? n_pkt : 0u)));
-            if (own_flags) a.flags_out = static_cast<uint8_t*>(scratch.ptr()) + rec_bytes;
+        if (walk || two) {
+            NC_HIP(scratch.acquire(dev, hs, word_bytes + rec_bytes + (own_flags ? n_pkt : 0u)));
+            uint8_t* sp = static_cast<uint8_t*>(scratch.ptr());
+            if (walk) {
+                a.defer_word = reinterpret_cast<uint32_t*>(sp);
+                a.defer_tag = scratch.next_tag();
+            }
+            if (own_flags) a.flags_out = sp + word_bytes + rec_bytes;
         }
         NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs,
-                                          two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
+                                          two ? reinterpret_cast<netcsum::PktTxRecord*>(
+                                                    static_cast<uint8_t*>(scratch.ptr()) + word_bytes)
+                                              : nullptr));
         if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
@@ -870,10 +886,12 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u%s", c.group_lanes,
              c.chunks_per_pass, c.nt ? ",nt" : "", tx ? "tx" : "rx", ip_ver, a.tile, walk ? " +pkt_v6_walk_kernel" : "");
     netcsum::set_last_launch(desc);
-    ScratchLease scratch;
-    if (own_flags) {
-        NC_HIP(scratch.acquire(dev, hs, n_pkt));
-        a.flags_out = static_cast<uint8_t*>(scratch.ptr());
+    ScratchLease scratch;                                 // [deferral word, 256 B | flags (own_flags)]
+    if (walk) {
+        NC_HIP(scratch.acquire(dev, hs, 256u + (own_flags ? n_pkt : 0u)));
+        a.defer_word = static_cast<uint32_t*>(scratch.ptr());
+        a.defer_tag = scratch.next_tag();
+        if (own_flags) a.flags_out = static_cast<uint8_t*>(scratch.ptr()) + 256u;
     }
     NC_HIP(netcsum::launch_pkt_batch(a, c, tx, ip_ver, hs));
     if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));

@@ -61,6 +61,8 @@ struct PktBatchArgs {
     uint32_t        touch;         // run-stream form: row-touch prologue (set by the launcher)
     uint8_t*        action_out;    // Rx: NETCSUM_RX_* action per packet (optional; rx_action)
     uint32_t        rx_cfg;        // Rx: NETCSUM_RXCFG_* bits for the actions
+    uint32_t*       defer_word;    // IPv6 / mixed: set to defer_tag by a batch kernel that leaves a
+    uint32_t        defer_tag;     // datagram EXT_HDR; the walk pass runs only when it holds the tag
 };
 
 // Tx UDP checksum policy of a datagram whose checksum field holds `field` (PktBatchArgs::udp_tx_csum).

@@ -140,17 +140,18 @@ __device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 
 //                Tx: every message through the pseudo-header (DataCalc + pseudo, net_icmpv6.c:1439;
 //                    the error messages' ~HdrCalc(pseudo) field trick, net_icmpv6.c:949-965, gives
 //                    the same value), no 0 -> 0xFFFF substitution
-// Extension headers (net_ipv6.c:8290-8360, RxPktProcessExtHdr): Hop-by-Hop (0, first only),
-// Routing (43) and Destination Options (60) — length (HdrExtLen + 1) * 8, net_ipv6.c:8601 — are
-// skipped, up to 4 of them, while the chain and the transport fields stay inside the bytes the
-// group's first chunks hold (16 * G from the frame start); the transport part then starts after
-// them and the pseudo-header length is the payload length minus their bytes (IP_DatagramLen =
-// IP_TotLen - IPv6_ExtHdrLen, net_ipv6.c:5682). A Fragment header (44) means FRAGMENT: the
-// transport checksum covers the reassembled datagram. Any other extension header (AH, ESP,
-// Mobility, No Next Header, experimental values) or a Hop-by-Hop header after the first gets EXT_HDR
-// and no transport verdict; so does a chain past that window, which the walk pass
-// (netcsum_v6walk.hip) then finishes; an extension header running past the payload is MALFORMED
-// (INVALID_EH_LEN).
+// Extension headers (net_ipv6.c:8290-8360, RxPktProcessExtHdr): Routing headers (43) the reference
+// accepts (type <= 2 or Segments Left 0, net_ipv6.c:8735-8753) — length (HdrExtLen + 1) * 8,
+// net_ipv6.c:8601 — are skipped, up to 4 of them, while the chain and the transport fields stay
+// inside the bytes the group's first chunks hold (16 * G from the frame start); the transport part
+// then starts after them and the pseudo-header length is the payload length minus their bytes
+// (IP_DatagramLen = IP_TotLen - IPv6_ExtHdrLen, net_ipv6.c:5682). A Fragment header (44) means
+// FRAGMENT: the transport checksum covers the reassembled datagram. Hop-by-Hop / Destination Options
+// headers (whose options must be walked, net_ipv6.c:8604-8672), any other routing header, a chain
+// past that window, and every other extension header (AH, ESP, Mobility, No Next Header,
+// experimental values) get EXT_HDR here; the walk pass (netcsum_v6walk.hip) then judges each of
+// those datagrams by the reference's rules; an extension header running past the payload is
+// MALFORMED.
 __device__ __forceinline__ bool ipv6_ext_hdr(uint32_t nh) {
     return nh == 0u || nh == 43u || nh == 44u || nh == 50u || nh == 51u || nh == 59u || nh == 60u ||
            nh == 135u || nh == 139u || nh == 140u || nh == 253u || nh == 254u;
@@ -176,12 +177,18 @@ __device__ __forceinline__ PktInfo pkt_parse_v6(u32x4 v0, uint32_t lead, uint32_
     // window: transport fields up to off + 24 and the dword reads below stay in the k = 0 chunks
     constexpr uint32_t kWin = 16u * (uint32_t)G;
     uint32_t off = 40u;
-    for (int e = 0; e < 4 && (p.proto == 0u || p.proto == 43u || p.proto == 60u); ++e) {
-        if ((p.proto == 0u && off != 40u) || lead + off + 8u > kWin) {
+    // accepted Routing headers walked here; option headers and rejected-looking Routing headers go
+    // to the walk pass (netcsum_v6walk.hip), which applies NetIPv6_RxOptHdr / RxRoutingHdr's rules
+    for (int e = 0; e < 4 && p.proto == 43u; ++e) {
+        if (lead + off + 8u > kWin) {
             p.flags |= F_EXT_HDR;
             return p;
         }
         const uint32_t d = pkt_dword(v0, lead, off, gbase);
+        if (((d >> 16) & 0xFFu) > 2u && (d >> 24) != 0u) {
+            p.flags |= F_EXT_HDR;
+            return p;
+        }
         off += (((d >> 8) & 0xFFu) + 1u) * 8u;
         p.proto = d & 0xFFu;
         if (off > tot) {
@@ -376,6 +383,9 @@ template <int G, bool TX, bool BS>
 __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs& A) {
     const uint32_t f = (ps.meta >> 16) & 0xFFu;
     const bool me = (ps.meta >> 26) & 1u;
+    if (me && (f & F_EXT_HDR) && A.defer_word != nullptr) {
+        *A.defer_word = A.defer_tag;                             // the walk pass has work (benign race)
+    }
     const bool si = TX && ((ps.meta >> 24) & 1u), sl = TX && ((ps.meta >> 25) & 1u);
     const uint32_t l4off = ps.meta & 0xFFFFu;
     if constexpr (BS) {

@@ -149,12 +149,19 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
     }
     const uint32_t window = 96u - lead;                          // bytes of the datagram in the window
     uint32_t off = 40u;
-    for (int e = 0; e < 4 && (nh == 0u || nh == 43u || nh == 60u); ++e) {
-        if ((nh == 0u && off != 40u) || off + 8u > window) {
+    // Routing headers the reference accepts (type <= 2 or Segments Left 0, net_ipv6.c:8735-8753) are
+    // walked here; Hop-by-Hop / Destination Options headers (whose options NetIPv6_RxOptHdr walks,
+    // net_ipv6.c:8604-8672) and any other routing header go to the walk pass (EXT_HDR), which judges them.
+    for (int e = 0; e < 4 && nh == 43u; ++e) {
+        if (off + 8u > window) {
             p.flags = NETCSUM_PKT_EXT_HDR;
             return p;
         }
         const uint32_t d = pkt_dword_at(wd, lead, off);
+        if (((d >> 16) & 0xFFu) > 2u && (d >> 24) != 0u) {
+            p.flags = NETCSUM_PKT_EXT_HDR;
+            return p;
+        }
         off += (((d >> 8) & 0xFFu) + 1u) * 8u;
         nh = d & 0xFFu;
         if (off > tot) {                                         // extension header past the payload
@@ -505,6 +512,9 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         }
     }
     const uint32_t idx = s_begin + lane;
+    if (A.defer_word != nullptr && (f & NETCSUM_PKT_EXT_HDR)) {
+        *A.defer_word = A.defer_tag;                             // the walk pass has work (benign race)
+    }
     if constexpr (REC) {
         // one 8-B store per packet (a struct assignment compiles to four partial stores, which
         // made this pass ~70 us slower on 1 M packets)

@@ -13,16 +13,19 @@
 //   16 lanes reading half-words in parallel, and the verdict (Rx) or the checksum field (Tx) and the
 //   flag are written by the group's lane 0 (vector stores).
 //
-// Datagrams are rare on this path (chains of more than 4 headers or longer than ~50 bytes), so the
-// pass costs one launch that reads the n flag bytes (1 MB for 1 M datagrams) when no datagram needs
-// it. The verdict rules are pkt_parse_v6's (netcsum_packets.hip; the same reference lines):
+// Datagrams are rare on this path (option headers, chains of more than 4 routing headers or longer
+// than ~50 bytes), and the pass is launched only when the batch kernels deferred one (their
+// deferral word, launch_pkt_v6_walk). The verdict rules are pkt_parse_v6's (netcsum_packets.hip; the same reference lines):
 //   TCP (6)     DataVerify / DataCalc + pseudo {src, dst, ulen, 0, 6}        net_tcp.c:7871-7879, 29839-29862
 //   UDP (17)    length check, field 0 = no checksum (Rx), 0 -> 0xFFFF (Tx)   net_udp.c:1903-1957, 2909-2937
 //   ICMPv6 (58) Rx types 1, 3, 4 without the pseudo-header, 128-131 / 134-137 with it, others no verdict;
 //               Tx every type with it                                         net_icmpv6.c:2910-2948, 1439
 // with ulen = payload length - extension-header bytes (net_ipv6.c:5682); Fragment (44) -> FRAGMENT,
-// another extension header or a late Hop-by-Hop -> EXT_HDR (no transport verdict, the reference
-// rejects those, net_ipv6.c:8307-8309, 8465-8476), a header running past the payload -> MALFORMED.
+// another extension header, a late Hop-by-Hop, an option with a discard action or a routing type > 2
+// with Segments Left != 0 -> EXT_HDR (no transport verdict: the reference drops those,
+// net_ipv6.c:8307-8309, 8465-8476, 8630-8671, 8735-8753), a header running past the payload ->
+// MALFORMED. The batch kernels leave every datagram with a Hop-by-Hop or Destination Options header
+// to this pass (its options must be walked).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,6 +46,30 @@ __device__ __forceinline__ bool ext_hdr_value(uint32_t nh) {   // net_ipv6.h NET
 
 __device__ __forceinline__ uint32_t be16(const uint8_t* p, uint32_t k) {
     return ((uint32_t)p[k] << 8) | (uint32_t)p[k + 1u];
+}
+
+// NetIPv6_RxOptHdr's option walk (net_ipv6.c:8604-8672) over a Hop-by-Hop / Destination Options
+// header h of eh_len octets: an option whose type & 0x1F is not Pad1 (0), PadN (1) or Router Alert
+// (5) and whose action bits (type & 0xC0) are not "skip" (0x00) drops the datagram
+// (NET_IPv6_ERR_INVALID_EH_OPT); Pad1 advances one octet, every other option Len + 2. An option that
+// starts at the header's last octet would have its Len read one past the header, but any value ends
+// the walk there, so that octet is not read. Group-uniform byte loads (one cached line per 64 B).
+__device__ __forceinline__ bool options_accept(const uint8_t* h, uint32_t eh_len) {
+    for (uint32_t nto = 0u; nto + 2u < eh_len;) {
+        const uint32_t t = h[2u + nto];
+        const uint32_t opt = t & 0x1Fu;
+        if (opt != 0u && opt != 1u && opt != 5u && (t & 0xC0u) != 0u) {
+            return false;
+        }
+        nto += (opt == 0u) ? 1u : ((nto + 3u < eh_len ? (uint32_t)h[3u + nto] : 0u) + 2u);
+    }
+    return true;
+}
+
+// NetIPv6_RxRoutingHdr (net_ipv6.c:8735-8753): routing types 0, 1, 2 pass; any other type drops the
+// datagram (NET_IPv6_ERR_INVALID_EH_OPT_SEQ) unless Segments Left is 0.
+__device__ __forceinline__ bool routing_accepts(const uint8_t* h) {
+    return h[2] <= 2u || h[3] == 0u;
 }
 
 // A datagram is finished by a group of kLanes lanes (a wave takes 4 datagrams at a time).
@@ -103,13 +130,17 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
             f = W_MALFORMED;                        // the header would run past the payload
             break;
         }
-        const uint32_t nx = p[off];
-        off += ((uint32_t)p[off + 1u] + 1u) * 8u;
-        nh = nx;
-        if (off > tot) {
-            f = W_MALFORMED;                        // NET_IPv6_ERR_INVALID_EH_LEN
+        const uint32_t eh_len = ((uint32_t)p[off + 1u] + 1u) * 8u;
+        if (off + eh_len > tot) {
+            f = W_MALFORMED;                        // (the reference reads on past the payload)
             break;
         }
+        if (!(nh == 43u ? routing_accepts(p + off) : options_accept(p + off, eh_len))) {
+            f = W_IP_OK | W_EXT_HDR;                // the reference drops the datagram here
+            break;
+        }
+        nh = p[off];
+        off += eh_len;
     }
     uint32_t csum_off = ~0u;
     bool pseudo = false, check = false;
@@ -193,6 +224,9 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
 // chain loads overlap).
 template <bool TX>
 __global__ void __launch_bounds__(256) pkt_v6_walk_kernel(PktBatchArgs A) {
+    if (A.defer_word != nullptr && *A.defer_word != A.defer_tag) {
+        return;                                     // no batch kernel deferred a datagram this call
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t grp = lane / kLanes;
     for (uint64_t w0 = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); w0 < A.n; w0 += (uint64_t)gridDim.x * 256u) {
