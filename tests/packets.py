@@ -117,6 +117,17 @@ def _options(rng: random.Random, n: int) -> bytes:
     return out[:n]
 
 
+def ext_body(rng: random.Random, t: int, n: int) -> bytes:
+    """The n octets after NextHdr / HdrExtLen of an extension header of type t that the reference
+    accepts (random octets for other types)."""
+    if t == 43:
+        rt = rng.choice([0, 1, 2]) if rng.random() < 0.6 else rng.randint(3, 255)
+        return bytes([rt, rng.randint(0, 255) if rt <= 2 else 0]) + rng.randbytes(n - 2)
+    if t in (0, 60):
+        return _options(rng, n)
+    return rng.randbytes(n)
+
+
 def _ext_chain(rng: random.Random, kinds, final_nh: int, reject: int | None = None) -> tuple[int, bytes]:
     """Extension headers of the given types (units of 8 B each) ending in final_nh -> (first nh, bytes).
     Option headers carry options the reference accepts and Routing headers a type / Segments Left it
@@ -126,14 +137,10 @@ def _ext_chain(rng: random.Random, kinds, final_nh: int, reject: int | None = No
     for j in reversed(range(len(kinds))):
         t, units = kinds[j]
         n = units * 8 - 2
-        if t == 43:
-            rt = rng.choice([0, 1, 2]) if rng.random() < 0.6 else rng.randint(3, 255)
-            sl = rng.randint(0, 255) if rt <= 2 else 0
-            if reject == j:
-                rt, sl = rng.randint(3, 255), rng.randint(1, 255)
-            body = bytes([rt, sl]) + rng.randbytes(n - 2)
+        body = ext_body(rng, t, n)
+        if t == 43 and reject == j:
+            body = bytes([rng.randint(3, 255), rng.randint(1, 255)]) + body[2:]
         elif t in (0, 60):
-            body = _options(rng, n)
             if reject == j:
                 k = rng.randint(0, n - 2)                                          # reachable: valid options before
                 pre = _options(rng, k) if k else b""
@@ -141,8 +148,6 @@ def _ext_chain(rng: random.Random, kinds, final_nh: int, reject: int | None = No
                     pre = _options(rng, k)
                 bad = rng.choice([x for x in range(2, 32) if x != 5]) | rng.choice([0x40, 0x80, 0xC0])
                 body = pre + bytes([bad]) + rng.randbytes(n - k - 1)
-        else:
-            body = rng.randbytes(n)
         out = struct.pack("!BB", nh, units - 1) + body + out
         nh = t
     return nh, out

@@ -10,7 +10,7 @@ import pytest
 
 import netcsum
 import oracle_packets as op
-from packets import KINDS6, make_packet_v6, packed_batch
+from packets import KINDS6, ext_body, make_packet_v6, packed_batch
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -174,8 +174,9 @@ def _long_chain_pkts(rng, max_units, n_hdrs=(1,), reps=3):
                 nh, ext = inner[6], b""
                 for _k in range(h):
                     u = rng.randint(1, units)
-                    ext = struct.pack("!BB", nh, u - 1) + rng.randbytes(u * 8 - 2) + ext
-                    nh = rng.choice([43, 60])
+                    t = rng.choice([43, 60])
+                    ext = struct.pack("!BB", nh, u - 1) + ext_body(rng, t, u * 8 - 2) + ext
+                    nh = t
                 body = ext + inner[40:]
                 hdr = inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40]
                 pkts.append(op.tx_finalize_v6(hdr + body)[0])

@@ -14,7 +14,7 @@ import pytest
 
 import netcsum
 import oracle_packets as op
-from packets import KINDS, make_packet
+from packets import KINDS, ext_body, make_packet
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -271,8 +271,9 @@ def test_pkt_stream_v6_extension_chains_of_any_length(lead):
             nh, ext = inner[6], b""
             for _k in range(n_hdr):
                 u = units if n_hdr == 1 else rng.randint(1, 3)
-                ext = struct.pack("!BB", nh, u - 1) + rng.randbytes(u * 8 - 2) + ext
-                nh = rng.choice([43, 60])
+                t = rng.choice([43, 60])
+                ext = struct.pack("!BB", nh, u - 1) + ext_body(rng, t, u * 8 - 2) + ext
+                nh = t
             body = ext + inner[40:]
             hdr = inner[:4] + struct.pack("!HB", len(body), nh) + inner[7:40]
             pkts.append(op.tx_finalize_v6(hdr + body)[0][:pkt_len])
