@@ -81,8 +81,12 @@ CPU_INT32U   NetUtil_16BitSumDataCalcAlign_32    (void        *pdata_32,
  * reverses the 32 bits (net_util.c:610-636; the drivers' multicast hash, e.g.
  * Dev/Ether/GMAC/net_dev_gmac.c:2673-2683). With NETCSUM_ARG_CHK_EXT_EN (default 1, the template's
  * NET_ERR_CFG_ARG_CHK_EXT_EN = DEF_ENABLED, net_cfg.h:178): p_data NULL -> 0 and
- * NET_ERR_FAULT_NULL_PTR, data_len 0 -> 0 and NET_UTIL_ERR_NULL_SIZE. The CRC is computed on the
- * GPU (NetUtil_MI355X_CRC32Host); Reflect is a bit permutation of one register, done in host C.
+ * NET_ERR_FAULT_NULL_PTR, data_len 0 -> 0 and NET_UTIL_ERR_NULL_SIZE. A call of up to 4096 octets
+ * (the stack's only use: 6-octet multicast MAC hashes) runs the reference's register update in host
+ * C — a GPU round trip would cost ~1000 x the CPU loop; a longer buffer goes to the GPU kernel
+ * (NetUtil_MI355X_CRC32Host). Reflect is a bit permutation of one register, done in host C. A stack
+ * may equally keep its own net_util.c CRC functions: throughput CRCs are the batch
+ * entry points below.
  *  NetUtil_32BitCRC_Calc     replaces Source/net_util.c:485  (decl net_util.h:442)
  *  NetUtil_32BitCRC_CalcCpl  replaces Source/net_util.c:571  (decl net_util.h:446)
  *  NetUtil_32BitReflect      replaces Source/net_util.c:610  (decl net_util.h:450) */
@@ -435,8 +439,10 @@ NET_ERR  NetUtil_MI355X_ShardVarLen        (const uint16_t *seg_len,
 /* CRC-32 batches (device memory): d_out[i] = NetUtil_32BitCRC_Calc (cpl = 0) or _CalcCpl (cpl != 0)
  * of segment i — base + i * stride, `len` bytes (strided) or base + d_off[i], d_len[i] bytes
  * (varlen) — any alignment and length; an empty segment gives 0 (the reference's NULL_SIZE case).
- * Segments up to 256 B (strided) take one lane each with slicing-by-4 tables in LDS; longer ones a
- * 16-lane group whose lanes CRC equal blocks and merge them by GF(2) shifts (netcsum_crc.hip). */
+ * Strided segments up to 96 B take one lane each (crc_tiny_kernel up to 16 B, else crc_lane_kernel,
+ * byte tables in LDS); longer ones and every varlen batch the interleaved form crc_ilv_kernel: 8 lanes
+ * per segment for strided segments >= 1 KiB, else 4, over interleaved 16-B chunks with 11-bit slicing
+ * tables in LDS (netcsum_crc.hip). NETCSUM_TUNE_CRC_KERNEL 1 selects the 16-lane block-combine form. */
 NET_ERR  NetUtil_MI355X_CRC32BatchStrided  (const void *d_base,
                                             uint64_t    stride,
                                             uint32_t    len,

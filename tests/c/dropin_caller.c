@@ -245,7 +245,8 @@ static void check_errors(void)
 }
 
 /* CRC-32 drop-ins (net_util.c:485-636): the EXT argument checks answered on the host, the
- * complement relation, the CRC-32 check value through the device, and the bit reflection. */
+ * complement relation, the CRC-32 check value and MAC hashes on the host (calls of up to 4096
+ * octets), a 5000-octet buffer through the device, and the bit reflection. */
 static uint32_t crc_bitwise(const uint8_t *p, uint32_t n)
 {
     uint32_t c = 0xFFFFFFFFu, i, j;
@@ -268,9 +269,17 @@ static void check_crc(void)
     CHECK(NetUtil_32BitCRC_CalcCpl(mac, 0, &err) == 0u && (unsigned)err == NET_UTIL_ERR_NULL_SIZE,
           "CRC(len 0) -> %u (net_util.c:504-508)", (unsigned)err);
     v = NetUtil_32BitCRC_CalcCpl(kat, 9, &err);
-    if (dev_result(err, "CRC32 CalcCpl")) CHECK(v == 0xCBF43926u, "CRC-32 check value %08x", (unsigned)v);
+    CHECK((unsigned)err == NET_UTIL_ERR_NONE && v == 0xCBF43926u, "CRC-32 check value %08x", (unsigned)v);
     v = NetUtil_32BitCRC_Calc(mac, 6, &err);
-    if (dev_result(err, "CRC32 Calc")) CHECK(v == crc_bitwise(mac, 6), "CRC of a MAC %08x", (unsigned)v);
+    CHECK((unsigned)err == NET_UTIL_ERR_NONE && v == crc_bitwise(mac, 6), "CRC of a MAC %08x (host)", (unsigned)v);
+    {
+        static uint8_t big[5000];
+        for (i = 0; i < sizeof big; ++i) big[i] = (uint8_t)(i * 131u + 7u);
+        v = NetUtil_32BitCRC_Calc(big, 4096, &err);
+        CHECK((unsigned)err == NET_UTIL_ERR_NONE && v == crc_bitwise(big, 4096), "CRC of 4096 B %08x", (unsigned)v);
+        v = NetUtil_32BitCRC_Calc(big, sizeof big, &err);
+        if (dev_result(err, "CRC32 Calc 5000 B")) CHECK(v == crc_bitwise(big, sizeof big), "CRC of 5000 B %08x", (unsigned)v);
+    }
     for (i = 0; i < 32; ++i) {
         r = NetUtil_32BitReflect(1u << i);
         CHECK(r == (1u << (31u - i)), "Reflect(bit %u) = %08x", i, r);

@@ -46,3 +46,20 @@ def test_crc_batch_rejects_null_before_device_work():
     assert L.NetUtil_MI355X_CRC32BatchStrided(None, 6, 6, 0, None, 0, None) == netcsum.NET_UTIL_ERR_NONE   # n = 0
     assert L.NetUtil_MI355X_CRC32BatchStrided(None, 6, 6, 4, 16, 0, None) == netcsum.NET_ERR_FAULT_NULL_PTR
     assert L.NetUtil_MI355X_CRC32BatchVarLen(8, None, 8, 4, 16, 0, None) == netcsum.NET_ERR_FAULT_NULL_PTR
+
+
+def test_dropin_short_crc_runs_on_the_host():
+    """Per-call CRCs of up to 4096 octets (the drivers' 6-octet multicast hashes) are the reference's
+    register update in host C, no device round trip: they work without a GPU and equal the oracle,
+    at every length 1..300 and at 4096; Reflect of them gives the drivers' 6-bit hash."""
+    import random
+    rng = random.Random(8)
+    for n in list(range(1, 301)) + [1500, 4096]:
+        m = rng.randbytes(n)
+        buf = (ctypes.c_uint8 * n).from_buffer_copy(m)
+        for cpl in (False, True):
+            assert netcsum.CRC32Calc(ctypes.addressof(buf), n, cpl) == oracle.crc32_calc(m, cpl), (n, cpl)
+    mac = (ctypes.c_uint8 * 6).from_buffer_copy(bytes([0x01, 0x00, 0x5E, 0x7F, 0x00, 0x01]))
+    crc, err = netcsum.CRC32Calc(ctypes.addressof(mac), 6, True)
+    assert err == netcsum.NET_UTIL_ERR_NONE
+    assert netcsum.Reflect32(crc) >> 26 == oracle.reflect32(oracle.crc32_calc(bytes(mac), True)[0]) >> 26

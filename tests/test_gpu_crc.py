@@ -1,5 +1,5 @@
 """GPU parity of the CRC-32 path (net_util.c:485-636): the drop-in NetUtil_32BitCRC_Calc / _CalcCpl
-on host buffers, the drivers' multicast hash built on them, and the strided / varlen batch kernels
+on host buffers (GPU past 4096 octets), the drivers' multicast hash built on them, and the strided / varlen batch kernels
 (one lane per short segment; for long ones 16-lane groups over interleaved 16-B chunks with table-driven
 shifts, the default, or over equal blocks combined by GF(2) multiplications, NETCSUM_TUNE_CRC_KERNEL 1),
 against the C restatement (pinned to the CRC-32 check value and zlib in tests/test_crc_cpu.py).
@@ -27,8 +27,10 @@ def _host(data: bytes):
 
 @pytest.mark.parametrize("cpl", [False, True])
 def test_dropin_crc_vs_oracle(cpl):
+    """Calls of up to 4096 octets run the reference's register update on the host (the per-call MAC
+    hash), longer ones go through the GPU kernel (NetUtil_MI355X_CRC32Host): both equal the oracle."""
     rng = random.Random(11 + cpl)
-    for n in list(range(1, 80)) + [255, 256, 257, 1023, 1500, 4096, 9000, 65535, 65536, 200003]:
+    for n in list(range(1, 80)) + [255, 256, 257, 1023, 1500, 4095, 4096, 4097, 9000, 65535, 65536, 200003]:
         m = rng.randbytes(n)
         keep, p = _host(m)
         for off in [o for o in ((0, 1, 3) if n < 300 else (0, 5)) if o < n]:
@@ -54,9 +56,10 @@ def test_dropin_multicast_hash_like_the_drivers():
 # (NETCSUM_TUNE_CRC_KERNEL, _NT, _LANES, _WIDE): auto, block combine, interleaved for every length (nt),
 # one lane per segment for every length, interleaved with 1 .. 16 lanes per segment; byte (0), 11-bit (1) or
 # lane-replicated 6-bit (2) tables
-FORMS = [(0, 0, 0, 1), (1, 0, 0, 1), (2, 1, 0, 1), (3, 0, 0, 1), (2, 0, 1, 1), (2, 0, 2, 1), (2, 0, 4, 1),
-         (2, 0, 8, 1), (2, 0, 16, 1), (2, 0, 4, 0), (2, 1, 16, 0), (2, 0, 1, 2), (2, 0, 4, 2), (2, 0, 8, 2),
-         (2, 1, 16, 2)]
+# The matrix guards the shipped forms (auto: tiny / lane / interleaved with 11-bit tables) and one
+# variant per alternative kernel a TUNE key selects; round 2's sweeps of every lane count and table
+# form are recorded in DESIGN.md and not re-run here.
+FORMS = [(0, 0, 0, 1), (1, 0, 0, 1), (2, 1, 0, 1), (3, 0, 0, 1), (2, 0, 16, 0), (2, 0, 1, 2)]
 
 
 def expected_kernel(form, length, varlen=False):
@@ -85,9 +88,8 @@ def crc_form(request):
     netcsum.tune(netcsum.TUNE_CRC_WIDE, 1)
 
 
-STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (96, 96), (97, 100), (128, 128), (129, 130), (255, 256), (256, 256), (257, 300),
-           (1500, 1500), (1514, 1518), (4096, 4100), (9000, 9001), (2048, 2048), (2049, 2050), (4111, 4111),
-           (65535, 65536)]
+STRIDED = [(6, 6), (6, 8), (1, 1), (16, 16), (17, 20), (96, 96), (97, 100), (257, 300), (1500, 1500), (1514, 1518),
+           (9000, 9001), (65535, 65536)]
 
 
 @pytest.mark.parametrize("length,stride", STRIDED)
@@ -95,7 +97,7 @@ STRIDED = [(6, 6), (6, 8), (1, 1), (3, 7), (20, 20), (63, 64), (64, 64), (96, 96
 def test_crc_batch_strided_vs_oracle(length, stride, cpl, crc_form):
     rng = np.random.default_rng(length * 3 + stride + cpl)
     n = 1000 if length <= 1514 else 200 if length <= 9001 else 24
-    for base_off in (0, 1, 2, 7, 13, 15):
+    for base_off in (0, 1, 13):
         data = rng.integers(0, 256, size=base_off + n * stride + 64, dtype=np.uint8)
         d = torch.from_numpy(data).to(DEV)
         out = torch.zeros(n, dtype=torch.int32, device=DEV)

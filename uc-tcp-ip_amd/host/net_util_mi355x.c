@@ -278,9 +278,45 @@ CPU_INT32U NetUtil_16BitSumDataCalcAlign_32(void *pdata_32, CPU_INT32U size)
 }
 
 /* ------------------------------------------------------------------------------------------
- * CRC-32 (net_util.c:485-636). The register is computed on the GPU; the host keeps the argument
- * checks of NET_ERR_CFG_ARG_CHK_EXT_EN and the final complement.
+ * CRC-32 (net_util.c:485-636). SURVEY §2 row 10 keeps the CRC a host function: the stack calls it
+ * per 6-octet MAC address (the drivers' multicast hash, e.g. Dev/Ether/GMAC/net_dev_gmac.c:2673-2683),
+ * where a GPU round trip (~9 us) would cost ~1000 x the reference's loop. So a call of up to
+ * NETCSUM_CRC_HOST_MAX octets runs the reference's register update (net_util.c:515-529: per octet,
+ * eight shift / conditional-xor steps of the reflected polynomial) one table lookup per octet here;
+ * a longer buffer is sent to the GPU kernel (NetUtil_MI355X_CRC32Host). Batches of CRCs use
+ * NetUtil_MI355X_CRC32Batch* directly. The argument checks of NET_ERR_CFG_ARG_CHK_EXT_EN and the
+ * final complement are the reference's.
  * ---------------------------------------------------------------------------------------- */
+#define NETCSUM_CRC_HOST_MAX  4096u
+
+/* T[v] = the eight steps of net_util.c:518-525 applied to the octet value v. */
+static uint32_t crc_step_table(uint32_t v)
+{
+    uint32_t j;
+    for (j = 0u; j < 8u; ++j) {
+        v = (v & 1u) ? ((v >> 1) ^ 0xEDB88320u) : (v >> 1);   /* NET_UTIL_32_BIT_CRC_POLY_REFLECT */
+    }
+    return v;
+}
+
+static uint32_t crc_host(const CPU_INT08U *p, uint32_t n)
+{
+    static uint32_t tab[256];
+    static volatile int ready = 0;
+    uint32_t crc = 0xFFFFFFFFu, i;                          /* NET_UTIL_32_BIT_ONES_CPL_NEG_ZERO */
+    if (!ready) {                                           /* idempotent: racing threads write equal values */
+        for (i = 0u; i < 256u; ++i) {
+            tab[i] = crc_step_table(i);
+        }
+        __atomic_store_n(&ready, 1, __ATOMIC_RELEASE);
+    }
+    (void)__atomic_load_n(&ready, __ATOMIC_ACQUIRE);
+    for (i = 0u; i < n; ++i) {
+        crc = (crc >> 8) ^ tab[(crc ^ p[i]) & 0xFFu];       /* :518, :527 */
+    }
+    return crc;
+}
+
 /* Replaces Source/net_util.c:485-530. */
 CPU_INT32U NetUtil_32BitCRC_Calc(CPU_INT08U *p_data, CPU_INT32U data_len, NET_ERR *p_err)
 {
@@ -296,6 +332,10 @@ CPU_INT32U NetUtil_32BitCRC_Calc(CPU_INT08U *p_data, CPU_INT32U data_len, NET_ER
         return 0u;
     }
 #endif
+    if (data_len <= NETCSUM_CRC_HOST_MAX) {
+        *p_err = NET_UTIL_ERR_NONE;
+        return (CPU_INT32U)crc_host(p_data, (uint32_t)data_len);   /* 0 octets: 0xFFFFFFFF (:518-528) */
+    }
     err = NetUtil_MI355X_CRC32Host(p_data, data_len, &crc);
     if (err != NET_UTIL_ERR_NONE) {
         *p_err = err;
