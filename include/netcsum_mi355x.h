@@ -378,6 +378,67 @@ NET_ERR  NetUtil_MI355X_RxBurstTally       (const uint8_t   *h_action,
                                             uint32_t        *ctr);
 
 /* ============================================================================================
+ * (2e) Host-memory forms (the path starts in NIC Rx buffers, IF/net_if.c:6593,
+ * and socket Tx buffers, Source/net_sock.c:5531). Same arguments and results as the device forms
+ * above with every pointer in HOST memory; the call splits the batch into n_chunks chunks (0 = 1)
+ * and pipelines, on three streams of the calling thread's context, H2D of each chunk's byte span
+ * [min offset, max end) (plus its descriptors) -> the device form -> D2H of the results (Tx: of the
+ * span itself, written back in place, so the call owns those bytes while it runs; an offset/length
+ * Tx batch whose chunk spans overlap runs as one chunk). Host buffers should be pinned
+ * (hipHostMalloc / hipHostRegister) for the copies to overlap. Returns when every result is in
+ * host memory. IP = mixed IPv4 / IPv6 (per datagram by the version nibble).
+ * ============================================================================================ */
+NET_ERR  NetUtil_MI355X_ChkSumBatchVarLenHost(const void      *h_base,
+                                              const uint64_t  *h_seg_off,
+                                              const uint16_t  *h_seg_len,
+                                              const void      *h_pseudo,
+                                              uint32_t         pseudo_stride,
+                                              CPU_INT16U       pseudo_len,
+                                              uint32_t         n_seg,
+                                              void            *h_out,
+                                              NETCSUM_OP       op,
+                                              uint32_t         n_chunks);
+
+NET_ERR  NetUtil_MI355X_RxValidateIPHost   (const void      *h_base,
+                                            const uint64_t  *h_off,
+                                            const uint16_t  *h_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *h_flags,
+                                            uint32_t         n_chunks);
+
+NET_ERR  NetUtil_MI355X_TxFinalizeIPHost   (void            *h_base,
+                                            const uint64_t  *h_off,
+                                            const uint16_t  *h_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *h_flags,
+                                            int              udp_tx_csum,
+                                            uint32_t         n_chunks);
+
+NET_ERR  NetUtil_MI355X_RxBurstHost        (const void      *h_base,
+                                            const uint64_t  *h_off,
+                                            const uint16_t  *h_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint32_t         rx_cfg,
+                                            uint8_t         *h_action,
+                                            uint8_t         *h_flags,
+                                            uint32_t         n_chunks);
+
+NET_ERR  NetUtil_MI355X_TxBurstHost        (void            *h_base,
+                                            const uint64_t  *h_off,
+                                            const uint16_t  *h_len,
+                                            uint64_t         stride,
+                                            CPU_INT16U       pkt_len,
+                                            uint32_t         n_pkt,
+                                            uint8_t         *h_flags,
+                                            uint32_t         n_chunks);
+
+/* ============================================================================================
  * (2c) Batched NET_BUF chains. Chain i = its pseudo-header
  * (d_pseudo + i*pseudo_stride, pseudo_len bytes; none if pseudo_len = 0) followed by pieces
  * [d_chain_first[i], d_chain_first[i+1]) in order, piece j = d_base + d_piece_off[j] with

@@ -164,3 +164,21 @@ def test_binding_rejects_undersized_buffers_before_launch():
         netcsum.batch_strided(seg, 100, 100, ph, 12, 12, 10, out, 0, stream=0)      # 120 B pseudo > 100
     with pytest.raises(ValueError):
         netcsum.batch_varlen(seg, np.zeros(9, np.uint64), np.zeros(10, np.uint16), None, 0, 0, 10, out, 0, stream=0)
+
+
+def test_host_memory_forms_check_arguments_before_device_work():
+    """(2e) host-memory forms: empty batches succeed, NULL pointers and bad configurations are
+    rejected before any device work (so on this CPU-only host too)."""
+    L = netcsum.lib()
+    E_NULL, E_ARG, OK = netcsum.NET_ERR_FAULT_NULL_PTR, netcsum.NET_UTIL_ERR_MI355X_INVALID_ARG, netcsum.NET_UTIL_ERR_NONE
+    assert L.NetUtil_MI355X_ChkSumBatchVarLenHost(None, None, None, None, 0, 0, 0, None, 0, 4) == OK
+    assert L.NetUtil_MI355X_ChkSumBatchVarLenHost(None, None, None, None, 0, 0, 5, None, 0, 4) == E_NULL
+    assert L.NetUtil_MI355X_ChkSumBatchVarLenHost(8, 8, 8, None, 0, 0, 5, 8, 7, 4) == E_ARG       # op
+    assert L.NetUtil_MI355X_RxValidateIPHost(8, None, None, 64, 64, 0, None, 4) == OK
+    assert L.NetUtil_MI355X_RxValidateIPHost(8, None, None, 64, 64, 3, None, 4) == E_NULL        # flags
+    assert L.NetUtil_MI355X_RxValidateIPHost(None, None, None, 64, 64, 3, 8, 4) == E_NULL
+    assert L.NetUtil_MI355X_RxValidateIPHost(8, 8, None, 64, 64, 3, 8, 4) == E_NULL              # off w/o len
+    assert L.NetUtil_MI355X_TxFinalizeIPHost(None, None, None, 64, 64, 3, None, 1, 4) == E_NULL
+    assert L.NetUtil_MI355X_RxBurstHost(8, None, None, 64, 64, 3, 0, None, None, 4) == E_NULL    # actions
+    assert L.NetUtil_MI355X_RxBurstHost(8, None, None, 64, 64, 3, 4, 8, None, 4) == E_ARG        # rx_cfg
+    assert L.NetUtil_MI355X_TxBurstHost(None, None, None, 64, 64, 3, None, 4) == E_NULL

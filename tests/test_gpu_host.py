@@ -1,0 +1,131 @@
+"""GPU parity of the host-memory forms (include/netcsum_mi355x.h (2e)): every
+pointer in host memory, the batch pipelined in chunks over three streams (H2D of each chunk's byte
+span and rebased descriptors -> the device form -> D2H of the results; Tx writes the span back).
+Results equal the oracle's for 1, 2, 3, 7 and 64 chunks, packed and unsorted offset/length batches,
+strided batches, odd base offsets; an overlapping Tx batch (chunk spans that overlap) is still exact."""
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle
+import oracle_offload as oo
+import oracle_packets as op
+from packets import KINDS, KINDS6, make_packet, make_packet_v6, packed_batch
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _pinned(a):
+    t = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+    return t
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 7, 64])
+@pytest.mark.parametrize("op_", [netcsum.OP_DATA_CALC, netcsum.OP_DATA_VERIFY])
+def test_varlen_host_vs_oracle(chunks, op_):
+    rng = np.random.default_rng(chunks * 3 + op_)
+    n = 3000
+    lens = rng.integers(40, 9001, size=n).astype(np.uint16)
+    lens[::101] = rng.integers(0, 40, size=len(lens[::101]))
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    off += 5
+    data = rng.integers(0, 256, size=int(off[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+    ph = rng.integers(0, 256, size=n * 12, dtype=np.uint8)
+    want = oracle.batch_varlen(data, off, lens, ph, 12, 12, op_)
+    hb, ho, hl, hp = _pinned(data), _pinned(off.view(np.int64)), _pinned(lens.view(np.int16)), _pinned(ph)
+    out = torch.zeros(n * (2 if op_ == netcsum.OP_DATA_CALC else 1), dtype=torch.uint8).pin_memory()
+    netcsum.batch_varlen_host(hb, ho, hl, hp, 12, 12, n, out, op_, n_chunks=chunks)
+    got = out.numpy().view(np.uint16) if op_ == netcsum.OP_DATA_CALC else out.numpy()
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+
+
+def test_varlen_host_unsorted_and_pageable():
+    """Reversed and interleaved offsets (chunk spans overlap: each chunk copies its own span) from
+    pageable numpy memory, no pseudo-header, HdrCalc."""
+    rng = np.random.default_rng(2)
+    n = 1200
+    lens = rng.integers(1, 1600, size=n).astype(np.uint16)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    perm = rng.permutation(n)
+    off, lens = off[perm].copy(), lens[perm].copy()
+    data = rng.integers(0, 256, size=int((off + lens).max()) + 64, dtype=np.uint8)
+    out = np.zeros(n, np.uint16)
+    netcsum.batch_varlen_host(data, off, lens, None, 0, 0, n, out, netcsum.OP_HDR_CALC, n_chunks=5)
+    assert np.array_equal(out, oracle.batch_varlen(data, off, lens, None, 0, 0, netcsum.OP_HDR_CALC))
+
+
+def _mixed(rng, n, max_payload):
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.5:
+            out.append(make_packet(rng, rng.choice(KINDS), payload=rng.randint(0, max_payload)))
+        else:
+            out.append(make_packet_v6(rng, rng.choice(KINDS6), payload=rng.randint(0, max_payload)))
+    return out
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 7])
+def test_rx_and_burst_host_varlen(chunks):
+    rng = random.Random(30 + chunks)
+    pkts = _mixed(rng, 1500, 1400)
+    buf, offs, lens = packed_batch(pkts, rng)
+    frames = [bytes(buf[o:o + n]) for o, n in zip(offs.tolist(), lens.tolist())]
+    want_f = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
+    want_a = np.array([netcsum.rx_action(int(x), oo.transport_proto(f), len(f) and f[0] >> 4 == 6)
+                       for x, f in zip(want_f, frames)], np.uint8)
+    hb = _pinned(buf)
+    fl = np.zeros(len(pkts), np.uint8)
+    netcsum.rx_validate_ip_host(hb, len(pkts), fl, off=offs, lens=lens, n_chunks=chunks)
+    assert np.array_equal(fl, want_f)
+    act = np.full(len(pkts), 0xEE, np.uint8)
+    fl2 = np.zeros(len(pkts), np.uint8)
+    netcsum.rx_burst_host(hb, len(pkts), act, flags=fl2, off=offs, lens=lens, n_chunks=chunks)
+    assert np.array_equal(act, want_a) and np.array_equal(fl2, want_f)
+    assert np.array_equal(hb.numpy(), buf)                       # Rx never writes the frames
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 64])
+def test_tx_host_strided(chunks):
+    rng = random.Random(40 + chunks)
+    n, stride = 2000, 1536
+    pkts = _mixed(rng, n, 1300)
+    buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
+    for i, p in enumerate(pkts):
+        p = p[:stride]
+        buf[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
+    want = buf.copy()
+    want_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        q, want_f[i] = op.tx_finalize_ip(bytes(buf[i * stride:(i + 1) * stride]), True)
+        want[i * stride:(i + 1) * stride] = np.frombuffer(q, np.uint8)
+    hb = _pinned(buf)
+    fl = np.zeros(n, np.uint8)
+    netcsum.tx_finalize_ip_host(hb, n, fl, stride=stride, pkt_len=stride, n_chunks=chunks)
+    assert np.array_equal(hb.numpy(), want) and np.array_equal(fl, want_f)
+
+
+def test_tx_burst_host_varlen_and_overlap():
+    rng = random.Random(50)
+    pairs = []
+    for i in range(1200):
+        pkt = (make_packet if i % 2 else make_packet_v6)(rng, rng.choice(["tcp", "udp", "udp"]),
+                                                         payload=rng.randint(0, 1200))
+        csum = rng.random() < 0.8
+        pairs.append((oo.tx_stack_offload(pkt, csum), op.tx_finalize_ip(pkt, csum)[0]))
+    buf, offs, lens = packed_batch([f for f, _ in pairs], rng, trailer=False)
+    want = buf.copy()
+    for (_, r), o in zip(pairs, offs.tolist()):
+        want[o:o + len(r)] = np.frombuffer(r, np.uint8)
+    hb = _pinned(buf)
+    netcsum.tx_burst_host(hb, len(pairs), off=offs, lens=lens, n_chunks=6)
+    assert np.array_equal(hb.numpy(), want)
+    # the same frames listed evens first, then odds: the chunks' spans overlap -> one chunk, same bytes
+    perm = np.concatenate([np.arange(0, len(pairs), 2), np.arange(1, len(pairs), 2)])
+    hb2 = _pinned(buf)
+    netcsum.tx_burst_host(hb2, len(pairs), off=offs[perm].copy(), lens=lens[perm].copy(), n_chunks=6)
+    assert np.array_equal(hb2.numpy(), want)

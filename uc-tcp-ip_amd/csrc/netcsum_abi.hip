@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "../../include/netcsum_mi355x.h"
 #include "netcsum_device.h"
@@ -458,11 +459,13 @@ struct HostCtx {
     hipStream_t          pstream[3] = {nullptr, nullptr, nullptr};
     uint8_t*             d_pipe[3] = {nullptr, nullptr, nullptr};
     size_t               pipe_cap = 0;
+    uint8_t*             h_pipe[3] = {nullptr, nullptr, nullptr};   // pinned descriptor staging per slot
+    size_t               hpipe_cap = 0;
 
     bool empty() const {
         if (stream || h_stage || d_stage || d_sum || h_sum) return false;
         for (int j = 0; j < 3; ++j) {
-            if (pstream[j] || d_pipe[j]) return false;
+            if (pstream[j] || d_pipe[j] || h_pipe[j]) return false;
         }
         return true;
     }
@@ -487,6 +490,7 @@ struct HostCtx {
         for (int j = 0; j < 3; ++j) {
             if (pstream[j]) (void)hipStreamDestroy(pstream[j]);
             if (d_pipe[j]) (void)hipFree(d_pipe[j]);
+            if (h_pipe[j]) (void)hipHostFree(h_pipe[j]);
         }
         if (have_cur && cur != dev && cur >= 0) (void)hipSetDevice(cur);
         *this = HostCtx{};
@@ -531,6 +535,74 @@ NET_ERR ensure_stage(HostCtx& c, size_t bytes) {
     NC_HIP(hipMalloc(&c.d_stage, cap));
     c.cap = cap;
     return NET_UTIL_ERR_NONE;
+}
+
+// The three pipeline slots of a host-memory batch: streams, device buffers of >= dev_bytes and pinned
+// descriptor staging of >= host_bytes (grown on demand; the previous call has drained them).
+NET_ERR ensure_pipe(HostCtx& c, size_t dev_bytes, size_t host_bytes) {
+    for (int j = 0; j < 3; ++j) {
+        if (!c.pstream[j]) NC_HIP(hipStreamCreateWithFlags(&c.pstream[j], hipStreamNonBlocking));
+    }
+    if (dev_bytes > c.pipe_cap) {
+        for (int j = 0; j < 3; ++j) {
+            if (c.d_pipe[j]) { (void)hipFree(c.d_pipe[j]); c.d_pipe[j] = nullptr; }
+        }
+        c.pipe_cap = 0;
+        for (int j = 0; j < 3; ++j) NC_HIP(hipMalloc(&c.d_pipe[j], dev_bytes));
+        c.pipe_cap = dev_bytes;
+    }
+    if (host_bytes > c.hpipe_cap) {
+        for (int j = 0; j < 3; ++j) {
+            if (c.h_pipe[j]) { (void)hipHostFree(c.h_pipe[j]); c.h_pipe[j] = nullptr; }
+        }
+        c.hpipe_cap = 0;
+        for (int j = 0; j < 3; ++j) NC_HIP(hipHostMalloc(&c.h_pipe[j], host_bytes, 0));
+        c.hpipe_cap = host_bytes;
+    }
+    return NET_UTIL_ERR_NONE;
+}
+
+size_t al256(size_t x) { return (x + 255u) & ~(size_t)255u; }
+
+// One chunk of a host-memory batch: items [s0, s0 + ns) whose bytes are [lo, hi) of the caller's buffer.
+struct HostChunk {
+    uint32_t s0, ns;
+    uint64_t lo, hi;
+};
+
+// Chunks of about n / n_chunks items each; items of a strided batch (h_off == NULL) are
+// [i * stride, i * stride + len), of an offset/length batch [h_off[i], h_off[i] + h_len[i]).
+// Returns the largest chunk's byte span; *disjoint = no two chunks' spans overlap.
+uint64_t plan_chunks(const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, uint32_t len, uint32_t n,
+                     uint32_t n_chunks, std::vector<HostChunk>& out, bool* disjoint) {
+    if (n_chunks == 0) n_chunks = 1;
+    if (n_chunks > n) n_chunks = n;
+    const uint32_t per = (n + n_chunks - 1u) / n_chunks;
+    uint64_t maxb = 0;
+    out.clear();
+    for (uint32_t s0 = 0; s0 < n; s0 += per) {
+        HostChunk k{s0, std::min(per, n - s0), 0, 0};
+        if (h_off == nullptr) {
+            k.lo = (uint64_t)s0 * stride;
+            k.hi = (uint64_t)(s0 + k.ns - 1u) * stride + len;
+        } else {
+            k.lo = ~0ull;
+            for (uint32_t i = s0; i < s0 + k.ns; ++i) {
+                k.lo = std::min<uint64_t>(k.lo, h_off[i]);
+                k.hi = std::max<uint64_t>(k.hi, h_off[i] + h_len[i]);
+            }
+            if (k.hi < k.lo) k.hi = k.lo;
+        }
+        maxb = std::max<uint64_t>(maxb, k.hi - k.lo);
+        out.push_back(k);
+    }
+    std::vector<HostChunk> by_lo(out);
+    std::sort(by_lo.begin(), by_lo.end(), [](const HostChunk& a, const HostChunk& b) { return a.lo < b.lo; });
+    *disjoint = true;
+    for (size_t k = 1; k < by_lo.size(); ++k) {
+        if (by_lo[k].lo < by_lo[k - 1].hi && by_lo[k].hi > by_lo[k].lo) *disjoint = false;
+    }
+    return maxb;
 }
 
 }  // namespace
@@ -989,6 +1061,168 @@ uint8_t NetUtil_MI355X_RxAction(uint8_t flags, uint8_t proto, int ipv6, uint32_t
 NET_ERR NetUtil_MI355X_TxBurst(void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                                CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, void* hip_stream) {
     return pkt_batch(d_base, d_off, d_len, stride, pkt_len, n_pkt, d_flags, 2u, true, 0, hip_stream);
+}
+
+// ----------------------------------------------------------- host-memory batches (PCIe-inclusive)
+// The path starts and ends in host memory (NIC Rx buffers, IF/net_if.c:6593; socket Tx buffers,
+// Source/net_sock.c:5531). Each entry point below is its device form run over chunks on the three
+// pipeline streams of the calling thread's context: chunk k's bytes [lo, hi) go H2D (with its
+// descriptors rebased to lo, staged in pinned memory), the device form runs on the copy, its results
+// come D2H — and for Tx the chunk's bytes themselves, written back over [lo, hi) of the caller's
+// buffer — while chunks k +- 1 copy and compute on the other streams. Slot k mod 3 is reused after its
+// stream has drained it. Host buffers should be pinned (hipHostMalloc / hipHostRegister) for the
+// copies to overlap; the call returns when every output is in host memory.
+
+NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t* h_seg_off, const uint16_t* h_seg_len,
+                                             const void* h_pseudo, uint32_t pseudo_stride, CPU_INT16U pseudo_len,
+                                             uint32_t n_seg, void* h_out, NETCSUM_OP op, uint32_t n_chunks) {
+    NET_ERR e = check_op(op, h_pseudo, pseudo_len);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (n_seg == 0) return NET_UTIL_ERR_NONE;
+    if (n_seg > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (h_out == nullptr || h_base == nullptr || h_seg_off == nullptr || h_seg_len == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    HostCtx* cp = nullptr;
+    e = host_ctx(&cp);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    HostCtx& c = *cp;
+    const bool verify = (op == NETCSUM_OP_DATA_VERIFY || op == NETCSUM_OP_HDR_VERIFY);
+    const size_t elt = verify ? 1u : 2u;
+    const bool has_ph = h_pseudo != nullptr && pseudo_len != 0;
+    std::vector<HostChunk> ch;
+    bool disjoint = true;
+    const uint64_t maxb = plan_chunks(h_seg_off, h_seg_len, 0, 0, n_seg, n_chunks, ch, &disjoint);
+    const uint32_t per = ch[0].ns;
+    const size_t ph_bytes = has_ph ? (size_t)(per - 1u) * pseudo_stride + pseudo_len : 0u;
+    // device slot: [bytes | offsets | lengths | pseudo-headers | outputs]; host slot: [offsets | lengths]
+    const size_t o_off = al256(maxb), o_len = o_off + al256((size_t)per * 8u), o_ph = o_len + al256((size_t)per * 2u);
+    const size_t o_out = o_ph + al256(ph_bytes), dev_need = o_out + al256((size_t)per * elt);
+    e = ensure_pipe(c, dev_need, al256((size_t)per * 8u) + (size_t)per * 2u);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    int dev = 0;
+    NC_HIP(hipGetDevice(&dev));
+    for (size_t k = 0; k < ch.size(); ++k) {
+        const HostChunk& q = ch[k];
+        const int j = (int)(k % 3u);
+        hipStream_t st = c.pstream[j];
+        if (k >= 3) NC_HIP(hipStreamSynchronize(st));       // slot j's staging is free again
+        uint8_t* d = c.d_pipe[j];
+        uint64_t* h_o = reinterpret_cast<uint64_t*>(c.h_pipe[j]);
+        uint16_t* h_l = reinterpret_cast<uint16_t*>(c.h_pipe[j] + al256((size_t)per * 8u));
+        for (uint32_t i = 0; i < q.ns; ++i) {
+            h_o[i] = h_seg_off[q.s0 + i] - q.lo;
+            h_l[i] = h_seg_len[q.s0 + i];
+        }
+        NC_HIP(hipMemcpyAsync(d, static_cast<const uint8_t*>(h_base) + q.lo, q.hi - q.lo, hipMemcpyHostToDevice, st));
+        NC_HIP(hipMemcpyAsync(d + o_off, h_o, (size_t)q.ns * 8u, hipMemcpyHostToDevice, st));
+        NC_HIP(hipMemcpyAsync(d + o_len, h_l, (size_t)q.ns * 2u, hipMemcpyHostToDevice, st));
+        if (has_ph) {
+            NC_HIP(hipMemcpyAsync(d + o_ph, static_cast<const uint8_t*>(h_pseudo) + (size_t)q.s0 * pseudo_stride,
+                                  (size_t)(q.ns - 1u) * pseudo_stride + pseudo_len, hipMemcpyHostToDevice, st));
+        }
+        netcsum::SegBatchArgs a{};
+        a.base = d;
+        a.seg_off = reinterpret_cast<const uint64_t*>(d + o_off);
+        a.seg_len_v = reinterpret_cast<const uint16_t*>(d + o_len);
+        a.pseudo = has_ph ? d + o_ph : nullptr;
+        a.pseudo_stride = pseudo_stride;
+        a.pseudo_len = has_ph ? pseudo_len : 0u;
+        a.n_seg = q.ns;
+        a.verify = verify ? 1u : 0u;
+        a.out = d + o_out;
+        // (a segment's byte parity is taken from the device address it is read at, so the copy's new
+        // alignment changes nothing)
+        e = launch_batch(a, 0u, st);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        NC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(h_out) + (size_t)q.s0 * elt, d + o_out, (size_t)q.ns * elt,
+                              hipMemcpyDeviceToHost, st));
+    }
+    for (int j = 0; j < 3; ++j) NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    return NET_UTIL_ERR_NONE;
+}
+
+// Packet batches from host memory: RxValidateIP / TxFinalizeIP / RxBurst / TxBurst over the chunks.
+// Tx writes each chunk's bytes back; chunks whose spans overlap (an unsorted or overlapping
+// offset/length batch) would write stale copies over each other, so such a batch runs as one chunk.
+static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, CPU_INT16U pkt_len,
+                        uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg, uint32_t udp_mode, bool tx,
+                        uint32_t n_chunks) {
+    if (n_pkt == 0) return NET_UTIL_ERR_NONE;
+    if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (h_base == nullptr || (h_off != nullptr) != (h_len != nullptr) || (!tx && h_flags == nullptr && h_action == nullptr)) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    HostCtx* cp = nullptr;
+    NET_ERR e = host_ctx(&cp);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    HostCtx& c = *cp;
+    std::vector<HostChunk> ch;
+    bool disjoint = true;
+    uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks, ch, &disjoint);
+    if (tx && !disjoint) maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, 1u, ch, &disjoint);
+    const bool varlen = h_off != nullptr;
+    const uint32_t per = ch[0].ns;
+    // device slot: [bytes | offsets | lengths | flags | actions]; host slot: [offsets | lengths]
+    const size_t o_off = al256(maxb), o_len = o_off + al256(varlen ? (size_t)per * 8u : 0u);
+    const size_t o_fl = o_len + al256(varlen ? (size_t)per * 2u : 0u), o_act = o_fl + al256(per);
+    e = ensure_pipe(c, o_act + al256(per), varlen ? al256((size_t)per * 8u) + (size_t)per * 2u : 0u);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    for (size_t k = 0; k < ch.size(); ++k) {
+        const HostChunk& q = ch[k];
+        const int j = (int)(k % 3u);
+        hipStream_t st = c.pstream[j];
+        uint8_t* d = c.d_pipe[j];
+        NC_HIP(hipMemcpyAsync(d, static_cast<const uint8_t*>(h_base) + q.lo, q.hi - q.lo, hipMemcpyHostToDevice, st));
+        if (varlen) {
+            if (k >= 3) NC_HIP(hipStreamSynchronize(st));   // slot j's staging is free again
+            uint64_t* h_o = reinterpret_cast<uint64_t*>(c.h_pipe[j]);
+            uint16_t* h_l = reinterpret_cast<uint16_t*>(c.h_pipe[j] + al256((size_t)per * 8u));
+            for (uint32_t i = 0; i < q.ns; ++i) {
+                h_o[i] = h_off[q.s0 + i] - q.lo;
+                h_l[i] = h_len[q.s0 + i];
+            }
+            NC_HIP(hipMemcpyAsync(d + o_off, h_o, (size_t)q.ns * 8u, hipMemcpyHostToDevice, st));
+            NC_HIP(hipMemcpyAsync(d + o_len, h_l, (size_t)q.ns * 2u, hipMemcpyHostToDevice, st));
+        }
+        e = pkt_batch(d, varlen ? reinterpret_cast<const uint64_t*>(d + o_off) : nullptr,
+                      varlen ? reinterpret_cast<const uint16_t*>(d + o_len) : nullptr, stride, pkt_len, q.ns,
+                      h_flags ? d + o_fl : nullptr, udp_mode, tx, 0, st, h_action ? d + o_act : nullptr, rx_cfg);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        if (h_flags) NC_HIP(hipMemcpyAsync(h_flags + q.s0, d + o_fl, q.ns, hipMemcpyDeviceToHost, st));
+        if (h_action) NC_HIP(hipMemcpyAsync(h_action + q.s0, d + o_act, q.ns, hipMemcpyDeviceToHost, st));
+        if (tx) {
+            NC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(h_base) + q.lo, d, q.hi - q.lo, hipMemcpyDeviceToHost, st));
+        }
+    }
+    for (int j = 0; j < 3; ++j) NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    return NET_UTIL_ERR_NONE;
+}
+
+NET_ERR NetUtil_MI355X_RxValidateIPHost(const void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                                        CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, uint32_t n_chunks) {
+    if (n_pkt != 0 && h_flags == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    return pkt_host(const_cast<void*>(h_base), h_off, h_len, stride, pkt_len, n_pkt, h_flags, nullptr, 0u, 1u, false,
+                    n_chunks);
+}
+
+NET_ERR NetUtil_MI355X_TxFinalizeIPHost(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                                        CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, int udp_tx_csum,
+                                        uint32_t n_chunks) {
+    return pkt_host(h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, nullptr, 0u, udp_tx_csum ? 1u : 0u, true,
+                    n_chunks);
+}
+
+NET_ERR NetUtil_MI355X_RxBurstHost(const void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                                   CPU_INT16U pkt_len, uint32_t n_pkt, uint32_t rx_cfg, uint8_t* h_action,
+                                   uint8_t* h_flags, uint32_t n_chunks) {
+    if (n_pkt != 0 && h_action == nullptr) return NET_ERR_FAULT_NULL_PTR;
+    if (rx_cfg & ~(uint32_t)NETCSUM_RXCFG_UDP_DISCARD_NO_CHK_SUM) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    return pkt_host(const_cast<void*>(h_base), h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, 1u,
+                    false, n_chunks);
+}
+
+NET_ERR NetUtil_MI355X_TxBurstHost(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                                   CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, uint32_t n_chunks) {
+    return pkt_host(h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, nullptr, 0u, 2u, true, n_chunks);
 }
 
 NET_ERR NetUtil_MI355X_Fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern,

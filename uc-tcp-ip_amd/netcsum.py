@@ -229,6 +229,16 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_RxAction.restype = ctypes.c_uint8
     L.NetUtil_MI355X_RxBurstTally.argtypes = [vp, u32, vp]
     L.NetUtil_MI355X_RxBurstTally.restype = i32
+    L.NetUtil_MI355X_ChkSumBatchVarLenHost.argtypes = [vp, vp, vp, vp, u32, u16, u32, vp, i32, u32]
+    L.NetUtil_MI355X_ChkSumBatchVarLenHost.restype = i32
+    L.NetUtil_MI355X_RxValidateIPHost.argtypes = [vp, vp, vp, u64, u16, u32, vp, u32]
+    L.NetUtil_MI355X_RxValidateIPHost.restype = i32
+    L.NetUtil_MI355X_TxFinalizeIPHost.argtypes = [vp, vp, vp, u64, u16, u32, vp, i32, u32]
+    L.NetUtil_MI355X_TxFinalizeIPHost.restype = i32
+    L.NetUtil_MI355X_RxBurstHost.argtypes = [vp, vp, vp, u64, u16, u32, u32, vp, vp, u32]
+    L.NetUtil_MI355X_RxBurstHost.restype = i32
+    L.NetUtil_MI355X_TxBurstHost.argtypes = [vp, vp, vp, u64, u16, u32, vp, u32]
+    L.NetUtil_MI355X_TxBurstHost.restype = i32
     L.NetUtil_32BitCRC_Calc.argtypes = [vp, u32, perr]
     L.NetUtil_32BitCRC_Calc.restype = u32
     L.NetUtil_32BitCRC_CalcCpl.argtypes = [vp, u32, perr]
@@ -577,6 +587,58 @@ def rx_burst_tally(actions):
     _check(lib().NetUtil_MI355X_RxBurstTally(a.ctypes.data if a.size else None, a.size, ctr.ctypes.data),
            "NetUtil_MI355X_RxBurstTally")
     return [int(x) for x in ctr]
+
+
+# ------------------------------------------------------------------ host-memory forms ((2e))
+def batch_varlen_host(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out, op=OP_DATA_CALC,
+                      n_chunks=8, check=True):
+    if n_seg:
+        _require(seg_off, 8 * n_seg, "segment offsets")
+        _require(seg_len, 2 * n_seg, "segment lengths")
+        _require(out, n_seg * (2 if op in (OP_DATA_CALC, OP_HDR_CALC) else 1), "out")
+    err = lib().NetUtil_MI355X_ChkSumBatchVarLenHost(_p(base), _p(seg_off), _p(seg_len), _p(pseudo), pseudo_stride,
+                                                     pseudo_len, n_seg, _p(out), op, n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_ChkSumBatchVarLenHost")
+    return err
+
+
+def rx_validate_ip_host(base, n, flags, off=None, lens=None, stride=0, pkt_len=0, n_chunks=8, check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_RxValidateIPHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags), n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_RxValidateIPHost")
+    return err
+
+
+def tx_finalize_ip_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, udp_tx_csum=True, n_chunks=8,
+                        check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_TxFinalizeIPHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
+                                                int(bool(udp_tx_csum)), n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_TxFinalizeIPHost")
+    return err
+
+
+def rx_burst_host(base, n, action, flags=None, off=None, lens=None, stride=0, pkt_len=0, rx_cfg=0, n_chunks=8,
+                  check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    if n:
+        _require(action, n, "actions")
+    err = lib().NetUtil_MI355X_RxBurstHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, rx_cfg, _p(action),
+                                           _p(flags), n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_RxBurstHost")
+    return err
+
+
+def tx_burst_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, n_chunks=8, check=True):
+    _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
+    err = lib().NetUtil_MI355X_TxBurstHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags), n_chunks)
+    if check:
+        _check(err, "NetUtil_MI355X_TxBurstHost")
+    return err
 
 
 def fill(buf, n_bytes, seed, pattern=0, stream=None, first_byte=0):
