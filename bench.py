@@ -35,6 +35,12 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+# CPU baseline: the OpenMP workers are pinned (OMP_PROC_BIND=close over cores); set
+# before torch loads libgomp, which reads them once. Single-rank runs only (the baseline is rank 0 at
+# N = 1; ranks of an N > 1 run would pin their threads onto the same cores).
+if os.environ.get("WORLD_SIZE", "1") == "1":
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
 sys.path.insert(0, os.path.join(REPO, "uc-tcp-ip_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
@@ -191,7 +197,9 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
     import tempfile
     threads, cpu_info = host_cpus()
     n = 1 << 18                                      # 256 Ki segments = 396 MB: larger than the host LLC
-    seg, ph = host_c2_shard(oracle, 0, n, L, plen)
+    # first-touched by the workers that will read them (the batch's static partition)
+    seg = oracle.fill_parallel(0, n * L, SEED, 0, n_threads=threads, unit=L)
+    ph = c2_pseudo_headers(0, n, L, plen) if plen else None
     sample_b = n * (L + plen)
     reps, el = _time_cpu(lambda: oracle.batch_strided(seg, L, L, ph, plen, plen, n, 0, n_threads=threads), seconds)
     gib = reps * sample_b / el / 2 ** 30
@@ -207,6 +215,8 @@ def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
                 best = round(rb * sample_b / eb / 2 ** 30, 3)
     except Exception as e:                           # noqa: BLE001 — a missing compiler only drops this line
         best = f"unavailable: {e}"
+    cpu_info.update({"omp_proc_bind": os.environ.get("OMP_PROC_BIND"), "omp_places": os.environ.get("OMP_PLACES"),
+                     "first_touch": "OpenMP workers (static partition of the batch)"})
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port", **cpu_info,
             "value_per_core": round(gib / threads, 3),
             "value_1thread": round(r1 * sample_b / e1 / 2 ** 30, 3),

@@ -452,6 +452,24 @@ void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t s
     }
 }
 
+/* The same bytes, first-touched by the OpenMP workers that will read them: units of `unit` bytes
+ * are distributed schedule(static) over n_threads threads, the partition Oracle_Batch* uses for
+ * n_bytes / unit segments of `unit` bytes each (CPU-baseline setup). */
+void Oracle_FillParallel(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern,
+                         int n_threads, uint64_t unit)
+{
+    int nt = (n_threads > 0) ? n_threads : omp_get_max_threads();
+    uint64_t n_units = unit ? (n_bytes + unit - 1u) / unit : 1u;
+    int64_t u;
+    if (unit == 0u) unit = n_bytes;
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (u = 0; u < (int64_t)n_units; ++u) {
+        uint64_t lo = (uint64_t)u * unit;
+        uint64_t len = (lo + unit <= n_bytes) ? unit : n_bytes - lo;
+        Oracle_Fill(buf + lo, first_byte + lo, len, seed, pattern);
+    }
+}
+
 /* ------------------------------ CRC-32 (net_util.c:485-636) ------------------------------- */
 
 /* Restates NetUtil_32BitCRC_Calc (net_util.c:485-530): register starts at

@@ -63,6 +63,8 @@ void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const ui
                         const uint32_t *chain_first, const uint8_t *pseudo, uint32_t pseudo_stride,
                         uint16_t pseudo_len, uint32_t n_chains, void *out, int op, int n_threads);
 void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern);
+void Oracle_FillParallel(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern,
+                         int n_threads, uint64_t unit);
 
 /* Config C1 (BASELINE configs[0]) per-datagram checksum sequence of the loopback UDP echo
  * (SURVEY §3.1/§3.2), `iters` times on the same NET_BUF: Tx DataCalc(pbuf, pseudo, plen)

@@ -77,6 +77,8 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.Oracle_BatchChains.restype = None
     L.Oracle_Fill.argtypes = [vp, u64, u64, u64, i32]
     L.Oracle_Fill.restype = None
+    L.Oracle_FillParallel.argtypes = [vp, u64, u64, u64, i32, i32, u64]
+    L.Oracle_FillParallel.restype = None
     L.Oracle_C1Loop.argtypes = [vp, vp, u16, vp, u64]
     L.Oracle_C1Loop.restype = u32
     L.Oracle_CRC32Calc.argtypes = [vp, u32, pu32]
@@ -177,6 +179,14 @@ def batch_chains(base: np.ndarray, piece_off: np.ndarray, piece_len: np.ndarray,
 def fill(first_byte: int, n_bytes: int, seed: int, pattern: int = 0) -> np.ndarray:
     buf = np.empty(n_bytes, dtype=np.uint8)
     lib().Oracle_Fill(buf.ctypes.data, first_byte, n_bytes, seed, pattern)
+    return buf
+
+
+def fill_parallel(first_byte: int, n_bytes: int, seed: int, pattern: int = 0, n_threads: int = 0,
+                  unit: int = 0) -> np.ndarray:
+    """fill(), first-touched by the OpenMP workers in the static partition of `unit`-byte items."""
+    buf = np.empty(n_bytes, dtype=np.uint8)
+    lib().Oracle_FillParallel(buf.ctypes.data, first_byte, n_bytes, seed, pattern, n_threads, unit)
     return buf
 
 

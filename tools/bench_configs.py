@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Secondary measurements for DESIGN.md (not the bench.py line): configs C3 and C4 with the library's
-default launch policy, the host-memory (PCIe-inclusive) C2 rate, and the per-packet drop-in latency.
+default launch policy and a CPU baseline beside each (the oracle's C restatement of net_util.c, -O2,
+OpenMP over the host CPUs bench.py uses, data first-touched by the workers, on a bounded sample),
+the packet batches (fused Rx, Tx on packed and on NET_BUF-shaped buffers, the offload-seam bursts),
+the host-memory (PCIe-inclusive) rates of C2, C4 and the bursts, and the per-packet drop-in latency.
 Every measured batch is spot-checked against the oracle."""
 import json
 import os
@@ -16,7 +19,17 @@ import torch  # noqa: E402
 
 import netcsum  # noqa: E402
 import oracle  # noqa: E402
-from bench import SEED, c2_pseudo_headers  # noqa: E402
+from bench import SEED, c2_pseudo_headers, host_cpus  # noqa: E402
+
+
+def cpu_rate(fn, nbytes, seconds=2.0):
+    """GiB/s of fn() over nbytes per call, repeated for `seconds` after one warm call."""
+    fn()
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        reps += 1
+    return round(reps * nbytes / (time.perf_counter() - t0) / 2 ** 30, 3)
 
 
 def events_ms(fn, st, reps=20, warm=3, warm_s=0.1):
@@ -55,7 +68,17 @@ def main():
     out["C3"] = {"headers": nh, "ms": round(ms, 4), "Ghdr_per_s": round(nh / ms / 1e6, 2), "kernel": netcsum.last_launch(),
                  "GiB_per_s_checksummed": round(nh * 20 / ms / 1e6 / 1.073741824, 1),
                  "GB_per_s_algorithmic": round(nh * 22 / ms / 1e6, 1), "parity_sample_ok": ok}
-    del hdr, o3
+    threads, _ = host_cpus()
+    ns = 1 << 22                                     # 4 Mi headers = 84 MB sample of the C3 shape
+    hs = oracle.fill_parallel(0, ns * 20, SEED, 0, n_threads=threads, unit=20)
+    for t in (threads, 1):
+        g = cpu_rate(lambda: oracle.batch_strided(hs, 20, 20, None, 0, 0, ns, 2, n_threads=t), ns * 20,
+                     2.0 if t > 1 else 0.5)
+        out["C3"]["cpu_GiB_per_s" + ("" if t > 1 else "_1thread")] = g
+    out["C3"]["cpu"] = {"threads": threads, "kind": "port (oracle/net_util_oracle.c -O2, HdrCalc per header)",
+                        "sample": f"{ns} x 20-B headers, first-touched by the workers",
+                        "Ghdr_per_s": round(out["C3"]["cpu_GiB_per_s"] * 2 ** 30 / 20 / 1e9, 3)}
+    del hdr, o3, hs
     torch.cuda.empty_cache()
     # ---- C4: 1 M packed UDP datagrams, 40..9000 B (seed 7), 12-B pseudo each
     rng = np.random.default_rng(7)
@@ -83,7 +106,35 @@ def main():
                  "GiB_per_s_checksummed": round((tot + 12 * nv) / ms / 1e6 / 1.073741824, 1),
                  "GB_per_s_algorithmic": round((tot + 14 * nv) / ms / 1e6, 1),
                  "descriptor_bytes_per_launch": 10 * nv, "kernel": netcsum.last_launch(), "parity_sample_ok": bool(np.array_equal(got, want))}
-    del base, o4, bh
+    # host-memory C4 (PCIe-inclusive): the same packed datagrams from pinned memory, pipelined
+    bh_p = torch.from_numpy(bh[:tot]).pin_memory()
+    off_h, len_h = torch.from_numpy(off.view(np.int64)).pin_memory(), torch.from_numpy(lens.view(np.int16)).pin_memory()
+    ph_h = torch.from_numpy(ph.reshape(-1)).pin_memory()
+    o4h = torch.empty(nv, dtype=torch.int16).pin_memory()
+    rates = {}
+    for chunks in (4, 16, 64):
+        netcsum.batch_varlen_host(bh_p, off_h, len_h, ph_h, 12, 12, nv, o4h, 0, n_chunks=chunks)
+        ts = []
+        for _ in range(4):
+            t0 = time.perf_counter()
+            netcsum.batch_varlen_host(bh_p, off_h, len_h, ph_h, 12, 12, nv, o4h, 0, n_chunks=chunks)
+            ts.append(time.perf_counter() - t0)
+        rates[chunks] = round((tot + 12 * nv) / statistics.median(ts) / 2 ** 30, 2)
+    out["C4"]["host_memory_GiB_per_s_by_chunks"] = rates
+    out["C4"]["host_memory_parity_ok"] = bool(np.array_equal(o4h.numpy().view(np.uint16)[sel], want))
+    del bh_p, off_h, len_h, ph_h, o4h
+    # CPU baseline on a 256 Ki-datagram sample of the same length distribution
+    threads, _ = host_cpus()
+    ncs = 1 << 18
+    tot_s = int(off[ncs - 1]) + int(lens[ncs - 1])
+    bs = oracle.fill_parallel(0, tot_s, SEED, 0, n_threads=threads, unit=max(1, tot_s // threads))
+    for t in (threads, 1):
+        g = cpu_rate(lambda: oracle.batch_varlen(bs, off[:ncs], lens[:ncs], ph[:ncs].reshape(-1), 12, 12, 0,
+                                                 n_threads=t), tot_s + 12 * ncs, 2.0 if t > 1 else 0.5)
+        out["C4"]["cpu_GiB_per_s" + ("" if t > 1 else "_1thread")] = g
+    out["C4"]["cpu"] = {"threads": threads, "kind": "port (oracle/net_util_oracle.c -O2, DataCalc per datagram)",
+                        "sample": f"first {ncs} datagrams ({tot_s / 1e9:.2f} GB), first-touched by the workers"}
+    del base, o4, bh, bs
     torch.cuda.empty_cache()
     # ---- fused Rx validation of 1 M x 1500-B IPv4/TCP datagrams vs the two-pass form
     n, L = 1 << 20, 1500
@@ -119,7 +170,27 @@ def main():
                                  "all_valid_fused": ok_all, "all_valid_two_pass": two_ok, "kernel": fused_kernel}
     ms_tx = events_ms(lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st), st)
     out["tx_finalize_1500B_tcp"] = {"ms": round(ms_tx, 4), "GiB_per_s": round(n * L / ms_tx / 1e6 / 1.073741824, 1),
+                                    "GB_per_s_algorithmic": round(n * (L + 4) / ms_tx / 1e6, 1),
                                     "kernel": netcsum.last_launch()}
+    # NET_BUF-shaped buffers: one 2 KiB buffer per datagram, the IPv4 header 64-B aligned at +64, so
+    # the IPv4 (+10) and TCP (+36) checksum fields share one 64-B line (tools/run_config.py tx_nb)
+    S, lead = 2048, 64
+    nbuf = torch.empty(n * S + 256, dtype=torch.uint8, device=dev)
+    netcsum.fill(nbuf, n * S, SEED, 0)
+    nv_ = nbuf[: n * S].view(n, S)
+    nv_[:, lead:lead + 12] = hdr
+    nb = nbuf[lead:]
+    netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st)
+    ms_nb_tx = events_ms(lambda: netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st), st)
+    k_nb_tx = netcsum.last_launch()
+    ms_nb_rx = events_ms(lambda: netcsum.rx_validate_ipv4(nb, n, flags, stride=S, pkt_len=L, stream=st), st)
+    out["netbuf_2KiB_1500B_tcp"] = {
+        "layout": "1 M buffers of 2048 B, IPv4 header at +64 (both checksum fields in one 64-B line)",
+        "ms_tx": round(ms_nb_tx, 4), "GB_per_s_algorithmic_tx": round(n * (L + 4) / ms_nb_tx / 1e6, 1),
+        "ms_rx": round(ms_nb_rx, 4), "GB_per_s_algorithmic_rx": round(n * (L + 1) / ms_nb_rx / 1e6, 1),
+        "all_valid_rx": bool(((flags & 0x07) == 0x07).all().item()), "kernel_tx": k_nb_tx,
+        "kernel_rx": netcsum.last_launch()}
+    del nbuf, nv_, nb
     # ---- the same 1 M x 1500-B datagrams as IPv6/TCP (40-B header, 40-B pseudo-header)
     hdr6 = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8, device=dev)
     v[:, 0:8] = hdr6
@@ -138,6 +209,33 @@ def main():
     okmx = bool(((flags & 0x07) == 0x07).all().item())
     out["mixed_v4_v6_1500B_tcp"] = {"packets": n, "ms_rx": round(msmx, 4), "all_valid_rx": okmx,
                                     "GiB_per_s_rx": round(n * L / msmx / 1e6 / 1.073741824, 1)}
+    # the checksum-offload seam's bursts on the same mixed ring (actions instead of / beside flags)
+    act = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ms_rb = events_ms(lambda: netcsum.rx_burst(pk, n, act, stride=L, pkt_len=L, stream=st), st)
+    ok_rb = bool((act == 0).all().item())
+    ms_tb = events_ms(lambda: netcsum.tx_burst(pk, n, None, stride=L, pkt_len=L, stream=st), st)
+    out["offload_bursts_mixed_1500B"] = {
+        "ms_rx_burst": round(ms_rb, 4), "GB_per_s_algorithmic_rx": round(n * (L + 1) / ms_rb / 1e6, 1),
+        "all_delivered": ok_rb, "ms_tx_burst": round(ms_tb, 4),
+        "GB_per_s_algorithmic_tx": round(n * (L + 4) / ms_tb / 1e6, 1), "kernel_tx": netcsum.last_launch()}
+    # ... and from pinned host memory (a NIC ring / socket buffers): PCIe-inclusive
+    pk_h = torch.empty(n * L, dtype=torch.uint8).pin_memory()
+    pk_h.copy_(pk[: n * L])
+    act_h = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    rate = {}
+    for name, fn in (("rx_burst_host", lambda: netcsum.rx_burst_host(pk_h, n, act_h, stride=L, pkt_len=L, n_chunks=16)),
+                     ("tx_burst_host", lambda: netcsum.tx_burst_host(pk_h, n, None, stride=L, pkt_len=L, n_chunks=16))):
+        fn()
+        ts = []
+        for _ in range(4):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        rate[name + "_GiB_per_s"] = round(n * L / statistics.median(ts) / 2 ** 30, 2)
+    rate["rx_burst_host_all_delivered"] = bool((act_h == 0).all().item())
+    rate["tx_burst_host_bytes_equal_device"] = bool(torch.equal(pk_h.to(dev), pk[: n * L]))
+    out["offload_bursts_mixed_1500B"].update(rate)
+    del pk_h, act_h
     out["ipv6_1500B_tcp"] = {"packets": n, "ms_rx": round(ms6, 4), "ms_tx": round(ms6_tx, 4),
                              "GiB_per_s_rx": round(n * L / ms6 / 1e6 / 1.073741824, 1),
                              "GiB_per_s_tx": round(n * L / ms6_tx / 1e6 / 1.073741824, 1), "all_valid_rx": ok6,

@@ -19,6 +19,28 @@ def rows(pattern):
     return list(csv.DictReader(open(f[0])))
 
 
+# the source file that defines each kernel (+ the shared headers): a summary is evidence for the
+# exact sources whose hash it records
+KERNEL_FILES = {"seg_stream": "netcsum_stream.hip", "read_run": "netcsum_stream.hip", "varlen_runlen": "netcsum_stream.hip",
+                "seg_hdrstream": "netcsum_hdrstream.hip", "seg_hdr_": "netcsum_hdr.hip", "pkt_stream": "netcsum_pktstream.hip",
+                "pkt_scatter": "netcsum_pktstream.hip", "pkt_batch": "netcsum_packets.hip", "pkt_v6_walk": "netcsum_v6walk.hip",
+                "chain_": "netcsum_chains.hip", "crc_": "netcsum_crc.hip", "seg_small": "netcsum_small.hip"}
+COMMON = ["netcsum_device.h", "netcsum_kernels.h", "netcsum_stream.h"]
+
+
+def src_sha(kernel_name):
+    import hashlib
+    import os
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "uc-tcp-ip_amd", "csrc")
+    f = next((v for k, v in KERNEL_FILES.items() if k in kernel_name), None)
+    if f is None:
+        return None
+    h = hashlib.sha256()
+    for name in [f] + COMMON:
+        h.update(open(os.path.join(csrc, name), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def main(tag, cfg, out):
     log = open(f"{out}/{tag}_{cfg}_run.log").read()
     m = re.search(r"algo_bytes=(\d+)", log)
@@ -35,6 +57,13 @@ def main(tag, cfg, out):
                 vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in vals.items():
             pmc[k][ctr + "_KB"] = statistics.median(v)
+    extra = defaultdict(lambda: defaultdict(list))     # optional third pass (EXTRA_PMC)
+    for r in rows(f"{out}/{tag}_{cfg}_extra/**/extra_counter_collection.csv"):
+        if "netcsum" in r["Kernel_Name"]:
+            extra[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in extra.items():
+        for c, v in cs.items():
+            pmc[k][c] = statistics.median(v)
     res = {"tag": tag, "config": cfg, "launch": next((ln for ln in log.splitlines() if ln.startswith(cfg + " ")), None),
            "algorithmic_bytes_per_launch": algo, "kernels": {}}
     for k in sorted(set(trace) | set(pmc)):
@@ -48,6 +77,7 @@ def main(tag, cfg, out):
                 d["traffic_over_algorithmic"] = round((d["hbm_read_bytes"] + d["hbm_write_bytes"]) / algo, 4)
         if algo and d["avg_us"]:
             d["algorithmic_GBps_at_avg"] = round(algo / (d["avg_us"] * 1e3), 1)
+        d["kernel_src_sha"] = src_sha(k)
         res["kernels"][k] = d
     print(json.dumps(res, indent=1))
 

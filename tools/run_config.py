@@ -6,6 +6,11 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   rx / tx  fused Rx / Tx finalize, 1 M x 1500-B IPv4/TCP, strided; tx2 = two-pass Tx
   rx6 / rxmix  fused Rx of the same datagrams as IPv6/TCP / alternating IPv4 and IPv6 (bench_configs)
   crc  CRC-32 CalcCpl of 1 M x 1500-B frames, strided (the library's default CRC form)
+  tx_nb / rx_nb  Tx finalize / fused Rx on NET_BUF-shaped buffers: 1 M buffers of 2048 B, the 1500-B
+       IPv4/TCP datagram at +64 (both checksum fields in one 64-B line)
+  rxb / txb  the offload-seam bursts (RxBurst / TxBurst) on 1 M x 1500-B alternating IPv4 / IPv6
+  chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
+       2 KiB buffer at +42), DataCalc
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
 import os
 import sys
@@ -61,6 +66,38 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device=dev)
         fn = lambda: netcsum.batch_varlen(base, off_d, len_d, ph, 12, 12, n, out, 0, stream=st)  # noqa: E731
         algo = total + 12 * n + 2 * n
+    elif name == "chains":
+        nc, per, B = 1 << 14, 45, 2048
+        plen = np.full(per, 1480, np.uint16)
+        plen[-1] = 65515 - 1480 * (per - 1) - 8
+        lens = np.tile(plen, nc)
+        offs = (np.arange(nc * per, dtype=np.uint64) * B + 42).astype(np.uint64)
+        first = (np.arange(nc + 1, dtype=np.uint64) * per).astype(np.uint32)
+        base = torch.empty(nc * per * B + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(base, nc * per * B, SEED, 0)
+        ph = torch.zeros(nc * 12, dtype=torch.uint8, device=dev)
+        off_d = torch.from_numpy(offs.view(np.int64)).to(dev)
+        len_d = torch.from_numpy(lens.view(np.int16)).to(dev)
+        first_d = torch.from_numpy(first.view(np.int32)).to(dev)
+        out = torch.empty(nc, dtype=torch.int16, device=dev)
+        fn = lambda: netcsum.batch_chains(base, off_d, len_d, first_d, ph, 12, 12, nc, out, 0, stream=st,  # noqa: E731
+                                          n_pieces=nc * per)
+        algo = int(lens.astype(np.int64).sum()) + 12 * nc + 2 * nc
+    elif name in ("tx_nb", "rx_nb"):
+        n, L, S, lead = 1 << 20, 1500, 2048, 64
+        nbuf = torch.empty(n * S + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(nbuf, n * S, SEED, 0)
+        nbuf[: n * S].view(n, S)[:, lead:lead + 12] = torch.tensor(
+            [0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8, device=dev)
+        nb = nbuf[lead:]
+        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st)
+        if name == "tx_nb":
+            fn = lambda: netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st)  # noqa: E731
+            algo = n * (L + 4)
+        else:
+            fn = lambda: netcsum.rx_validate_ipv4(nb, n, flags, stride=S, pkt_len=L, stream=st)  # noqa: E731
+            algo = n * (L + 1)
     else:
         n, L = 1 << 20, 1500
         pk = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
@@ -71,10 +108,10 @@ def main():
         flags = torch.zeros(n, dtype=torch.uint8, device=dev)
         if name == "tx2":
             netcsum.tune(netcsum.TUNE_TX_PASSES, 2)
-        if name in ("rx6", "rxmix"):
+        if name in ("rx6", "rxmix", "rxb", "txb"):
             v[:, 0:8] = torch.tensor([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], dtype=torch.uint8,
                                      device=dev)
-            if name == "rxmix":
+            if name in ("rxmix", "rxb", "txb"):
                 v[0::2, 0:12] = torch.tensor([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0],
                                              dtype=torch.uint8, device=dev)
                 v[0::2, 12:20] = 0x0A
@@ -82,7 +119,13 @@ def main():
             fn = lambda: netcsum.rx_validate_ip(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
             if name == "rx6":
                 fn = lambda: netcsum.rx_validate_ipv6(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
+            act = torch.zeros(n, dtype=torch.uint8, device=dev)
+            if name == "rxb":
+                fn = lambda: netcsum.rx_burst(pk, n, act, stride=L, pkt_len=L, stream=st)  # noqa: E731
             algo = n * (L + 1)
+            if name == "txb":
+                fn = lambda: netcsum.tx_burst(pk, n, None, stride=L, pkt_len=L, stream=st)  # noqa: E731
+                algo = n * (L + 4)
         elif name == "rx":
             fn = lambda: netcsum.rx_validate_ipv4(pk, n, flags, stride=L, pkt_len=L, stream=st)  # noqa: E731
             algo = n * (L + 1)

@@ -304,12 +304,18 @@ struct ScratchSlot {
     hipEvent_t         ev = nullptr;  // recorded after the last launches that used p
     bool               ev_live = false;
     bool               pinned = false;  // used under stream capture: never freed while the thread runs
+    bool               unordered = false;  // used by a lease with no event since the last record
     uint32_t           seq = 0;         // last tag handed out (ScratchLease::next_tag)
 };
 
 hipError_t slot_wait(ScratchSlot& sl) {                // all launches that used sl.p have finished
-    if (!sl.ev_live) return hipSuccess;
-    const hipError_t e = hipEventSynchronize(sl.ev);
+    hipError_t e = hipSuccess;
+    if (sl.unordered) {
+        e = hipDeviceSynchronize();                    // (the caller has made sl.dev current)
+        sl.unordered = false;
+    } else if (sl.ev_live) {
+        e = hipEventSynchronize(sl.ev);
+    }
     sl.ev_live = false;
     return e;
 }
@@ -339,11 +345,15 @@ struct ScratchCache {
 thread_local ScratchCache tls_scratch;
 
 // A buffer of >= `bytes` for launches on stream `st` of device `dev`; end() (or the destructor) after
-// the last launch that uses it records the slot's event.
+// the last launch that uses it records the slot's event. An UNORDERED lease (ordered = false) is for
+// contents any interleaving leaves correct (the varlen run word: any value is a valid run length):
+// it records no event (an event record costs ~3 us of GPU time per call, profiles/r3d_event_probe)
+// and its slot is freed after a device synchronisation instead.
 class ScratchLease {
 public:
-    hipError_t acquire(int dev, hipStream_t st, size_t bytes) {
+    hipError_t acquire(int dev, hipStream_t st, size_t bytes, bool ordered = true) {
         stream_ = st;
+        ordered_ = ordered;
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (st != nullptr && hipStreamIsCapturing(st, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
         capturing_ = cs != hipStreamCaptureStatusNone;
@@ -380,16 +390,17 @@ public:
             }
             hit->cap = cap;
         }
-        if (hit->ev_live && !capturing_ && hipEventQuery(hit->ev) == hipErrorNotReady) {
+        if (ordered && hit->ev_live && !capturing_ && hipEventQuery(hit->ev) == hipErrorNotReady) {
             hipError_t e = hipStreamWaitEvent(st, hit->ev, 0);
             if (e != hipSuccess) return e;
         }
-        if (hit->ev == nullptr && !capturing_) {
+        if (hit->ev == nullptr && !capturing_ && ordered) {
             hipError_t e = hipEventCreateWithFlags(&hit->ev, hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
         hit->used = ++c.tick;
         if (capturing_) hit->pinned = true;
+        if (!ordered) hit->unordered = true;
         slot_ = hit;
         return hipSuccess;
     }
@@ -403,7 +414,7 @@ public:
     hipError_t end() {
         ScratchSlot* sl = slot_;
         slot_ = nullptr;
-        if (sl == nullptr || capturing_) return hipSuccess;
+        if (sl == nullptr || capturing_ || !ordered_) return hipSuccess;
         const hipError_t e = hipEventRecord(sl->ev, stream_);
         sl->ev_live = e == hipSuccess;
         return e;
@@ -414,6 +425,7 @@ private:
     ScratchSlot* slot_ = nullptr;
     hipStream_t  stream_ = nullptr;
     bool         capturing_ = false;
+    bool         ordered_ = true;
 };
 
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStream_t s) {
@@ -425,11 +437,13 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         // adaptive varlen runs: a one-block kernel samples the lengths and leaves the run length in
         // this stream's scratch word, which the batch kernel reads (stream order; any value is safe:
         // the kernel never runs shorter runs than its grid covers)
+        // (at +128: the packet batches keep their deferral word at +0 of the same slot)
         ScratchLease word;
-        NC_HIP(word.acquire(dev, s, 256u));
+        NC_HIP(word.acquire(dev, s, 256u, false));
+        uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
         NC_HIP(netcsum::launch_varlen_runlen(a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
-                                             c.stream_spw, static_cast<uint32_t*>(word.ptr()), s));
-        a.run_dev = static_cast<const uint32_t*>(word.ptr());
+                                             c.stream_spw, run, s));
+        a.run_dev = run;
         NC_HIP(netcsum::launch_seg_batch(a, c, s));
         NC_HIP(word.end());
         return NET_UTIL_ERR_NONE;
