@@ -14,4 +14,14 @@
 #define NET_ERR_CFG_ARG_CHK_EXT_EN   DEF_ENABLED   /* template default, Cfg/Template/net_cfg.h:178 */
 #endif
 #define NET_TCP_MODULE_EN                        /* net_cfg_net.h: TCP configured in */
+#ifdef NETCSUM_TEST_OFFLOAD                      /* the burst adapters' build: every checksum offloaded */
+#define NET_IPV4_CFG_CHK_SUM_OFFLOAD_RX_EN   DEF_ENABLED   /* Cfg/Template/net_cfg.h:669-682 */
+#define NET_IPV4_CFG_CHK_SUM_OFFLOAD_TX_EN   DEF_ENABLED
+#define NET_ICMP_CFG_CHK_SUM_OFFLOAD_RX_EN   DEF_ENABLED
+#define NET_ICMP_CFG_CHK_SUM_OFFLOAD_TX_EN   DEF_ENABLED
+#define NET_UDP_CFG_CHK_SUM_OFFLOAD_RX_EN    DEF_ENABLED
+#define NET_UDP_CFG_CHK_SUM_OFFLOAD_TX_EN    DEF_ENABLED
+#define NET_TCP_CFG_CHK_SUM_OFFLOAD_RX_EN    DEF_ENABLED
+#define NET_TCP_CFG_CHK_SUM_OFFLOAD_TX_EN    DEF_ENABLED
+#endif
 #endif

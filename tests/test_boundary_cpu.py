@@ -10,7 +10,10 @@
 * a plain C caller (tests/c/dropin_caller.c) runs every variant under -fsanitize=address,undefined:
   chains of 0-1000 buffers walked and compared with its own concatenation, the error paths of
   net_util.c:168-179,1566-1577,1637-1672 through the drop-in, two threads at once; without a GPU
-  every device call must fail with NET_UTIL_ERR_MI355X_DEV (no fallback).
+  every device call must fail with NET_UTIL_ERR_MI355X_DEV (no fallback);
+* the offload-seam burst caller (tests/c/burst_caller.c) builds standalone and in-stack against
+  stand-in headers configured with every NET_*_CFG_CHK_SUM_OFFLOAD_{RX,TX}_EN enabled, and refuses to
+  build against a stack whose offload flags are off (the adapters replace the stack's checksum calls).
 """
 import os
 import re
@@ -21,7 +24,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/Source"
 CDIR = os.path.join(REPO, "tests", "c")
-VARIANTS = ["standalone_asan", "dbg_asan", "instack_asan", "instack_dbg_asan"]
+VARIANTS = ["standalone_asan", "dbg_asan", "instack_asan", "instack_dbg_asan", "burst_asan", "burst_instack_asan"]
 FUNCS = ["NetUtil_16BitOnesCplChkSumHdrCalc", "NetUtil_16BitOnesCplChkSumHdrVerify",
          "NetUtil_16BitOnesCplChkSumDataCalc", "NetUtil_16BitOnesCplChkSumDataVerify",
          "NetUtil_32BitCRC_Calc", "NetUtil_32BitCRC_CalcCpl", "NetUtil_32BitReflect"]
@@ -74,3 +77,15 @@ def test_c_caller_under_sanitizers(callers, variant):
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert r.stdout.startswith("ok "), r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+
+
+def test_burst_caller_requires_the_offload_configuration():
+    """In-stack, burst_caller.c compiles only when the stack maps its offload flags to the
+    NET_*_CHK_SUM_OFFLOAD_* macros its call sites test (Source/net_cfg_net.h:174-190, 305-366)."""
+    inc = ["-I" + os.path.join(REPO, "tests", "instack"), "-I" + os.path.join(REPO, "include")]
+    src = os.path.join(CDIR, "burst_caller.c")
+    on = subprocess.run(["gcc", "-std=c99", "-fsyntax-only", "-DNETCSUM_IN_STACK", "-DNETCSUM_TEST_OFFLOAD", *inc, src],
+                        capture_output=True, text=True)
+    assert on.returncode == 0, on.stderr
+    off = subprocess.run(["gcc", "-std=c99", "-fsyntax-only", "-DNETCSUM_IN_STACK", *inc, src], capture_output=True, text=True)
+    assert off.returncode != 0 and "OFFLOAD" in off.stderr

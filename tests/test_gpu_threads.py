@@ -36,6 +36,19 @@ def test_c_caller_on_gpu():
     assert r.stdout.startswith("ok ") and "device_missing=0" in r.stdout, r.stdout
 
 
+def test_burst_caller_on_gpu():
+    """tests/c/burst_caller.c with the GPU: a 4096-frame host ring through RxBurstHost (actions and
+    counters equal the caller's own RFC 1071 verdicts) and TxBurstHost (every frame verifies)."""
+    for exe_name in ("burst", "burst_instack"):
+        exe = os.path.join(REPO, "tests", "c", "build", exe_name)
+        if not os.path.exists(exe):
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "c"), "build/" + exe_name], check=True)
+        env = dict(os.environ, NETCSUM_EXPECT_GPU="1")
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=110, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+        assert r.stdout.startswith("ok ") and "gpu=1" in r.stdout, r.stdout
+
+
 def _cases(seed, n):
     rng = random.Random(seed)
     out = []

@@ -3,11 +3,11 @@
 # configs record (tools/bench_configs.py). usage (on the box): bash tools/gpu_pmc_all.sh TAG [configs...]
 set -o pipefail
 T=${1:?tag}; shift
-CONFIGS=${*:-c3 c4 chains rx rx6 rxmix rxb txb tx tx_nb rx_nb}
+CONFIGS=${*:-c3 c4 chains rx rx6 rxmix rxb txb tx tx_nb rx_nb tx_nb2k rx_nb2k}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 for c in $CONFIGS; do
   case $c in
-    tx|tx_nb|txb) X="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" ;;
+    tx|tx_nb|tx_nb2k|txb) X="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" ;;
     *) X="" ;;
   esac
   EXTRA_PMC="$X" bash tools/gpu_pmc.sh $T $c > gpurun_out/${T}_${c}_session.log 2>&1 || { tail -20 gpurun_out/${T}_${c}_session.log; exit 1; }

@@ -45,10 +45,14 @@ def main(tag, cfg, out):
     log = open(f"{out}/{tag}_{cfg}_run.log").read()
     m = re.search(r"algo_bytes=(\d+)", log)
     algo = int(m.group(1)) if m else None
+    m = re.search(r"reps=(\d+)", log)
+    reps = int(m.group(1)) if m else None
     trace = defaultdict(list)
-    for r in rows(f"{out}/{tag}_{cfg}_trace/**/trace_kernel_trace.csv"):
+    for r in sorted(rows(f"{out}/{tag}_{cfg}_trace/**/trace_kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"])):
         if "netcsum" in r["Kernel_Name"]:
             trace[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    if reps:                                            # the timed launches only (after the warm-up)
+        trace = defaultdict(list, {k: (v[-reps:] if len(v) > reps else v) for k, v in trace.items()})
     pmc = defaultdict(dict)
     for kind, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         vals = defaultdict(list)

@@ -6,8 +6,11 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   rx / tx  fused Rx / Tx finalize, 1 M x 1500-B IPv4/TCP, strided; tx2 = two-pass Tx
   rx6 / rxmix  fused Rx of the same datagrams as IPv6/TCP / alternating IPv4 and IPv6 (bench_configs)
   crc  CRC-32 CalcCpl of 1 M x 1500-B frames, strided (the library's default CRC form)
-  tx_nb / rx_nb  Tx finalize / fused Rx on NET_BUF-shaped buffers: 1 M buffers of 2048 B, the 1500-B
-       IPv4/TCP datagram at +64 (both checksum fields in one 64-B line)
+  tx_nb / rx_nb  Tx finalize / fused Rx on NET_BUF-shaped buffers of the reference's template
+       (Cfg/Template/net_dev_cfg.c:146-149: 1518-B large buffers, 4-B alignment -> a 1520-B stride):
+       the 1500-B IPv4/TCP datagram after a 14-B Ethernet header, 1506 B present per buffer
+  tx_nb2k / rx_nb2k  the same in 2048-B buffers with the IPv4 header at +64 (both checksum fields
+       in one 64-B line)
   rxb / txb  the offload-seam bursts (RxBurst / TxBurst) on 1 M x 1500-B alternating IPv4 / IPv6
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -83,20 +86,22 @@ def main():
         fn = lambda: netcsum.batch_chains(base, off_d, len_d, first_d, ph, 12, 12, nc, out, 0, stream=st,  # noqa: E731
                                           n_pieces=nc * per)
         algo = int(lens.astype(np.int64).sum()) + 12 * nc + 2 * nc
-    elif name in ("tx_nb", "rx_nb"):
-        n, L, S, lead = 1 << 20, 1500, 2048, 64
+    elif name in ("tx_nb", "rx_nb", "tx_nb2k", "rx_nb2k"):
+        n, L = 1 << 20, 1500
+        S, lead = (2048, 64) if name.endswith("2k") else (1520, 14)
+        present = min(S - lead, 65535)
         nbuf = torch.empty(n * S + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(nbuf, n * S, SEED, 0)
         nbuf[: n * S].view(n, S)[:, lead:lead + 12] = torch.tensor(
             [0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], dtype=torch.uint8, device=dev)
         nb = nbuf[lead:]
         flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-        netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st)
-        if name == "tx_nb":
-            fn = lambda: netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=L, stream=st)  # noqa: E731
+        netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=present, stream=st)
+        if name.startswith("tx"):
+            fn = lambda: netcsum.tx_finalize_ipv4(nb, n, None, stride=S, pkt_len=present, stream=st)  # noqa: E731
             algo = n * (L + 4)
         else:
-            fn = lambda: netcsum.rx_validate_ipv4(nb, n, flags, stride=S, pkt_len=L, stream=st)  # noqa: E731
+            fn = lambda: netcsum.rx_validate_ipv4(nb, n, flags, stride=S, pkt_len=present, stream=st)  # noqa: E731
             algo = n * (L + 1)
     else:
         n, L = 1 << 20, 1500
@@ -132,8 +137,15 @@ def main():
         else:
             fn = lambda: netcsum.tx_finalize_ipv4(pk, n, None, stride=L, pkt_len=L, stream=st)  # noqa: E731
             algo = n * (L + 4)
-    for _ in range(3):
+    # warm up by time (the first ~100 launches after an idle gap run at lower clocks);
+    # pmc_kernels.py averages only the `reps` launches after these
+    import time
+    warm, t0 = 0, time.perf_counter()
+    while warm < 3 or time.perf_counter() - t0 < (0.5 if reps > 5 else 0.0):
         fn()
+        warm += 1
+        if warm % 16 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
@@ -142,7 +154,8 @@ def main():
     b.record(st)
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
-    print(f"{name} {netcsum.last_launch()} ms={ms:.4f} algo_bytes={algo} GBps={algo / ms / 1e6:.1f}", flush=True)
+    print(f"{name} {netcsum.last_launch()} ms={ms:.4f} algo_bytes={algo} GBps={algo / ms / 1e6:.1f} "
+          f"warm_launches={warm} reps={reps}", flush=True)
 
 
 if __name__ == "__main__":
