@@ -566,7 +566,8 @@ NET_ERR  NetUtil_MI355X_ReadStream         (const void *d_buf,
                                             uint64_t   *d_sink,
                                             void       *hip_stream);
 
-/* Launch tuning knobs (process-wide; 0 = automatic). */
+/* Launch tuning knobs (0 = automatic). A setting applies to the CALLING host thread's launches only;
+ * every thread starts from the defaults. */
 typedef enum netcsum_tune_key {
     NETCSUM_TUNE_GRID_BLOCKS   = 1,   /* workgroups per launch (0: exactly fill the chip)        */
     NETCSUM_TUNE_GROUP_LANES   = 2,   /* lanes per segment: 0 auto, else 1,4,8,16,32,64          */

@@ -182,3 +182,4 @@ def test_host_memory_forms_check_arguments_before_device_work():
     assert L.NetUtil_MI355X_RxBurstHost(8, None, None, 64, 64, 3, 0, None, None, 4) == E_NULL    # actions
     assert L.NetUtil_MI355X_RxBurstHost(8, None, None, 64, 64, 3, 4, 8, None, 4) == E_ARG        # rx_cfg
     assert L.NetUtil_MI355X_TxBurstHost(None, None, None, 64, 64, 3, None, 4) == E_NULL
+

@@ -192,3 +192,40 @@ def test_scratch_buffers_many_threads_many_streams():
         t.join(timeout=100)
     assert not any(t.is_alive() for t in ths)
     assert errors == []
+
+
+def test_tuning_applies_to_the_calling_thread_only():
+    """NetUtil_MI355X_Tune is per host thread: the main thread forcing the lane-group packet kernel
+    (TUNE_KERNEL 2) and runs of 4 segments does not change another thread's launches, which take the
+    default forms; results are the oracle's either way."""
+    import numpy as np
+    n, L = 4096, 1500
+    rng = np.random.default_rng(5)
+    seg = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+    want = oracle.batch_strided(seg, L, L, None, 0, 0, n, 0)
+    d = torch.from_numpy(seg).cuda()
+    out_main = torch.zeros(n, dtype=torch.int16, device="cuda")
+    netcsum.tune(netcsum.TUNE_KERNEL, 2)
+    try:
+        netcsum.batch_strided(d, L, L, None, 0, 0, n, out_main)
+        torch.cuda.synchronize()
+        desc_main = netcsum.last_launch()
+        seen = {}
+
+        def other():
+            torch.cuda.set_device(0)
+            o = torch.zeros(n, dtype=torch.int16, device="cuda")
+            netcsum.batch_strided(d, L, L, None, 0, 0, n, o)
+            torch.cuda.synchronize()
+            seen["desc"] = netcsum.last_launch()
+            seen["ok"] = np.array_equal(o.cpu().numpy().view(np.uint16), want)
+            netcsum.thread_release()
+
+        t = threading.Thread(target=other)
+        t.start()
+        t.join(timeout=60)
+    finally:
+        netcsum.tune(netcsum.TUNE_KERNEL, 0)
+    assert desc_main.startswith("seg_pipe_kernel"), desc_main
+    assert seen["desc"].startswith("seg_stream_kernel"), seen
+    assert seen["ok"] and np.array_equal(out_main.cpu().numpy().view(np.uint16), want)

@@ -24,16 +24,16 @@ namespace {
 constexpr int kMaxDev = 64;
 constexpr size_t kZeroCopyMax = 16u * 1024u;      // streams up to 16 KiB: zero-copy single-block path
 
-std::atomic<int> g_tune_grid{0};
-std::atomic<int> g_tune_group{0};
-std::atomic<int> g_tune_nt{-1};                   // -1: auto (nt when groups share no chunks)
-std::atomic<int> g_tune_block{256};
-std::atomic<int> g_tune_kernel{0};                 // 0 = auto (5 when small_supported, else 2)
-std::atomic<int> g_tune_chunks{0};
-std::atomic<int> g_tune_probe{1};                 // LDS-DMA read probe by default
-std::atomic<int> g_tune_grid_mult{1};
-std::atomic<int> g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
-std::atomic<int> g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
+thread_local netcsum::TuneKnob g_tune_grid{0};
+thread_local netcsum::TuneKnob g_tune_group{0};
+thread_local netcsum::TuneKnob g_tune_nt{-1};                   // -1: auto (nt when groups share no chunks)
+thread_local netcsum::TuneKnob g_tune_block{256};
+thread_local netcsum::TuneKnob g_tune_kernel{0};                 // 0 = auto (5 when small_supported, else 2)
+thread_local netcsum::TuneKnob g_tune_chunks{0};
+thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read probe by default
+thread_local netcsum::TuneKnob g_tune_grid_mult{1};
+thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
+thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {

@@ -704,10 +704,10 @@ uint32_t h_x8n(uint64_t n) {
     return p;
 }
 
-std::atomic<int> g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL (netcsum_mi355x.h)
-std::atomic<int> g_crc_lanes{0};       // NETCSUM_TUNE_CRC_LANES: interleaved lanes per segment, 0 auto
-std::atomic<int> g_crc_nt{0};          // NETCSUM_TUNE_CRC_NT: non-temporal chunk loads (interleaved form)
-std::atomic<int> g_crc_wide{1};        // NETCSUM_TUNE_CRC_WIDE: 0 byte, 1 11-bit, 2 lane-replicated 6-bit tables
+thread_local TuneKnob g_crc_kernel{0};      // NETCSUM_TUNE_CRC_KERNEL (netcsum_mi355x.h)
+thread_local TuneKnob g_crc_lanes{0};       // NETCSUM_TUNE_CRC_LANES: interleaved lanes per segment, 0 auto
+thread_local TuneKnob g_crc_nt{0};          // NETCSUM_TUNE_CRC_NT: non-temporal chunk loads (interleaved form)
+thread_local TuneKnob g_crc_wide{1};        // NETCSUM_TUNE_CRC_WIDE: 0 byte, 1 11-bit, 2 lane-replicated 6-bit tables
 
 enum class CrcForm { Lane, Block, Ilv1, Ilv2, Ilv4, Ilv8, Ilv16 };
 

@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(256) seg_hdrstream_kernel(SegBatchArgs A, uint
     touch_retire(touch);
 }
 
-std::atomic<int> g_hdr_burst{-1};      // NETCSUM_TUNE_HDR_BURST: -1 default (kHdrBurstDefault), 0, 1
+thread_local TuneKnob g_hdr_burst{-1};      // NETCSUM_TUNE_HDR_BURST: -1 default (kHdrBurstDefault), 0, 1
 constexpr bool kHdrBurstDefault = true;     // C3 0.0584 -> 0.0571-0.0575 ms (profiles/r2zi_c3_burst_sweep.jsonl)
 
 }  // namespace

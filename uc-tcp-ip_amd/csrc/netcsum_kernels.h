@@ -6,6 +6,15 @@
 
 namespace netcsum {
 
+// A launch option (NetUtil_MI355X_Tune): one value per calling host thread, so one thread's tuning
+// never changes another thread's launches; a new thread starts from the defaults.
+struct TuneKnob {
+    int v;
+    template <class... A>
+    int load(A...) const { return v; }
+    void store(int x) { v = x; }
+};
+
 struct SegBatchArgs {
     const uint8_t*  base;          // strided: first segment; varlen: base of the offsets
     const uint64_t* seg_off;       // varlen only (nullptr => strided)

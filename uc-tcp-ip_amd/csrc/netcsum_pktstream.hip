@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(64) l2_writeback_kernel() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-std::atomic<int> g_tx_flush{-1};
+thread_local TuneKnob g_tx_flush{-1};
 
 int tx_flush_mode() {
     const int m = g_tx_flush.load(std::memory_order_relaxed);

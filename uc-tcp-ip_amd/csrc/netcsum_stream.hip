@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint16_t* len
 }  // namespace
 
 namespace {
-std::atomic<int> g_varlen_run_bytes{-1};   // NETCSUM_TUNE_VARLEN_RUN_BYTES: -1 default, 0 fixed runs of 8
+thread_local TuneKnob g_varlen_run_bytes{-1};   // NETCSUM_TUNE_VARLEN_RUN_BYTES: -1 default, 0 fixed runs of 8
 constexpr uint32_t kVarlenRunBytes = 16384u;
 }  // namespace
 
@@ -557,9 +557,9 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
     }
 }
 
-std::atomic<int> g_stream_waves{-1};
-std::atomic<int> g_stream_touch{-1};
-std::atomic<int> g_stream_xcd{-1};
+thread_local TuneKnob g_stream_waves{-1};
+thread_local TuneKnob g_stream_touch{-1};
+thread_local TuneKnob g_stream_xcd{-1};
 }
 
 hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s) {
