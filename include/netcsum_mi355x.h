@@ -614,10 +614,11 @@ typedef enum netcsum_tune_key {
                                          every 1-KiB piece of a wave's run loaded up front): 1 on,
                                          0 off, -1 each kernel's default (segment batches on, packet
                                          batches off)                                               */
-    NETCSUM_TUNE_STREAM_XCD    = 13,  /* segment / varlen / header stream kernels: 1 = XCD-aware block
-                                         order (each XCD's blocks take one contiguous 1/8 of the runs),
-                                         0 = the dispatch order, -1 = each kernel's default (segment
-                                         and varlen batches on, header batches off)                  */
+    NETCSUM_TUNE_STREAM_XCD    = 13,  /* segment / varlen / header / packet stream kernels: 1 = XCD-
+                                         aware block order (each XCD's blocks take one contiguous 1/8
+                                         of the runs), 0 = the dispatch order, -1 = each kernel's
+                                         default (segment and varlen batches on, header and packet
+                                         batches off)                                                */
     NETCSUM_TUNE_TX_FLUSH      = 14,  /* run-stream Tx finalize, write-back of the dirty checksum-field
                                          lines: -1 / 0 none (they are evicted during later launches),
                                          1 scatter stores written through at system scope, 2 an L2

@@ -72,6 +72,7 @@ struct PktBatchArgs {
     uint32_t        rx_cfg;        // Rx: NETCSUM_RXCFG_* bits for the actions
     uint32_t*       defer_word;    // IPv6 / mixed: set to defer_tag by a batch kernel that leaves a
     uint32_t        defer_tag;     // datagram EXT_HDR; the walk pass runs only when it holds the tag
+    uint32_t        xcd;           // run-stream form: XCD-aware block order (set by the launcher)
 };
 
 // Tx UDP checksum policy of a datagram whose checksum field holds `field` (PktBatchArgs::udp_tx_csum).

@@ -367,7 +367,8 @@ template <int D, bool NT, bool TX, bool REC, int VER>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n) {
         return;
     }
@@ -622,6 +623,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     // no piece touch by default: the header prologue already loads each packet's first bytes with
     // the plain policy, and touching every piece on top is slower (r2ct: Rx 0.2174 -> 0.2315 ms)
     a.touch = stream_touch(false) ? 1u : 0u;
+    a.xcd = stream_xcd(false) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     if (TX && rec != nullptr) {
