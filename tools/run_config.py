@@ -11,6 +11,7 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
        the 1500-B IPv4/TCP datagram after a 14-B Ethernet header, 1506 B present per buffer
   tx_nb2k / rx_nb2k  the same in 2048-B buffers with the IPv4 header at +64 (both checksum fields
        in one 64-B line)
+  rx_sNNNN / tx_sNNNN  the 1500-B datagrams at stride NNNN (1500 = packed), 1500 B present
   rxb / txb  the offload-seam bursts (RxBurst / TxBurst) on 1 M x 1500-B alternating IPv4 / IPv6
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -86,10 +87,12 @@ def main():
         fn = lambda: netcsum.batch_chains(base, off_d, len_d, first_d, ph, 12, 12, nc, out, 0, stream=st,  # noqa: E731
                                           n_pieces=nc * per)
         algo = int(lens.astype(np.int64).sum()) + 12 * nc + 2 * nc
-    elif name in ("tx_nb", "rx_nb", "tx_nb2k", "rx_nb2k"):
+    elif name in ("tx_nb", "rx_nb", "tx_nb2k", "rx_nb2k") or name.startswith(("rx_s", "tx_s")):
         n, L = 1 << 20, 1500
         S, lead = (2048, 64) if name.endswith("2k") else (1520, 14)
         present = min(S - lead, 65535)
+        if name.startswith(("rx_s", "tx_s")):                     # rx_sNNNN: stride NNNN, datagram at 0
+            S, lead, present = int(name[4:]), 0, 1500
         nbuf = torch.empty(n * S + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(nbuf, n * S, SEED, 0)
         nbuf[: n * S].view(n, S)[:, lead:lead + 12] = torch.tensor(
