@@ -431,13 +431,13 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         uint32_t u = cur, c = cs, e = ce, a = acc, t = tot_v;
         if (!(u < s_end && e <= pend)) {                       // no packet ends in this piece
             if (u < s_end) {
-                a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+                a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
             }
         } else {
-            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
 #pragma clang loop vectorize(disable) unroll(disable)
             do {
-                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                const uint32_t Pe = piece_prefix(v, full, lane16, e - qb);
                 const uint32_t T = wave_total(a + (Pe - Ps));
                 t = (lane == u - s_begin) ? T : t;
                 a = 0u;
@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                 if (u < s_end) {
                     e = c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin));
                 }
-                Ps = adj ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+                Ps = adj ? Pe : piece_prefix(v, full, lane16, min(c - qb, 1024u));
             } while (u < s_end && e <= pend);
             if (u < s_end) {
                 a = full - Ps;

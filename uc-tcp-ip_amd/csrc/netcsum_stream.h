@@ -33,8 +33,19 @@ __device__ __forceinline__ u32x4 opaque_tuple(u32x4 v) {
 // This lane's share of the bytes of a 1-KiB piece that lie below piece offset x (wave-uniform,
 // 0..1024): its whole chunk if the chunk ends at or below x, the low (x - 16*lane) bytes if x falls
 // inside it, nothing above. A span [xs, xe) of the piece is prefix(xe) - prefix(xs), exactly.
-__device__ __forceinline__ uint32_t piece_prefix(u32x4 v, uint32_t lane16, uint32_t x) {
-    return low_bytes(v, min(max((int)x - (int)lane16, 0), 16));
+// s4 = sum4(v, 0), the whole chunk. Only the lane holding byte x masks its chunk, and its byte count
+// is x & 15: the two 64-bit masks depend on x alone, so with x uniform they are scalar work and each
+// boundary costs the wave 4 AND + 4 SAD + 2 compare + 2 select (the per-lane clamp-and-mask form
+// it replaces cost ~35 VALU per boundary; profiles/r3h_instmix_rx_gap.txt).
+__device__ __forceinline__ uint32_t piece_prefix(u32x4 v, uint32_t s4, uint32_t lane16, uint32_t x) {
+    const uint32_t k = x & 15u;
+    const uint64_t m0 = k >= 8u ? ~0ull : (1ull << (8u * k)) - 1ull;
+    const uint64_t m1 = k <= 8u ? 0ull : (1ull << (8u * (k - 8u))) - 1ull;
+    uint32_t pv = __builtin_amdgcn_sad_u16(v.x & (uint32_t)m0, 0u, 0u);
+    pv = __builtin_amdgcn_sad_u16(v.y & (uint32_t)(m0 >> 32), 0u, pv);
+    pv = __builtin_amdgcn_sad_u16(v.z & (uint32_t)m1, 0u, pv);
+    pv = __builtin_amdgcn_sad_u16(v.w & (uint32_t)(m1 >> 32), 0u, pv);
+    return (lane16 + 16u <= x) ? s4 : ((lane16 < x) ? pv : 0u);
 }
 
 // Sum over the 64 lanes (every lane active): inclusive row scans by DPP row_shr 1/2/4/8 (lanes with

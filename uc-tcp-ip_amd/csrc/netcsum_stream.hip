@@ -188,7 +188,8 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     uint32_t ce = cs + L;
     uint32_t acc = 0u;                                         // this lane's share so far (mod 2^32)
     if constexpr (ONE) {
-        acc = 0u - piece_prefix(opaque_tuple(dv[0]), lane16, cs);    // bytes of piece 0 before the run
+        const u32x4 v0 = opaque_tuple(dv[0]);                  // bytes of piece 0 before the run
+        acc = 0u - piece_prefix(v0, sum4(v0, 0u), lane16, cs);
     }
 
     // State lives in locals inside consume and is written back unconditionally at the end: a branch
@@ -201,7 +202,7 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
         uint32_t u = cur, c = cs, e = ce, a = acc;
         if constexpr (ONE) {
             if (u < s_end && e <= pend) {                      // segment `u` ends in this piece
-                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                const uint32_t Pe = piece_prefix(v, full, lane16, e - qb);
                 finish(u, wave_total(a + Pe), (((e - L) & 1u) != 0u) != ph_odd);
                 a = full - Pe;                                 // the next segment starts at e
                 ++u;
@@ -212,19 +213,19 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
         } else {
             if (!(u < s_end && e <= pend)) {                   // no segment ends in this piece
                 if (u < s_end) {
-                    a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+                    a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
                 }
             } else {
-                uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+                uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
 #pragma clang loop vectorize(disable) unroll(disable)
                 do {
-                    const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                    const uint32_t Pe = piece_prefix(v, full, lane16, e - qb);
                     finish(u, wave_total(a + (Pe - Ps)), ((c & 1u) != 0u) != ph_odd);
                     a = 0u;
                     ++u;
                     c += st;
                     e += st;
-                    Ps = (st == L) ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+                    Ps = (st == L) ? Pe : piece_prefix(v, full, lane16, min(c - qb, 1024u));
                 } while (u < s_end && e <= pend);
                 if (u < s_end) {
                     a = full - Ps;
@@ -378,13 +379,13 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
         uint32_t u = cur, c = cs, e = ce, a = acc;
         if (!(u < s_end && e <= pend)) {
             if (u < s_end) {
-                a += (c <= qb) ? full : full - piece_prefix(v, lane16, min(c - qb, 1024u));
+                a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
             }
         } else {
-            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, lane16, c - qb);
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
 #pragma clang loop vectorize(disable) unroll(disable)
             do {
-                const uint32_t Pe = piece_prefix(v, lane16, e - qb);
+                const uint32_t Pe = piece_prefix(v, full, lane16, e - qb);
                 finish_segment<PH>(u - s_begin, wave_total(a + (Pe - Ps)), ((c & 1u) != 0u) != ph_odd,
                                    A.verify != 0u, lane, ps0, ps1, res0, res1);
                 a = 0u;
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
                     c = pick(rs0, rs1, u - s_begin);
                     e = pick(re0, re1, u - s_begin);
                 }
-                Ps = (c == pe) ? Pe : piece_prefix(v, lane16, min(c - qb, 1024u));
+                Ps = (c == pe) ? Pe : piece_prefix(v, full, lane16, min(c - qb, 1024u));
             } while (u < s_end && e <= pend);
             if (u < s_end) {
                 a = full - Ps;
