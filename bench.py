@@ -187,7 +187,36 @@ def c1_per_call(oracle, netcsum, gpu):
         gpu_us = (time.perf_counter() - t0) / (reps * 4) * 1e6
         res.update({"gpu_dropin_us_per_call": round(gpu_us, 3), "gpu_matches_oracle": got == want,
                     "gpu_over_cpu": round(gpu_us / cpu_us, 1)})
+        res["crc32_mac_per_call"] = crc_per_call(oracle, netcsum)
     return res
+
+
+def crc_per_call(oracle, netcsum):
+    """The drivers' per-call CRC-32 (NetUtil_32BitCRC_CalcCpl of one 6-B multicast MAC address, the
+    reference's only CRC use): the drop-in (host table below 4 KiB, net_util_mi355x.c), the GPU round
+    trip the drop-in no longer takes for it (NetUtil_MI355X_CRC32Host: launch + D2H + sync), and the
+    oracle's C restatement, all called from Python through ctypes (the call overhead is in all three)."""
+    import ctypes
+    mac = bytes([0x01, 0x00, 0x5E, 0x00, 0x00, 0xFB])
+    hb = netcsum.HostBytes(mac)
+    want = oracle.crc32_calc(mac, cpl=True)[0]
+    reps = 2000
+
+    def per_call(fn):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return (time.perf_counter() - t0) / reps * 1e6
+    out = ctypes.c_uint32()
+    lib = netcsum.lib()
+    dropin_us = per_call(lambda: netcsum.CRC32Calc(hb.ptr, 6, cpl=True))
+    gpu_us = per_call(lambda: lib.NetUtil_MI355X_CRC32Host(hb.ptr, 6, ctypes.byref(out)))
+    cpu_us = per_call(lambda: oracle.crc32_calc(mac, cpl=True))
+    got = netcsum.CRC32Calc(hb.ptr, 6, cpl=True)[0]
+    return {"address": "01:00:5e:00:00:fb", "dropin_us_per_call": round(dropin_us, 3),
+            "gpu_round_trip_us_per_call": round(gpu_us, 3), "oracle_us_per_call": round(cpu_us, 3),
+            "dropin_matches_oracle": got == want}
 
 
 def cpu_baseline(oracle, n_seg_full, L, plen, seconds):
