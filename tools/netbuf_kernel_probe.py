@@ -5,7 +5,7 @@ against the lane-group kernel (TUNE_KERNEL 2), two interleaved passes:
   (1520, 14, 1506)  the reference's template large buffers (net_dev_cfg.c:146-149)
   (2048, 64, 1984)  2-KiB buffers, IPv4 header at +64, the rest of the buffer declared present
   (2048, 64, 1500)  the same with only the datagram declared present (run-stream only with mode 2)
-  (1500, 0, 1500)   packed (what skipping costs where there is no slack)
+  (1500, 0, 1500)   packed, for reference
 
 Prints one JSON line per (pass, layout, kernel). profiles/r3j_netbuf_kernel_probe.jsonl; an
 experiment build that skipped the chunks after each datagram's end in slots >= 1 KiB is in
