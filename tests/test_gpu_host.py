@@ -18,6 +18,13 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _defaults():
+    yield
+    netcsum.tune(netcsum.TUNE_KERNEL, 0)
+    netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
+
+
 def _pinned(a):
     t = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
     return t
@@ -124,8 +131,53 @@ def test_tx_burst_host_varlen_and_overlap():
     hb = _pinned(buf)
     netcsum.tx_burst_host(hb, len(pairs), off=offs, lens=lens, n_chunks=6)
     assert np.array_equal(hb.numpy(), want)
-    # the same frames listed evens first, then odds: the chunks' spans overlap -> one chunk, same bytes
+    # the same frames listed evens first, then odds: the chunks' spans overlap (each chunk's records
+    # patch only its own datagrams' fields), same bytes
     perm = np.concatenate([np.arange(0, len(pairs), 2), np.arange(1, len(pairs), 2)])
     hb2 = _pinned(buf)
     netcsum.tx_burst_host(hb2, len(pairs), off=offs[perm].copy(), lens=lens[perm].copy(), n_chunks=6)
     assert np.array_equal(hb2.numpy(), want)
+
+
+@pytest.mark.parametrize("kernel,passes", [(0, 2), (0, 1), (2, 0)])
+@pytest.mark.parametrize("chunks", [1, 5, 64])
+def test_tx_host_records_every_kernel_form(kernel, passes, chunks):
+    """Which fields a datagram had written comes from whichever Tx kernel wrote them: the run-stream
+    kernel (two passes: the scatter pass; one pass: its epilogue), the lane-group kernel
+    (TUNE_KERNEL 2), and the IPv6 walk pass for chains past the first kernel's window; UDP datagrams
+    without a checksum get their 0 written; malformed ones nothing. Pageable numpy memory, odd lead."""
+    import struct
+    from packets import ext_body
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    rng = random.Random(700 + 10 * kernel + passes + chunks)
+    n, stride, lead = 900, 1100, 3
+    pkts = []
+    for i in range(n):
+        if i % 3 == 0:                                   # IPv6 with a long Destination Options header
+            inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 600))
+            u = rng.randint(1, 30)
+            body = struct.pack("!BB", inner[6], u - 1) + ext_body(rng, 60, u * 8 - 2) + inner[40:]
+            pkts.append(inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40] + body)
+        elif i % 3 == 1:
+            pkts.append(make_packet(rng, rng.choice(KINDS), payload=rng.randint(0, 1000)))
+        else:
+            pkts.append(make_packet_v6(rng, rng.choice(KINDS6), payload=rng.randint(0, 1000)))
+    buf = np.frombuffer(rng.randbytes(lead + n * stride + 64), np.uint8).copy()
+    for i, p in enumerate(pkts):
+        p = p[:stride]
+        buf[lead + i * stride:lead + i * stride + len(p)] = np.frombuffer(p, np.uint8)
+    want = buf.copy()
+    want_f = np.zeros(n, np.uint8)
+    for i in range(n):
+        o = lead + i * stride
+        q, want_f[i] = op.tx_finalize_ip(bytes(buf[o:o + stride]), True)
+        want[o:o + stride] = np.frombuffer(q, np.uint8)
+    got = buf.copy()
+    fl = np.zeros(n, np.uint8)
+    netcsum.tx_finalize_ip_host(got[lead:], n, fl, stride=stride, pkt_len=stride, n_chunks=chunks)
+    assert netcsum.last_launch().startswith("pkt_batch_kernel" if kernel == 2 else "pkt_stream_kernel")
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(j), (int(j) - lead) // stride, (int(j) - lead) % stride) for j in bad[:8]]
+    assert np.array_equal(fl, want_f)
+    assert (want_f & op.L4_CHECKED).any() and (want_f & op.MALFORMED).any()

@@ -870,10 +870,12 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
     return NET_UTIL_ERR_NONE;
 }
 
-// udp_mode: PktBatchArgs::udp_tx_csum (Tx); d_action / rx_cfg: the Rx burst actions (Rx, optional).
+// udp_mode: PktBatchArgs::udp_tx_csum (Tx); d_action / rx_cfg: the Rx burst actions (Rx, optional);
+// d_fieldpos: Tx, which fields each packet had written (the host-memory forms' records, optional).
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                          CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, uint32_t udp_mode, bool tx,
-                         int ip_ver, void* hip_stream, uint8_t* d_action = nullptr, uint32_t rx_cfg = 0u) {
+                         int ip_ver, void* hip_stream, uint8_t* d_action = nullptr, uint32_t rx_cfg = 0u,
+                         uint32_t* d_fieldpos = nullptr) {
     if (n_pkt == 0) return NET_UTIL_ERR_NONE;
     if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr && d_action == nullptr)) {
@@ -892,6 +894,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     a.udp_tx_csum = udp_mode;
     a.action_out = tx ? nullptr : d_action;
     a.rx_cfg = rx_cfg;
+    a.fieldpos_out = tx ? d_fieldpos : nullptr;
     netcsum::LaunchCfg c{};
     const uint32_t chunks = d_off ? 288u : ((uint32_t)pkt_len + 30u) / 16u;
     int g = g_tune_group.load();
@@ -1154,9 +1157,26 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
     return NET_UTIL_ERR_NONE;
 }
 
+// Tx records returned from the device for a chunk of a host-memory Tx batch: the checksum fields
+// written into the caller's host buffer (memcpy of the bytes as the device wrote them).
+static void apply_field_records(uint8_t* h_base, const uint64_t* h_off, uint64_t stride, uint32_t s0, uint32_t ns,
+                                const uint64_t* rec) {
+    for (uint32_t i = 0; i < ns; ++i) {
+        const uint64_t r = rec[i];
+        const uint32_t pos = (uint32_t)(r >> 32);
+        if ((pos & (netcsum::kFieldIP | netcsum::kFieldL4)) == 0u) continue;
+        uint8_t* p = h_base + (h_off ? h_off[s0 + i] : (uint64_t)(s0 + i) * stride);
+        const uint16_t ip = (uint16_t)r, l4 = (uint16_t)(r >> 16);
+        if (pos & netcsum::kFieldIP) std::memcpy(p + 10, &ip, 2);
+        if (pos & netcsum::kFieldL4) std::memcpy(p + (pos & 0xFFFFu), &l4, 2);
+    }
+}
+
 // Packet batches from host memory: RxValidateIP / TxFinalizeIP / RxBurst / TxBurst over the chunks.
-// Tx writes each chunk's bytes back; chunks whose spans overlap (an unsorted or overlapping
-// offset/length batch) would write stale copies over each other, so such a batch runs as one chunk.
+// Tx: the device form runs on the chunk's copy and records which checksum fields it wrote
+// (fieldpos); a gather pass packs them into 8-B records, only those return D2H, and the host writes
+// the fields into its own buffer once the chunk's stream has drained (before its slot is reused,
+// and at the end) — 8 B per datagram over PCIe instead of the chunk's bytes.
 static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, CPU_INT16U pkt_len,
                         uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg, uint32_t udp_mode, bool tx,
                         uint32_t n_chunks) {
@@ -1171,23 +1191,38 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
     HostCtx& c = *cp;
     std::vector<HostChunk> ch;
     bool disjoint = true;
-    uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks, ch, &disjoint);
-    if (tx && !disjoint) maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, 1u, ch, &disjoint);
+    if (n_chunks > 0 && n_pkt / n_chunks > (1u << 28)) n_chunks = (n_pkt >> 28) + 1u;   // records: 32-bit offsets
+    const uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks == 0 ? 1u : n_chunks, ch, &disjoint);
     const bool varlen = h_off != nullptr;
     const uint32_t per = ch[0].ns;
-    // device slot: [bytes | offsets | lengths | flags | actions]; host slot: [offsets | lengths]
+    // device slot: [bytes | offsets | lengths | flags | actions | field positions | records];
+    // host slot: [offsets | lengths | records]
     const size_t o_off = al256(maxb), o_len = o_off + al256(varlen ? (size_t)per * 8u : 0u);
     const size_t o_fl = o_len + al256(varlen ? (size_t)per * 2u : 0u), o_act = o_fl + al256(per);
-    e = ensure_pipe(c, o_act + al256(per), varlen ? al256((size_t)per * 8u) + (size_t)per * 2u : 0u);
+    const size_t o_fp = o_act + al256(per), o_rec = o_fp + al256(tx ? (size_t)per * 4u : 0u);
+    const size_t h_rec = varlen ? al256((size_t)per * 8u) + al256((size_t)per * 2u) : 0u;
+    e = ensure_pipe(c, o_rec + al256(tx ? (size_t)per * 8u : 0u), h_rec + (tx ? (size_t)per * 8u : 0u));
     if (e != NET_UTIL_ERR_NONE) return e;
+    uint8_t* hb = static_cast<uint8_t*>(h_base);
+    auto drain = [&](size_t k) -> NET_ERR {                  // chunk k's stream has finished: apply its records
+        NC_HIP(hipStreamSynchronize(c.pstream[k % 3u]));
+        if (tx) {
+            apply_field_records(hb, h_off, stride, ch[k].s0, ch[k].ns,
+                                reinterpret_cast<const uint64_t*>(c.h_pipe[k % 3u] + h_rec));
+        }
+        return NET_UTIL_ERR_NONE;
+    };
     for (size_t k = 0; k < ch.size(); ++k) {
         const HostChunk& q = ch[k];
         const int j = (int)(k % 3u);
         hipStream_t st = c.pstream[j];
         uint8_t* d = c.d_pipe[j];
-        NC_HIP(hipMemcpyAsync(d, static_cast<const uint8_t*>(h_base) + q.lo, q.hi - q.lo, hipMemcpyHostToDevice, st));
+        if (k >= 3 && (varlen || tx)) {                      // slot j's staging is free again
+            e = drain(k - 3u);
+            if (e != NET_UTIL_ERR_NONE) return e;
+        }
+        NC_HIP(hipMemcpyAsync(d, hb + q.lo, q.hi - q.lo, hipMemcpyHostToDevice, st));
         if (varlen) {
-            if (k >= 3) NC_HIP(hipStreamSynchronize(st));   // slot j's staging is free again
             uint64_t* h_o = reinterpret_cast<uint64_t*>(c.h_pipe[j]);
             uint16_t* h_l = reinterpret_cast<uint16_t*>(c.h_pipe[j] + al256((size_t)per * 8u));
             for (uint32_t i = 0; i < q.ns; ++i) {
@@ -1197,17 +1232,30 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
             NC_HIP(hipMemcpyAsync(d + o_off, h_o, (size_t)q.ns * 8u, hipMemcpyHostToDevice, st));
             NC_HIP(hipMemcpyAsync(d + o_len, h_l, (size_t)q.ns * 2u, hipMemcpyHostToDevice, st));
         }
-        e = pkt_batch(d, varlen ? reinterpret_cast<const uint64_t*>(d + o_off) : nullptr,
-                      varlen ? reinterpret_cast<const uint16_t*>(d + o_len) : nullptr, stride, pkt_len, q.ns,
-                      h_flags ? d + o_fl : nullptr, udp_mode, tx, 0, st, h_action ? d + o_act : nullptr, rx_cfg);
+        uint32_t* d_fp = tx ? reinterpret_cast<uint32_t*>(d + o_fp) : nullptr;
+        if (tx) NC_HIP(hipMemsetAsync(d_fp, 0, (size_t)q.ns * 4u, st));   // a packet no kernel wrote: no fields
+        const uint64_t* d_o = varlen ? reinterpret_cast<const uint64_t*>(d + o_off) : nullptr;
+        e = pkt_batch(d, d_o, varlen ? reinterpret_cast<const uint16_t*>(d + o_len) : nullptr, stride, pkt_len, q.ns,
+                      h_flags ? d + o_fl : nullptr, udp_mode, tx, 0, st, h_action ? d + o_act : nullptr, rx_cfg, d_fp);
         if (e != NET_UTIL_ERR_NONE) return e;
         if (h_flags) NC_HIP(hipMemcpyAsync(h_flags + q.s0, d + o_fl, q.ns, hipMemcpyDeviceToHost, st));
         if (h_action) NC_HIP(hipMemcpyAsync(h_action + q.s0, d + o_act, q.ns, hipMemcpyDeviceToHost, st));
         if (tx) {
-            NC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(h_base) + q.lo, d, q.hi - q.lo, hipMemcpyDeviceToHost, st));
+            netcsum::PktBatchArgs g{};
+            g.base = d;
+            g.off = d_o;
+            g.stride = stride;
+            g.n = q.ns;
+            g.fieldpos_out = d_fp;
+            uint64_t* d_rec = reinterpret_cast<uint64_t*>(d + o_rec);
+            NC_HIP(netcsum::launch_pkt_field_gather(g, d_rec, st));
+            NC_HIP(hipMemcpyAsync(c.h_pipe[j] + h_rec, d_rec, (size_t)q.ns * 8u, hipMemcpyDeviceToHost, st));
         }
     }
-    for (int j = 0; j < 3; ++j) NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    for (size_t k = ch.size() > 3 ? ch.size() - 3 : 0; k < ch.size(); ++k) {
+        e = drain(k);
+        if (e != NET_UTIL_ERR_NONE) return e;
+    }
     return NET_UTIL_ERR_NONE;
 }
 

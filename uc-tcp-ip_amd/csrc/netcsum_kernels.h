@@ -73,7 +73,15 @@ struct PktBatchArgs {
     uint32_t*       defer_word;    // IPv6 / mixed: set to defer_tag by a batch kernel that leaves a
     uint32_t        defer_tag;     // datagram EXT_HDR; the walk pass runs only when it holds the tag
     uint32_t        xcd;           // run-stream form: XCD-aware block order (set by the launcher)
+    uint32_t*       fieldpos_out;  // Tx (optional): per packet, which checksum fields were written —
+                                   // kFieldIP | kFieldL4 | transport field offset (host-memory forms)
 };
+constexpr uint32_t kFieldIP = 1u << 31;    // fieldpos_out: the IPv4 header checksum field (+10) written
+constexpr uint32_t kFieldL4 = 1u << 30;    // fieldpos_out: the transport field at (bits 0-15) written
+// One 8-B record per packet of a host-memory Tx batch (pkt_field_gather_kernel): the written field
+// values as they lie in memory (IP | transport << 16), the transport offset << 32, and the
+// kFieldIP / kFieldL4 bits << 32 (bits 62 / 63).
+hipError_t launch_pkt_field_gather(const PktBatchArgs& a, uint64_t* rec_out, hipStream_t s);
 
 // Tx UDP checksum policy of a datagram whose checksum field holds `field` (PktBatchArgs::udp_tx_csum).
 __host__ __device__ __forceinline__ bool udp_tx_compute(uint32_t mode, uint32_t field) {

@@ -404,6 +404,12 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
         }
         const __amdgpu_buffer_rsrc_t rf = byte_rsrc(A.flags_out, A.flags_out ? A.n : 0u);
         store_byte(rf, f, me ? ps.idx : kOOB);
+        if constexpr (TX) {                                      // host-memory forms: what was written
+            const uint64_t qb = A.fieldpos_out ? (uint64_t)A.n * 4u : 0u;
+            const __amdgpu_buffer_rsrc_t rq = byte_rsrc(A.fieldpos_out, (uint32_t)(qb < 0xFFFFFFFFull ? qb : 0xFFFFFFFFull));
+            __builtin_amdgcn_raw_buffer_store_b32((si ? kFieldIP : 0u) | (sl ? kFieldL4 | l4off : 0u), rq,
+                                                  (int)(me ? ps.idx * 4u : kOOB), 0, 0);
+        }
         if constexpr (!TX) {
             const __amdgpu_buffer_rsrc_t ra = byte_rsrc(A.action_out, A.action_out ? A.n : 0u);
             store_byte(ra, l4off, me ? ps.idx : kOOB);
@@ -423,6 +429,9 @@ __device__ __forceinline__ void pkt_store(const PktStore& ps, const PktBatchArgs
         }
         if (!TX && A.action_out) {
             A.action_out[ps.idx] = (uint8_t)l4off;
+        }
+        if (TX && A.fieldpos_out) {
+            A.fieldpos_out[ps.idx] = (si ? kFieldIP : 0u) | (sl ? kFieldL4 | l4off : 0u);
         }
     }
 }

@@ -539,6 +539,9 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         if (cl4 != ~0u) {
             store_field(p + pk.l4_csum_off, cl4);
         }
+        if (A.fieldpos_out) {
+            A.fieldpos_out[idx] = (cip != ~0u ? kFieldIP : 0u) | (cl4 != ~0u ? kFieldL4 | (pk.l4_csum_off & 0xFFFFu) : 0u);
+        }
     }
 }
 
@@ -555,6 +558,9 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
         const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
         if (A.flags_out) {
             A.flags_out[i] = (uint8_t)flags;
+        }
+        if (A.fieldpos_out) {
+            A.fieldpos_out[i] = ((store & 1u) ? kFieldIP : 0u) | ((store & 2u) ? kFieldL4 | l4_off : 0u);
         }
         uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
         if constexpr (WT) {
@@ -579,6 +585,27 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the wave ends when its write-back has
     }
+}
+
+// Host-memory Tx forms (netcsum_abi.hip pkt_host): one 8-B record per packet of the checksum fields
+// the Tx kernels wrote into the device copy (fieldpos_out), so that only 8 B per packet return over
+// PCIe instead of the chunk's bytes; the host writes the fields into its own buffer.
+__global__ void __launch_bounds__(256) pkt_field_gather_kernel(PktBatchArgs A, uint64_t* rec) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.n) {
+        return;
+    }
+    const uint32_t pos = A.fieldpos_out[i];
+    const uint8_t* p = A.base + (A.off ? A.off[i] : i * A.stride);
+    uint32_t v = 0u;
+    if (pos & kFieldIP) {
+        v |= (uint32_t)p[10] | ((uint32_t)p[11] << 8);
+    }
+    if (pos & kFieldL4) {
+        const uint32_t o = pos & 0xFFFFu;
+        v |= ((uint32_t)p[o] | ((uint32_t)p[o + 1u] << 8)) << 16;
+    }
+    rec[i] = (uint64_t)v | ((uint64_t)pos << 32);
 }
 
 // TX_FLUSH 3 / 4: a separate launch of 8 / 256 one-wave workgroups, each an agent-scope release,
@@ -639,6 +666,13 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
 }
 
 }  // namespace
+
+hipError_t launch_pkt_field_gather(const PktBatchArgs& a, uint64_t* rec_out, hipStream_t s) {
+    if (a.n == 0u) return hipSuccess;
+    if (a.fieldpos_out == nullptr || rec_out == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pkt_field_gather_kernel, dim3((unsigned)(((uint64_t)a.n + 255u) / 256u)), dim3(256), 0, s, a, rec_out);
+    return hipGetLastError();
+}
 
 void set_tx_flush(int mode) {
     g_tx_flush.store(mode);

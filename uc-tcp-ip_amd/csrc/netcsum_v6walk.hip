@@ -170,6 +170,7 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
                     if (lane == 0u) {
                         p[csum_off] = 0u;           // NET_UDP_HDR_CHK_SUM_NONE (net_udp.c:2935)
                         p[csum_off + 1u] = 0u;
+                        if (A.fieldpos_out) A.fieldpos_out[i] = kFieldL4 | csum_off;
                     }
                 } else {
                     pseudo = check = true;
@@ -203,6 +204,7 @@ __device__ void walk_one(const PktBatchArgs& A, uint32_t i, uint32_t lane) {
             if (lane == 0u) {
                 p[csum_off] = (uint8_t)(c >> 8);
                 p[csum_off + 1u] = (uint8_t)c;
+                if (A.fieldpos_out) A.fieldpos_out[i] = kFieldL4 | csum_off;
             }
             f |= W_L4_CHECKED | W_L4_OK;
         } else {
