@@ -403,6 +403,91 @@ void Oracle_BatchChains(const uint8_t *base, const uint64_t *piece_off, const ui
     }
 }
 
+/* Per-datagram Rx / Tx checksum sequence of the stack on a strided batch (the CPU line of the fused
+ * packet rows): IPv4 — Rx HdrVerify(IP header) (net_ipv4.c:5247) then, for TCP / UDP, DataVerify of
+ * the transport over a one-buffer NET_BUF with the 12-B pseudo-header {src, dst, 0, proto, length}
+ * (net_tcp.c:7851-7857, net_udp.c:1918-1934; UDP checksum 0 not checked, :1920); Tx the fields
+ * zeroed, HdrCalc written (net_ipv4.c:9573-9586), DataCalc written, UDP 0 -> 0xFFFF
+ * (net_tcp.c:29824-29862, net_udp.c:2891-2937). IPv6 without extension headers — the transport over
+ * the 40-B pseudo-header {src, dst, length, 0, next header} (net_tcp.c:7871-7876, net_udp.c:1947-1953).
+ * The version nibble picks the path per datagram. flags[i]: bit 0 IP header OK (IPv6: 1), bit 1
+ * transport OK, bit 2 transport checked. No length / shape checks: the batch is well formed (the
+ * configs' synthetic datagrams); test and bench use only. */
+static uint16_t orc_be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+static void orc_one_datagram(uint8_t *p, uint16_t avail, int tx, uint8_t *flag)
+{
+    uint8_t  pseudo[40];
+    uint16_t plen, hlen, tot, l4len, c;
+    uint8_t  proto;
+    uint32_t err;
+    NET_BUF  buf;
+    uint8_t  f = 0u;
+    int      v6 = (p[0] >> 4) == 6;
+    if (v6) {
+        hlen  = 40u;
+        l4len = orc_be16(p + 4);
+        tot   = (uint16_t)(40u + l4len);
+        proto = p[6];
+        memcpy(pseudo, p + 8, 32);
+        pseudo[32] = 0u; pseudo[33] = 0u; pseudo[34] = (uint8_t)(l4len >> 8); pseudo[35] = (uint8_t)l4len;
+        pseudo[36] = 0u; pseudo[37] = 0u; pseudo[38] = 0u; pseudo[39] = proto;
+        plen  = 40u;
+        f     = 1u;
+    } else {
+        hlen  = (uint16_t)((p[0] & 0x0Fu) * 4u);
+        tot   = orc_be16(p + 2);
+        proto = p[9];
+        l4len = (uint16_t)(tot - hlen);
+        if (tx) {
+            p[10] = 0u; p[11] = 0u;
+            c = Oracle_HdrCalc(p, hlen, &err, 0);
+            memcpy(p + 10, &c, 2);
+            f = 1u;
+        } else {
+            f = Oracle_HdrVerify(p, hlen, &err, 0) ? 1u : 0u;
+        }
+        memcpy(pseudo, p + 12, 8);
+        pseudo[8] = 0u; pseudo[9] = proto; pseudo[10] = (uint8_t)(l4len >> 8); pseudo[11] = (uint8_t)l4len;
+        plen  = 12u;
+    }
+    if (tot <= avail && (proto == 6u || proto == 17u)) {
+        uint16_t fo = (uint16_t)(hlen + (proto == 6u ? 16u : 6u));
+        buf.Hdr.NextBufPtr      = NULL;
+        buf.Hdr.ProtocolHdrType = (proto == 6u) ? (v6 ? NET_PROTOCOL_TYPE_TCP_V6 : NET_PROTOCOL_TYPE_TCP_V4)
+                                                : (v6 ? NET_PROTOCOL_TYPE_UDP_V6 : NET_PROTOCOL_TYPE_UDP_V4);
+        buf.Hdr.TransportHdrIx  = hlen;
+        buf.Hdr.TransportHdrLen = 0u;
+        buf.Hdr.DataLen         = l4len;
+        buf.DataPtr             = p;
+        if (tx) {
+            p[fo] = 0u; p[fo + 1u] = 0u;
+            c = Oracle_DataCalc(&buf, pseudo, plen, &err, 0);
+            if (proto == 17u && c == 0u) c = 0xFFFFu;
+            memcpy(p + fo, &c, 2);
+            f |= 6u;
+        } else if (proto == 6u || orc_be16(p + fo) != 0u) {
+            f |= (uint8_t)(4u | (Oracle_DataVerify(&buf, pseudo, plen, &err, 0) ? 2u : 0u));
+        }
+    }
+    *flag = f;
+}
+
+void Oracle_PktBatch(uint8_t *base, uint64_t stride, uint16_t avail, uint32_t n, int tx, uint8_t *flags,
+                     int n_threads)
+{
+    int64_t i;
+#ifdef _OPENMP
+    int nt = (n_threads > 0) ? n_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nt)
+#else
+    (void)n_threads;
+#endif
+    for (i = 0; i < (int64_t)n; ++i) {
+        orc_one_datagram(base + (uint64_t)i * stride, avail, tx, &flags[i]);
+    }
+}
+
 uint32_t Oracle_C1Loop(const void *pdata_buf, const void *ppseudo_hdr, uint16_t pseudo_hdr_size,
                        const void *ip_hdr, uint64_t iters)
 {

@@ -66,6 +66,12 @@ void Oracle_Fill(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t s
 void Oracle_FillParallel(uint8_t *buf, uint64_t first_byte, uint64_t n_bytes, uint64_t seed, int pattern,
                          int n_threads, uint64_t unit);
 
+/* The stack's per-datagram Rx (tx = 0: HdrVerify + DataVerify) or Tx (tx = 1: HdrCalc + DataCalc
+ * written in place) checksum sequence over a strided batch of well-formed IPv4 / IPv6 (no extension
+ * header) datagrams, OpenMP static: the CPU line of the fused packet rows (net_util_oracle.c). */
+void Oracle_PktBatch(uint8_t *base, uint64_t stride, uint16_t avail, uint32_t n, int tx, uint8_t *flags,
+                     int n_threads);
+
 /* Config C1 (BASELINE configs[0]) per-datagram checksum sequence of the loopback UDP echo
  * (SURVEY §3.1/§3.2), `iters` times on the same NET_BUF: Tx DataCalc(pbuf, pseudo, plen)
  * (net_udp.c:2891) -> HdrCalc(ip_hdr, 20) (net_ipv4.c:9578) -> Rx HdrVerify(ip_hdr, 20)

@@ -89,6 +89,8 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.Oracle_Reflect32.restype = u32
     L.Oracle_CRC32Batch.argtypes = [vp, vp, vp, u64, u32, u32, vp, i32]
     L.Oracle_CRC32Batch.restype = None
+    L.Oracle_PktBatch.argtypes = [vp, u64, u16, u32, i32, vp, i32]
+    L.Oracle_PktBatch.restype = None
     L.Oracle_MaxThreads.argtypes = []
     L.Oracle_MaxThreads.restype = i32
     return L
@@ -224,3 +226,11 @@ def crc32_batch(base: np.ndarray, n: int, cpl: bool, stride: int = 0, length: in
     lib().Oracle_CRC32Batch(base.ctypes.data, None if o is None else o.ctypes.data,
                             None if ln is None else ln.ctypes.data, stride, length, n, out.ctypes.data, int(cpl))
     return out
+
+
+def pkt_batch(base: np.ndarray, stride: int, avail: int, n: int, tx: bool, n_threads: int = 1) -> np.ndarray:
+    """The stack's per-datagram Rx / Tx checksum sequence over a strided batch (Oracle_PktBatch; Tx
+    writes the fields into `base`): flags bit 0 IP OK, bit 1 transport OK, bit 2 transport checked."""
+    flags = np.zeros(n, np.uint8)
+    lib().Oracle_PktBatch(base.ctypes.data, stride, avail, n, int(bool(tx)), flags.ctypes.data, n_threads)
+    return flags

@@ -3,8 +3,9 @@
 default launch policy and a CPU baseline beside each (the oracle's C restatement of net_util.c, -O2,
 OpenMP over the host CPUs bench.py uses, data first-touched by the workers, on a bounded sample),
 the packet batches (fused Rx, Tx on packed and on NET_BUF-shaped buffers, the offload-seam bursts),
-the host-memory (PCIe-inclusive) rates of C2, C4 and the bursts, and the per-packet drop-in latency.
-Every measured batch is spot-checked against the oracle."""
+the host-memory (PCIe-inclusive) rates of C2, C4 and the bursts, the per-packet drop-in latency, and
+the CPU lines of the packet and chain rows (the stack's per-datagram checksum calls in the C
+restatement). Every measured batch is spot-checked against the oracle."""
 import json
 import os
 import statistics
@@ -50,6 +51,53 @@ def events_ms(fn, st, reps=20, warm=3, warm_s=0.1):
         b.record(st)
     torch.cuda.synchronize()
     return statistics.median(a.elapsed_time(b) for a, b in ev)
+
+
+def packet_cpu_lines(threads):
+    """CPU lines of the packet and chain rows: the C restatement's per-datagram sequence
+    (Oracle_PktBatch: HdrVerify + DataVerify on Rx, HdrCalc + DataCalc written on Tx) over a 256 Ki x
+    1500-B sample of the same datagrams (IPv4/TCP, IPv6/TCP, alternating), and the per-chain
+    DataCalc over 2 Ki of the 64 KiB chains; data first-touched by the OpenMP workers, GiB/s of
+    datagram / payload bytes, all host threads and one."""
+    ns, L = 1 << 18, 1500
+    buf = oracle.fill_parallel(0, ns * L, SEED, 0, n_threads=threads, unit=L)
+    v = buf.reshape(ns, L)
+    h4 = np.array([0x45, 0, L >> 8, L & 0xFF, 0, 0, 0x40, 0, 64, 6, 0, 0], np.uint8)
+    h6 = np.array([0x60, 0, 0, 0, (L - 40) >> 8, (L - 40) & 0xFF, 6, 64], np.uint8)
+    res = {"threads": threads, "kind": "port (oracle/net_util_oracle.c -O2: the stack's per-datagram checksum "
+           "calls, Oracle_PktBatch / Oracle_BatchChains)", "sample": f"{ns} x {L}-B datagrams (393 MB), "
+           "first-touched by the workers; chains: 2048 x 45 fragments"}
+    for tag, setup in (("ipv4", lambda: v.__setitem__((slice(None), slice(0, 12)), h4)),
+                       ("ipv6", lambda: v.__setitem__((slice(None), slice(0, 8)), h6)),
+                       ("mixed", lambda: (v.__setitem__((slice(None), slice(0, 8)), h6),
+                                          v.__setitem__((slice(0, None, 2), slice(0, 12)), h4)))):
+        setup()
+        oracle.pkt_batch(buf, L, L, ns, True, n_threads=threads)             # valid checksums
+        ok = bool((oracle.pkt_batch(buf, L, L, ns, False, n_threads=threads) == 7).all())
+        for t in (threads, 1):
+            sfx = "" if t > 1 else "_1thread"
+            res[f"{tag}_rx_GiB_per_s{sfx}"] = cpu_rate(lambda: oracle.pkt_batch(buf, L, L, ns, False, n_threads=t),
+                                                      ns * L, seconds=2.0 if t > 1 else 1.0)
+            res[f"{tag}_tx_GiB_per_s{sfx}"] = cpu_rate(lambda: oracle.pkt_batch(buf, L, L, ns, True, n_threads=t),
+                                                      ns * L, seconds=2.0 if t > 1 else 1.0)
+        res[f"{tag}_all_valid"] = ok
+    del buf, v
+    nc, per, B = 1 << 11, 45, 2048
+    plen = np.full(per, 1480, np.uint16)
+    plen[-1] = 65515 - 1480 * (per - 1) - 8
+    lens = np.tile(plen, nc)
+    offs = (np.arange(nc * per, dtype=np.uint64) * B + 42).astype(np.uint64)
+    first = (np.arange(nc + 1, dtype=np.uint64) * per).astype(np.uint32)
+    cb = oracle.fill_parallel(0, nc * per * B, SEED, 0, n_threads=threads, unit=per * B)
+    ph = np.zeros((nc, 12), np.uint8)
+    ph[:, 9] = 17
+    ph = ph.reshape(-1)
+    pay = int(lens.astype(np.int64).sum()) + 12 * nc
+    for t in (threads, 1):
+        res["chains_GiB_per_s" + ("" if t > 1 else "_1thread")] = cpu_rate(
+            lambda: oracle.batch_chains(cb, offs, lens, first, ph, 12, 12, nc, 0, n_threads=t), pay,
+            seconds=2.0 if t > 1 else 1.0)
+    return res
 
 
 def main():
@@ -332,6 +380,7 @@ def main():
                                      "kernel": kf},
                     "macs_6B": {"n": nm, "ms": round(ms_m, 4), "G_per_s": round(nm / ms_m / 1e6, 2),
                                 "GB_per_s": round(nm * 10 / ms_m / 1e6, 1), "kernel": netcsum.last_launch()}}
+    out["cpu_packet_rows"] = packet_cpu_lines(host_cpus()[0])
     print(json.dumps(out))
 
 
