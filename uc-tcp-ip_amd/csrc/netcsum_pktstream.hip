@@ -415,6 +415,43 @@ __device__ __forceinline__ void store_fields_sectors(uint8_t* p, bool w1, uint32
     }
 }
 
+// One-pass form of the same: the 128 B [cb, cb + 128) from the 64-B boundary at or below the IP field
+// (+10) were captured by the prologue into `cap` (chunk c at cap[c * cs]); the fields inside it are patched and the 64-B
+// sector(s) holding them stored whole; a field outside it, or a sector that would begin before the
+// batch (the first datagram's bytes below `base` belong to the caller), keeps its 2-B store.
+__device__ __forceinline__ void store_fields_captured(uint8_t* p, const uint8_t* base, const u32x4* cap, uint32_t cs,
+                                                      bool w1, uint32_t v1, bool w2, uint32_t f2, uint32_t v2) {
+    const uintptr_t pa = (uintptr_t)p, cb = (pa + 10u) & ~(uintptr_t)63u;
+    const bool okb = cb >= (uintptr_t)base;
+    const uintptr_t a1 = pa + 10u, a2 = pa + f2;
+    const bool in1 = w1 && okb;                                  // [a1, a1 + 2) is inside [cb, cb + 128)
+    const bool in2 = w2 && okb && a2 >= cb && a2 + 2u <= cb + 128u;
+    if (w1 && !in1) {
+        store_field(p + 10, v1);
+    }
+    if (w2 && !in2) {
+        store_field(p + f2, v2);
+    }
+#pragma unroll
+    for (int sct = 0; sct < 2; ++sct) {
+        const uintptr_t lo = cb + 64u * (uint32_t)sct, hi = lo + 64u;
+        const bool need = (in1 && a1 + 1u >= lo && a1 < hi) || (in2 && a2 + 1u >= lo && a2 < hi);
+        if (!need) {
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uintptr_t ca = lo + 16u * (uint32_t)k;
+            u32x4 v = cap[(uint32_t)(4 * sct + k) * cs];
+            v = patch_chunk(v, ca, a1, v1, in1);
+            v = patch_chunk(v, ca, a2, v2, in2);
+            *reinterpret_cast<gchunk*>(ca) = v;
+        }
+    }
+}
+
+extern __shared__ u32x4 pkt_cap[];     // one-pass sector write-back: 128 B per packet of each wave's run
+
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
 template <int VER, bool TX>
@@ -470,6 +507,22 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
         h[c] = buf_load16<false>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
+    }
+    if constexpr (TX && !REC) {
+        // whole-sector write-back (one pass): the 128 B from the 64-B boundary at or below the IP
+        // checksum field are captured now, while their lines are in the L2 (the window loads just
+        // issued), by LDS-DMA (no VGPRs held; complete at the stream's final vmcnt(0)), for the
+        // epilogue, which patches the fields and stores the sectors whole. Layout per wave: 8
+        // chunk rows of spw lanes (lane k of row c at + 16 (c spw + k)).
+        if (A.tx_sector && mine) {
+            const uintptr_t cb = ((uintptr_t)A.base + (uint64_t)(s_begin + lane) * A.stride + 10u) & ~(uintptr_t)63u;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                __builtin_amdgcn_global_load_lds(
+                    reinterpret_cast<const __attribute__((address_space(1))) void*>(cb + 16u * (uint32_t)c),
+                    (__attribute__((address_space(3))) void*)&pkt_cap[(w * 8u + (uint32_t)c) * spw], 16, 0, 0);
+            }
+        }
     }
     uint32_t wd[24];
 #pragma unroll
@@ -604,7 +657,8 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     if constexpr (TX) {
         uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)idx * A.stride;
         if (A.tx_sector) {
-            store_fields_sectors<1>(p, cip != ~0u, 10u, cip, cl4 != ~0u, pk.l4_csum_off, cl4, 0u);
+            store_fields_captured(p, A.base, &pkt_cap[w * 8u * spw + lane], spw, cip != ~0u, cip, cl4 != ~0u,
+                                  pk.l4_csum_off, cl4);
         } else {
             if (cip != ~0u) {
                 store_field(p + 10, cip);
@@ -759,7 +813,9 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         e = launch_scatter(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+    const uint32_t cap = (TX && a.tx_sector) ? 4u * spw * 128u : 0u;      // sector capture, 4 waves
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256),
+                       std::max(stream_lds_bytes(0), cap), s, a, spw, rec);
     hipError_t e = hipGetLastError();
     return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }
