@@ -638,14 +638,9 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_HDR_BURST     = 19,  /* header stream kernel (C3): 1 = a run's results gathered in LDS
                                          and written as whole 16-B pieces, 0 = one store per piece,
                                          -1 = the default                                             */
-    NETCSUM_TUNE_VARLEN_RUN_BYTES = 20,/* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
+    NETCSUM_TUNE_VARLEN_RUN_BYTES = 20 /* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
                                          run length chosen on the device from sampled lengths; 0 =
                                          runs of 8 segments; -1 = the default (16 KiB)                 */
-    NETCSUM_TUNE_TX_SECTOR     = 21   /* run-stream Tx finalize (strided batches of >= 256-B datagrams):
-                                         0 auto, 1 checksum fields written as 2-B stores, 2 the 64-B
-                                         sectors holding them loaded, patched and written whole (the
-                                         other 62 bytes of a sector are rewritten with their values);
-                                         takes precedence over TX_FLUSH 1 / 2                       */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -110,8 +110,7 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(22, 0) == 219                                 # no such key
-    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_SECTOR, 3) == 219             # 0, 1 or 2
+    assert L.NetUtil_MI355X_Tune(21, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_VARLEN_RUN_BYTES, -2) == 219     # -1 .. 2^20
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_HDR_BURST, 2) == 219             # 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CRC_KERNEL, 4) == 219            # 0..3

@@ -32,7 +32,6 @@ def _defaults():
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
         netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
         netcsum.tune(netcsum.TUNE_TX_FLUSH, -1)
-        netcsum.tune(netcsum.TUNE_TX_SECTOR, 0)
     reset()
     yield
     reset()
@@ -102,13 +101,8 @@ SHAPES = [(1500, 1500), (1514, 1514), (1540, 1514), (1501, 1500), (64, 64), (100
 @pytest.mark.parametrize("stride,pkt_len", SHAPES)
 @pytest.mark.parametrize("lead", [0, 1, 6])
 @pytest.mark.parametrize("passes", [1, 2])
-@pytest.mark.parametrize("sector", [1, 2])
-def test_pkt_stream_vs_oracle(stride, pkt_len, lead, passes, sector):
-    """sector 2 (NETCSUM_TUNE_TX_SECTOR): the 32-B sectors holding the fields are rewritten whole —
-    every other byte must still equal the oracle's (including odd addresses, where a field can
-    straddle two sectors, and datagrams < 256 B, which keep 2-B stores)."""
+def test_pkt_stream_vs_oracle(stride, pkt_len, lead, passes):
     netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
-    netcsum.tune(netcsum.TUNE_TX_SECTOR, sector)
     rng = random.Random(stride * 131 + pkt_len * 7 + lead)
     n = 700 if stride < 5000 else 200
     udp_tx_csum = lead != 6
@@ -235,15 +229,13 @@ def _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver):
                                             (577, 577), (9000, 9000)])
 @pytest.mark.parametrize("lead", [0, 1, 6, 13])
 @pytest.mark.parametrize("passes", [1, 2])
-@pytest.mark.parametrize("sector", [1, 2])
-def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes, sector):
+def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     """Every IPv6 kind (TCP / UDP / UDP without checksum, ICMPv6 echo / error / NDP / other types,
     extension-header chains inside and beyond the lane's window, Hop-by-Hop after the first, Fragment,
     opaque extension headers, malformed versions / lengths, corrupted bytes), alone (VER 6) or mixed
     with every IPv4 kind (VER 0), Rx verdicts and Tx bytes + verdicts against the oracle (chains past
-    the lane's 96-B prologue finished by the walk pass); both field write-back forms."""
+    the lane's 96-B prologue finished by the walk pass)."""
     netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
-    netcsum.tune(netcsum.TUNE_TX_SECTOR, sector)
     rng = random.Random(ver * 1000 + stride * 7 + pkt_len + lead * 131 + passes)
     n = 600 if stride < 5000 else 150
     udp_tx_csum = lead != 6

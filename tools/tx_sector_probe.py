@@ -5,6 +5,13 @@
 interleaved passes. Every form's bytes are compared with the default form's (same input each time).
 
   python tools/tx_sector_probe.py > gpurun_out/TAG_tx_sector_probe.jsonl
+
+Experiment record: NETCSUM_TUNE_TX_SECTOR existed only in the experiment builds of commits 9306138
+(32-B sectors) and 9841321 (64-B sectors, one-pass capture by LDS-DMA = box r4e; the r4c build — the
+two-pass 4-lane scatter loading its sectors, one-pass reload — and the r4d build — one-pass capture in
+VGPRs — differ from it only in the one-pass path); every form was slower than
+the 2-B field stores (profiles/r3s_tx_sector32_probe.jsonl, r3s_tx_sector64_probe.jsonl) and the
+option was removed from the product. Run it against one of those builds.
 """
 import json
 import os

@@ -34,7 +34,6 @@ thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read 
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
-thread_local netcsum::TuneKnob g_tune_tx_sector{0};             // run-stream Tx: 0 auto, 1 2-B field stores, 2 sectors
 std::atomic<int> g_err_reports{0};
 
 NET_ERR dev_fail(const char* what, hipError_t e) {
@@ -945,13 +944,9 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
         const bool two = tx && g_tune_tx_passes.load() != 1;
-        // whole-sector field write-back (netcsum_pktstream.hip store_fields_sectors): only where no two
-        // datagrams' fields can share a 64-B sector
-        a.tx_sector = (tx && g_tune_tx_sector.load() == 2 && a.len_u >= netcsum::kTxSectorMinLen) ? 1u : 0u;
-        char desc[160];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s%s", d, snt ? ",nt" : "",
-                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw,
-                 a.tx_sector ? " sector64" : "", two ? (a.tx_sector ? " +pkt_scatter_sector_kernel" : " +pkt_scatter_kernel") : "",
+        char desc[136];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s", d, snt ? ",nt" : "",
+                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
                  walk ? " +pkt_v6_walk_kernel" : "");
         netcsum::set_last_launch(desc);
         // scratch: [deferral word (IPv6 / mixed), 256 B | records (two-pass Tx) | flags (own_flags)]
@@ -1366,10 +1361,6 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_TX_PASSES:
         if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_tx_passes.store(value);
-        return NET_UTIL_ERR_NONE;
-    case NETCSUM_TUNE_TX_SECTOR:
-        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
-        g_tune_tx_sector.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_STREAM_WAVES:
         if (value != -1 && value != 0 && (value < 3 || value > 8)) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

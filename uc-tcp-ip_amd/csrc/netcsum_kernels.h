@@ -75,10 +75,7 @@ struct PktBatchArgs {
     uint32_t        xcd;           // run-stream form: XCD-aware block order (set by the launcher)
     uint32_t*       fieldpos_out;  // Tx (optional): per packet, which checksum fields were written —
                                    // kFieldIP | kFieldL4 | transport field offset (host-memory forms)
-    uint32_t        tx_sector;     // run-stream Tx: fields written as whole 32-B sectors (set by the
-                                   // launcher: strided batches of >= kTxSectorMinLen-B datagrams)
 };
-constexpr uint32_t kTxSectorMinLen = 256u;   // no two datagrams' checksum fields share a 32-B sector
 constexpr uint32_t kFieldIP = 1u << 31;    // fieldpos_out: the IPv4 header checksum field (+10) written
 constexpr uint32_t kFieldL4 = 1u << 30;    // fieldpos_out: the transport field at (bits 0-15) written
 // One 8-B record per packet of a host-memory Tx batch (pkt_field_gather_kernel): the written field

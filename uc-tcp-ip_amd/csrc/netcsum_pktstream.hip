@@ -345,113 +345,6 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memc
     q[1] = (uint8_t)(v >> 8);
 }
 
-// Sector write-back (PktBatchArgs::tx_sector): the aligned 64-B sector(s) holding a datagram's checksum
-// fields are loaded, the fields patched in registers and the sectors stored WHOLE. HBM is written in
-// 64-B units: a 2-B store (or a whole 32-B one) leaves a partially written 64-B sector dirty in the L2,
-// and its write-back is a read-modify-write; a whole 64-B sector is a plain write
-// (tools/tx_wb_probe.hip, profiles/r3s_tx_wb_probe.jsonl: 1 M scattered field pairs cost 84 us of HBM
-// time as 2-B stores, 75 us as whole 32-B sectors, 48 us as whole 64-B sectors). The other 62 bytes of
-// a sector are written back with the values just loaded, so the launcher enables this only where no
-// other datagram's field can share a sector (strided batches of >= kTxSectorMinLen-B datagrams, fields
-// within the first 96 B) and only for fields that do not cross a sector boundary (a field at an
-// address = 63 mod 64 keeps its 2-B store).
-__device__ __forceinline__ u32x4 patch_chunk(u32x4 x, uintptr_t c, uintptr_t a, uint32_t v, bool on) {
-    uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (uint32_t j = 0; j < 2u; ++j) {
-        const uintptr_t b = a + j;
-        const bool in = on && b >= c && b < c + 16u;
-        const uint32_t o = (uint32_t)(b - c) & 15u, sh = (o & 3u) * 8u, di = o >> 2;
-        const uint32_t byte = (v >> (8u * j)) & 0xFFu;
-#pragma unroll
-        for (uint32_t d = 0; d < 4u; ++d) {
-            w[d] = (in && di == d) ? ((w[d] & ~(0xFFu << sh)) | (byte << sh)) : w[d];
-        }
-    }
-    return u32x4{w[0], w[1], w[2], w[3]};
-}
-
-typedef __attribute__((address_space(1))) u32x4 gchunk;
-
-// The sectors of one datagram's fields, written by `lanes` lanes (1: this lane does all 4 chunks of a
-// sector; 4: lane `sub` does chunk `sub`). Fields: (p + f1, v1) if w1, (p + f2, v2) if w2.
-template <int LANES>
-__device__ __forceinline__ void store_fields_sectors(uint8_t* p, bool w1, uint32_t f1, uint32_t v1, bool w2,
-                                                     uint32_t f2, uint32_t v2, uint32_t sub) {
-    const uintptr_t a1 = (uintptr_t)p + f1, a2 = (uintptr_t)p + f2;
-    const bool s1 = w1 && (a1 & 63u) != 63u, s2 = w2 && (a2 & 63u) != 63u;
-    if (sub == 0u) {
-        if (w1 && !s1) {
-            store_field(p + f1, v1);
-        }
-        if (w2 && !s2) {
-            store_field(p + f2, v2);
-        }
-    }
-    const uintptr_t b1 = a1 & ~(uintptr_t)63u, b2 = a2 & ~(uintptr_t)63u;
-    const bool two = s1 && s2 && b1 != b2;
-    const uintptr_t bA = s1 ? b1 : b2;                       // first sector (field 1's, else field 2's)
-    if (!(s1 || s2)) {
-        return;
-    }
-    constexpr int K = 4 / LANES;                              // chunks per lane per sector
-    u32x4 x[K], y[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t c = (uint32_t)k * LANES + sub;
-        x[k] = *reinterpret_cast<gchunk*>(bA + 16u * c);
-        y[k] = two ? *reinterpret_cast<gchunk*>(b2 + 16u * c) : x[k];
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t c = (uint32_t)k * LANES + sub;
-        const uintptr_t ca = bA + 16u * c, cb = b2 + 16u * c;
-        u32x4 v = patch_chunk(x[k], ca, a1, v1, s1);
-        v = patch_chunk(v, ca, a2, v2, s2);
-        *reinterpret_cast<gchunk*>(ca) = v;
-        if (two) {
-            *reinterpret_cast<gchunk*>(cb) = patch_chunk(y[k], cb, a2, v2, true);
-        }
-    }
-}
-
-// One-pass form of the same: the 128 B [cb, cb + 128) from the 64-B boundary at or below the IP field
-// (+10) were captured by the prologue into `cap` (chunk c at cap[c * cs]); the fields inside it are patched and the 64-B
-// sector(s) holding them stored whole; a field outside it, or a sector that would begin before the
-// batch (the first datagram's bytes below `base` belong to the caller), keeps its 2-B store.
-__device__ __forceinline__ void store_fields_captured(uint8_t* p, const uint8_t* base, const u32x4* cap, uint32_t cs,
-                                                      bool w1, uint32_t v1, bool w2, uint32_t f2, uint32_t v2) {
-    const uintptr_t pa = (uintptr_t)p, cb = (pa + 10u) & ~(uintptr_t)63u;
-    const bool okb = cb >= (uintptr_t)base;
-    const uintptr_t a1 = pa + 10u, a2 = pa + f2;
-    const bool in1 = w1 && okb;                                  // [a1, a1 + 2) is inside [cb, cb + 128)
-    const bool in2 = w2 && okb && a2 >= cb && a2 + 2u <= cb + 128u;
-    if (w1 && !in1) {
-        store_field(p + 10, v1);
-    }
-    if (w2 && !in2) {
-        store_field(p + f2, v2);
-    }
-#pragma unroll
-    for (int sct = 0; sct < 2; ++sct) {
-        const uintptr_t lo = cb + 64u * (uint32_t)sct, hi = lo + 64u;
-        const bool need = (in1 && a1 + 1u >= lo && a1 < hi) || (in2 && a2 + 1u >= lo && a2 < hi);
-        if (!need) {
-            continue;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uintptr_t ca = lo + 16u * (uint32_t)k;
-            u32x4 v = cap[(uint32_t)(4 * sct + k) * cs];
-            v = patch_chunk(v, ca, a1, v1, in1);
-            v = patch_chunk(v, ca, a2, v2, in2);
-            *reinterpret_cast<gchunk*>(ca) = v;
-        }
-    }
-}
-
-extern __shared__ u32x4 pkt_cap[];     // one-pass sector write-back: 128 B per packet of each wave's run
-
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
 template <int VER, bool TX>
@@ -507,22 +400,6 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
         h[c] = buf_load16<false>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
-    }
-    if constexpr (TX && !REC) {
-        // whole-sector write-back (one pass): the 128 B from the 64-B boundary at or below the IP
-        // checksum field are captured now, while their lines are in the L2 (the window loads just
-        // issued), by LDS-DMA (no VGPRs held; complete at the stream's final vmcnt(0)), for the
-        // epilogue, which patches the fields and stores the sectors whole. Layout per wave: 8
-        // chunk rows of spw lanes (lane k of row c at + 16 (c spw + k)).
-        if (A.tx_sector && mine) {
-            const uintptr_t cb = ((uintptr_t)A.base + (uint64_t)(s_begin + lane) * A.stride + 10u) & ~(uintptr_t)63u;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                __builtin_amdgcn_global_load_lds(
-                    reinterpret_cast<const __attribute__((address_space(1))) void*>(cb + 16u * (uint32_t)c),
-                    (__attribute__((address_space(3))) void*)&pkt_cap[(w * 8u + (uint32_t)c) * spw], 16, 0, 0);
-            }
-        }
     }
     uint32_t wd[24];
 #pragma unroll
@@ -656,16 +533,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     }
     if constexpr (TX) {
         uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)idx * A.stride;
-        if (A.tx_sector) {
-            store_fields_captured(p, A.base, &pkt_cap[w * 8u * spw + lane], spw, cip != ~0u, cip, cl4 != ~0u,
-                                  pk.l4_csum_off, cl4);
-        } else {
-            if (cip != ~0u) {
-                store_field(p + 10, cip);
-            }
-            if (cl4 != ~0u) {
-                store_field(p + pk.l4_csum_off, cl4);
-            }
+        if (cip != ~0u) {
+            store_field(p + 10, cip);
+        }
+        if (cl4 != ~0u) {
+            store_field(p + pk.l4_csum_off, cl4);
         }
         if (A.fieldpos_out) {
             A.fieldpos_out[idx] = (cip != ~0u ? kFieldIP : 0u) | (cl4 != ~0u ? kFieldL4 | (pk.l4_csum_off & 0xFFFFu) : 0u);
@@ -715,29 +587,6 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
     }
 }
 
-// The same pass with whole 64-B sector write-back (PktBatchArgs::tx_sector): four lanes per packet,
-// lane `sub` loads, patches and stores chunk `sub` of each sector holding a field.
-__global__ void __launch_bounds__(256) pkt_scatter_sector_kernel(PktBatchArgs A, const PktTxRecord* rec) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    const uint32_t i = (uint32_t)(t >> 2), sub = (uint32_t)t & 3u;
-    if (i >= A.n) {
-        return;
-    }
-    const uint64_t r = reinterpret_cast<const uint64_t*>(rec)[i];
-    const uint32_t vals = (uint32_t)r, l4_off = (uint32_t)(r >> 32) & 0xFFFFu;
-    const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
-    if (sub == 0u) {
-        if (A.flags_out) {
-            A.flags_out[i] = (uint8_t)flags;
-        }
-        if (A.fieldpos_out) {
-            A.fieldpos_out[i] = ((store & 1u) ? kFieldIP : 0u) | ((store & 2u) ? kFieldL4 | l4_off : 0u);
-        }
-    }
-    uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
-    store_fields_sectors<4>(p, (store & 1u) != 0u, 10u, vals & 0xFFFFu, (store & 2u) != 0u, l4_off, vals >> 16, sub);
-}
-
 // Host-memory Tx forms (netcsum_abi.hip pkt_host): one 8-B record per packet of the checksum fields
 // the Tx kernels wrote into the device copy (fieldpos_out), so that only 8 B per packet return over
 // PCIe instead of the chunk's bytes; the host writes the fields into its own buffer.
@@ -776,9 +625,7 @@ int tx_flush_mode() {
 hipError_t launch_scatter(const PktBatchArgs& a, const PktTxRecord* rec, hipStream_t s) {
     const int m = tx_flush_mode();
     const dim3 g((a.n + 255u) / 256u), b(256);
-    if (a.tx_sector) {
-        hipLaunchKernelGGL(pkt_scatter_sector_kernel, dim3((unsigned)(((uint64_t)a.n * 4u + 255u) / 256u)), b, 0, s, a, rec);
-    } else if (m == 1) {
+    if (m == 1) {
         hipLaunchKernelGGL((pkt_scatter_kernel<true, false>), g, b, 0, s, a, rec);
     } else if (m == 2) {
         hipLaunchKernelGGL((pkt_scatter_kernel<false, true>), g, b, 0, s, a, rec);
@@ -813,9 +660,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         e = launch_scatter(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
-    const uint32_t cap = (TX && a.tx_sector) ? 4u * spw * 128u : 0u;      // sector capture, 4 waves
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256),
-                       std::max(stream_lds_bytes(0), cap), s, a, spw, rec);
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
     hipError_t e = hipGetLastError();
     return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }

@@ -68,7 +68,6 @@ TUNE_CRC_LANES = 17
 TUNE_CRC_WIDE = 18
 TUNE_HDR_BURST = 19
 TUNE_VARLEN_RUN_BYTES = 20
-TUNE_TX_SECTOR = 21
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
