@@ -31,6 +31,14 @@ for l in open('$O/${T}_tx_sector_probe.jsonl'):
     if l.startswith('{'):
         r=json.loads(l); print({k:v for k,v in r.items() if k!='kernel'})
 " ;;
+  frag)
+    timeout -k 10 300 python -u tools/frag_stream_probe.py > $O/${T}_frag_stream_probe.jsonl 2>&1 || { tail -5 $O/${T}_frag_stream_probe.jsonl; exit 1; }
+    python3 -c "
+import json
+for l in open('$O/${T}_frag_stream_probe.jsonl'):
+    if l.startswith('{'):
+        r=json.loads(l); print({k:v for k,v in r.items() if not k.startswith('kernel')})
+" ;;
   pitch)
     timeout -k 10 300 python -u tools/pitch_probe.py > $O/${T}_pitch_probe.jsonl 2>&1 || { tail -5 $O/${T}_pitch_probe.jsonl; exit 1; }
     python3 -c "
