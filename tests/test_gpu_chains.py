@@ -1,6 +1,9 @@
 """GPU parity of the batched NET_BUF chain checksums (NetUtil_MI355X_ChkSumBatchChains) against the C
 oracle walking the same pieces as NET_BUF chains (net_util.c:1545-1687), bit-exact, over every
-group width, scattered odd-offset pieces, empty pieces, NULL chains, odd pseudo-headers, u32 wrap."""
+group width, scattered odd-offset pieces, empty pieces, NULL chains, odd pseudo-headers, u32 wrap,
+for the default two-pass form (per-piece sums, then a combine pass per chain), the wave-per-chain form
+(NETCSUM_TUNE_KERNEL 1) and the two-pass form's fallback for batches with more pieces than its
+records hold."""
 import random
 
 import numpy as np
@@ -19,9 +22,11 @@ DEV = "cuda"
 def _defaults():
     netcsum.tune(netcsum.TUNE_GROUP_LANES, 0)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
+    netcsum.tune(netcsum.TUNE_KERNEL, 0)
     yield
     netcsum.tune(netcsum.TUNE_GROUP_LANES, 0)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
+    netcsum.tune(netcsum.TUNE_KERNEL, 0)
 
 
 def _dev(a, dtype):
@@ -47,14 +52,19 @@ def _want(cb, op):
                                cb.pseudo_len, cb.n, op)
 
 
-@pytest.mark.parametrize("group", [0, 16, 32, 64])
+@pytest.mark.parametrize("group", [0, 1, 16, 32, 64])           # 1: the wave-per-chain form (KERNEL 1)
 @pytest.mark.parametrize("pseudo_len", [0, 12, 13, 40])
 @pytest.mark.parametrize("op", [0, 1])
 def test_chain_batch_matches_oracle(group, pseudo_len, op):
     rng = random.Random(group * 131 + pseudo_len * 3 + op)
     cb = make_chain_batch(rng, 1500, pseudo_len=pseudo_len, self_verify=0.5 if op else 0.0)
-    netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
+    if group == 1:
+        netcsum.tune(netcsum.TUNE_KERNEL, 1)
+    else:
+        netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     got, want = _gpu(cb, op), _want(cb, op)
+    assert netcsum.last_launch().startswith("chain_wave_kernel" if group == 1 else "chain_batch_kernel" if group
+                                            else "chain_piece_kernel"), netcsum.last_launch()
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:5]]
     if op:
@@ -62,18 +72,63 @@ def test_chain_batch_matches_oracle(group, pseudo_len, op):
 
 
 @pytest.mark.parametrize("grid", [1, 3, 0])
-def test_chain_batch_grid_stride_and_long_chains(grid):
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_chain_batch_grid_stride_and_long_chains(grid, kernel):
     rng = random.Random(100 + grid)
     cb = make_chain_batch(rng, 3000, max_pieces=45, max_piece=1480, pseudo_len=12)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, grid)
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
     assert np.array_equal(_gpu(cb, 0), _want(cb, 0))
 
 
-def test_chain_batch_u32_wrap():
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_chain_batch_u32_wrap(kernel):
+    netcsum.tune(netcsum.TUNE_KERNEL, kernel)
     rng = random.Random(5)
     cb = make_chain_batch(rng, 64, wrap_chains=32, pseudo_len=13)
     assert np.array_equal(_gpu(cb, 0), _want(cb, 0))
     assert np.array_equal(_gpu(cb, 1), _want(cb, 1))
+
+
+@pytest.mark.parametrize("n_pieces", [1, 63, 64, 65, 1000, 4097])
+def test_chain_batch_piece_tiles(n_pieces):
+    """Pass 1's tiles of 64 pieces: piece counts around the tile size, one chain per 7 pieces."""
+    rng = np.random.default_rng(n_pieces)
+    lens = rng.integers(0, 1600, size=n_pieces).astype(np.uint16)
+    offs = np.zeros(n_pieces, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 3, size=n_pieces - 1).astype(np.uint64))
+    base = rng.integers(0, 256, size=int(offs[-1]) + 1700, dtype=np.uint8)
+    first = np.minimum(np.arange(0, n_pieces + 7, 7, dtype=np.uint64), n_pieces).astype(np.uint32)
+    first = np.unique(first)
+    n = len(first) - 1
+    ph = rng.integers(0, 256, size=12 * n, dtype=np.uint8)
+    out = torch.zeros(n, dtype=torch.int16, device=DEV)
+    netcsum.batch_chains(_dev(base, np.uint8), _dev(offs, np.int64), _dev(lens, np.int16), _dev(first, np.int32),
+                         _dev(ph, np.uint8), 12, 12, n, out, op=0, n_pieces=n_pieces)
+    torch.cuda.synchronize()
+    want = oracle.batch_chains(base, offs, lens, first, ph, 12, 12, n, 0)
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+
+
+def test_chain_batch_more_pieces_than_records():
+    """The two-pass form keeps max(2^20, 128 x chains) piece records; a batch of 4 chains with
+    1.2 M pieces (0-5 B each, odd lengths and addresses) is done by its wave-per-chain fallback."""
+    rng = np.random.default_rng(77)
+    per = 300_001
+    n = 4
+    lens = rng.integers(0, 6, size=n * per).astype(np.uint16)
+    offs = np.zeros(n * per, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 1)                # 1-B gaps: scattered parities
+    base = rng.integers(0, 256, size=int(offs[-1]) + 64, dtype=np.uint8)
+    first = (np.arange(n + 1, dtype=np.uint64) * per).astype(np.uint32)
+    ph = rng.integers(0, 256, size=13 * n, dtype=np.uint8)
+    out = torch.zeros(n, dtype=torch.int16, device=DEV)
+    netcsum.batch_chains(_dev(base, np.uint8), _dev(offs, np.int64), _dev(lens, np.int16), _dev(first, np.int32),
+                         _dev(ph, np.uint8), 13, 13, n, out, op=0, n_pieces=n * per)
+    torch.cuda.synchronize()
+    want = oracle.batch_chains(base, offs, lens, first, ph, 13, 13, n, 0)
+    assert netcsum.last_launch().startswith("chain_piece_kernel")
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
 
 
 def test_chain_batch_matches_single_segment_batch():

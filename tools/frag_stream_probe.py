@@ -12,8 +12,14 @@ profiles/r3s_frag_stream_probe.jsonl, by "build": r4f the product library; r4g a
 that form and, with TUNE_KERNEL 1, the wave-per-chain kernel); r4h / r4i the same with the even/odd
 sums taken as byte + half-word sums (v_sad_u8 + v_sad_u16, half the VALU ops); r4j the wave-per-chain
 kernel with its descriptors batch-loaded into VGPRs (64 per vector load, read by v_readlane) instead
-of scalar loads a step ahead. None of the experiment builds was faster (0.195-0.200 ms throughout);
-none was kept.
+of scalar loads a step ahead. None of those was faster (0.195-0.200 ms throughout); none was kept.
+r4k adds the varlen lane-group pipe forced to 16 lanes x 6 chunks (0.165 ms at pitch 2048, tiles of 64
+segments; 0.173 grid-stride). r4l-r4n: the two-pass form rebuilt on that geometry (pass 1 in tiles
+of 64 consecutive pieces, pass 2 a 16-lane group per chain): 0.191-0.197 ms, rocprof 177-180 us +
+5.3 us (profiles/r3s_r4m/r4n_frag_rocprof_kernel_stats.csv) against 197 us for the wave-per-chain
+kernel — the product form since r4n. r4o: pass 1 without the byte sum (timing only, wrong
+results): 178 us, so the VALU of the even/odd split is not what separates it from the segment
+kernel's 169 us.
 """
 import json
 import os
@@ -65,11 +71,27 @@ def main():
             r["varlen_pipe_ms"] = events_ms(lambda: netcsum.batch_varlen(base, off_d, len_d, None, 0, 0, npc, os_,
                                                                          netcsum.OP_DATA_CALC, stream=st), st)
             r["kernel_varlen_pipe"] = netcsum.last_launch()
+            netcsum.tune(netcsum.TUNE_GROUP_LANES, 16)
+            netcsum.tune(netcsum.TUNE_CHUNKS, 6)
+            r["varlen_pipe16_ms"] = events_ms(lambda: netcsum.batch_varlen(base, off_d, len_d, None, 0, 0, npc, os_,
+                                                                           netcsum.OP_DATA_CALC, stream=st), st)
+            r["kernel_varlen_pipe16"] = netcsum.last_launch()
+            netcsum.tune(netcsum.TUNE_TILE, 0)
+            r["varlen_pipe16_t0_ms"] = events_ms(lambda: netcsum.batch_varlen(base, off_d, len_d, None, 0, 0, npc, os_,
+                                                                              netcsum.OP_DATA_CALC, stream=st), st)
+            r["kernel_varlen_pipe16_t0"] = netcsum.last_launch()
+            r["strided_t0_ms"] = events_ms(lambda: netcsum.batch_strided(base[ix:], P, flen, None, 0, 0, npc, os_,
+                                                                         netcsum.OP_DATA_CALC, stream=st), st)
+            r["kernel_strided_t0"] = netcsum.last_launch()
+            netcsum.tune(netcsum.TUNE_TILE, -1)
+            netcsum.tune(netcsum.TUNE_GROUP_LANES, 0)
+            netcsum.tune(netcsum.TUNE_CHUNKS, 0)
             netcsum.tune(netcsum.TUNE_KERNEL, 0)
             r["strided_ms"] = events_ms(lambda: netcsum.batch_strided(base[ix:], P, flen, None, 0, 0, npc, os_,
                                                                       netcsum.OP_DATA_CALC, stream=st), st)
             r["kernel_strided"] = netcsum.last_launch()
-            for k in ("chain", "chain_wave", "varlen", "varlen_pipe", "strided"):
+            for k in ("chain", "chain_wave", "varlen", "varlen_pipe", "varlen_pipe16", "varlen_pipe16_t0", "strided",
+                      "strided_t0"):
                 r[k + "_ms"] = round(r[k + "_ms"], 4)
                 r[k + "_GBps_payload"] = round(payload / r[k + "_ms"] / 1e6, 1)
             print(json.dumps(r), flush=True)

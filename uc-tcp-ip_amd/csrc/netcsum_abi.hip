@@ -1012,10 +1012,24 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
     a.n = n_chains;
     a.verify = (op == NETCSUM_OP_DATA_VERIFY) ? 1u : 0u;
     a.out = d_out;
-    // GROUP_LANES 16/32/64: chain_batch_kernel with that many lanes per chain; otherwise (auto) the
-    // wave-per-chain kernel (4 chains per 256-thread block).
+    // GROUP_LANES 16/32/64: chain_batch_kernel with that many lanes per chain; KERNEL 1: the
+    // wave-per-chain kernel (4 chains per 256-thread block); otherwise (auto) the two-pass form
+    // (per-piece sums in piece order, then a combine pass per chain), its records in this thread's
+    // scratch for this stream: room for max(2^20, 128 x chains) pieces (a batch with more pieces is
+    // done by the wave-per-chain form inside the combine pass).
     int g = g_tune_group.load();
     g = (g == 16 || g == 32 || g == 64) ? g : 0;
+    if (g == 0 && g_tune_kernel.load() != 1) {
+        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 20, 128ull * n_chains), 0xFFFFFFFFull);
+        netcsum::set_last_launch("chain_piece_kernel<G=16,K=6,tile=64,nt> +chain_combine_kernel");
+        ScratchLease scratch;
+        NC_HIP(scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * 8u));
+        NC_HIP(netcsum::launch_chain_two_pass(a, static_cast<uint64_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
+                                              static_cast<hipStream_t>(hip_stream)));
+        NC_HIP(scratch.end());
+        return NET_UTIL_ERR_NONE;
+    }
+    netcsum::set_last_launch(g ? "chain_batch_kernel" : "chain_wave_kernel");
     const uint32_t gpb = g ? 256u / (uint32_t)g : 4u;
     const uint64_t need = ((uint64_t)n_chains + gpb - 1u) / gpb;
     int grid = g_tune_grid.load();

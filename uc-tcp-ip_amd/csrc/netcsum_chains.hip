@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
 
@@ -221,14 +223,13 @@ __device__ __forceinline__ void wave_consume(const WStage& st, int ql, uint64_t&
     if (st.swap) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
 }
 
-__global__ void __launch_bounds__(256) chain_wave_kernel(ChainBatchArgs A) {
+// Chain `ch` (wave-uniform) by the calling wave.
+__device__ __forceinline__ void wave_chain(const ChainBatchArgs& A, uint32_t ch) {
     const int lane = (int)(threadIdx.x & 63u);
     const int ql = lane & (kWQ - 1);
     const int qi = lane >> 4;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * 4u;
     const uintptr_t base = (uintptr_t)A.base;
-    for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += nw) {      // wave-uniform
+    {
         const uint32_t p0 = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + ch));
         const uint32_t p1 = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + ch + 1u));
         uint64_t E = 0u, O = 0u;
@@ -269,7 +270,252 @@ __global__ void __launch_bounds__(256) chain_wave_kernel(ChainBatchArgs A) {
     }
 }
 
+__global__ void __launch_bounds__(256) chain_wave_kernel(ChainBatchArgs A) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * 4u;
+    for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += nw) {      // wave-uniform
+        wave_chain(A, ch);
+    }
+}
+
+// ---- two-pass form (default) --------------------------------------------------------------------
+// The wave-per-chain kernel reads a 64-KiB-datagram batch (16 Ki chains x 45 fragments of 1480 B) in
+// 0.195 ms; the segment kernel in its lane-group form, 16 lanes x 6 chunks per segment, two segments
+// in flight per group, blocks owning tiles of 64 consecutive segments, reads the same fragments as
+// a varlen batch in 0.165 ms (profiles/r3s_frag_stream_probe.jsonl; 0.173 without the tiles). So
+// chain batches take two passes:
+//  1. chain_piece_kernel, that segment form over the batch's pieces in index order: per piece the
+//     exact sums of its bytes at even / odd ADDRESSES (taken as a byte sum and a half-word sum, two
+//     VALU ops per dword) into an 8-B record;
+//  2. chain_combine_kernel, a wave per chain, 64 pieces per step: each piece's stream parity
+//     (pseudo-header length + the lengths before it, mod 2) from a ballot of the odd lengths, the
+//     record swapped where that differs from the address parity, the pseudo-header added, the
+//     exact 64-bit total wrapped to u32 like the reference accumulator and folded (chain_out).
+// The piece count lives on the device (chain_first[n]); the records go to a scratch buffer of `cap`
+// pieces sized by the host from the chain count, and a batch with more pieces than that is done by
+// the combine kernel in the wave-per-chain form (pass 1 then returns at once) — correct, slower.
+constexpr int kPG = 16;    // lanes per piece
+constexpr int kPK = 6;     // 16-B chunks per lane per pass
+constexpr uint32_t kPTile = 4u;   // pieces per group per tile (a block's tile: 64 consecutive pieces)
+
+struct PieceStage {
+    u32x4     v[kPK];
+    uintptr_t a;
+    uint32_t  len;
+};
+
+__device__ __forceinline__ void piece_issue(PieceStage& st, uintptr_t a, uint32_t len, int lane) {
+    st.a = a;
+    st.len = len;
+    const uintptr_t q0 = a & ~(uintptr_t)15;
+    const uint32_t nch = len ? (uint32_t)(((a & 15u) + len + 15u) >> 4) : 0u;
+    const uintptr_t z = zero_addr();
+#pragma unroll
+    for (int k = 0; k < kPK; ++k) {
+        const uint32_t c = (uint32_t)(k * kPG + lane);
+        st.v[k] = load16<true>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : z));
+    }
+}
+
+// Byte sum b and little-endian half-word sum h (= e + 256 o) of this lane's share of the piece.
+__device__ __forceinline__ void piece_consume(const PieceStage& st, int lane, uint32_t& b, uint32_t& h) {
+    const uint32_t lead = (uint32_t)(st.a & 15u);
+    const uint32_t rend = lead + st.len;
+    const uint32_t nch = st.len ? (rend + 15u) >> 4 : 0u;
+    b = 0u;
+    h = 0u;
+    auto add = [&](u32x4 v) {
+        b = __builtin_amdgcn_sad_u8(v.x, 0u, b);
+        h = __builtin_amdgcn_sad_u16(v.x, 0u, h);
+        b = __builtin_amdgcn_sad_u8(v.y, 0u, b);
+        h = __builtin_amdgcn_sad_u16(v.y, 0u, h);
+        b = __builtin_amdgcn_sad_u8(v.z, 0u, b);
+        h = __builtin_amdgcn_sad_u16(v.z, 0u, h);
+        b = __builtin_amdgcn_sad_u8(v.w, 0u, b);
+        h = __builtin_amdgcn_sad_u16(v.w, 0u, h);
+    };
+#pragma unroll
+    for (int k = 0; k < kPK; ++k) {
+        const uint32_t c = (uint32_t)(k * kPG + lane);
+        u32x4 v = opaque(st.v[k]);
+        if (c < nch) {
+            v = edge_mask_rel(v, c, lead, rend);
+        }
+        add(v);
+    }
+    if (nch > (uint32_t)(kPG * kPK)) {                            // pieces longer than one pass
+        const uintptr_t q0 = st.a & ~(uintptr_t)15;
+        for (uint32_t c0 = (uint32_t)(kPG * kPK); c0 < nch; c0 += (uint32_t)(kPG * kPK)) {
+            u32x4 w[kPK];
+#pragma unroll
+            for (int k = 0; k < kPK; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * kPG + lane);
+                w[k] = load16<true>(reinterpret_cast<gu32x4*>((c < nch) ? (q0 + 16u * (uintptr_t)c) : zero_addr()));
+            }
+#pragma unroll
+            for (int k = 0; k < kPK; ++k) {
+                const uint32_t c = c0 + (uint32_t)(k * kPG + lane);
+                u32x4 v = w[k];
+                if (c < nch) {
+                    v = edge_mask_rel(v, c, lead, rend);
+                }
+                add(v);
+            }
+        }
+    }
+}
+
+// Group-reduce (b, h) and store the piece's record (e | o << 32); h - b = 255 o exactly (a piece
+// is < 64 KiB, so o < 2^24), divided by multiplying with 255's inverse mod 2^32.
+__device__ __forceinline__ void piece_store(uint64_t* eo, uint32_t j, uint32_t b, uint32_t h, int lane, bool valid) {
+#pragma unroll
+    for (int m = kPG / 2; m >= 1; m >>= 1) {
+        b += (uint32_t)__shfl_xor((int)b, m, 64);
+        h += (uint32_t)__shfl_xor((int)h, m, 64);
+    }
+    if (valid && lane == 0) {
+        const uint32_t o = (h - b) * 0xFEFEFEFFu;
+        eo[j] = (uint64_t)(b - o) | ((uint64_t)o << 32);
+    }
+}
+
+__global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint64_t* eo, uint32_t cap) {
+    const int lane = (int)(threadIdx.x & (kPG - 1));
+    constexpr uint32_t gpb = 256u / kPG;                          // groups per block
+    constexpr uint32_t tile = gpb * kPTile;                       // pieces per block tile
+    const uint32_t g = threadIdx.x / kPG;
+    const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
+    const uint32_t ntiles = (np + tile - 1u) / tile;
+    if (np > cap) {                                               // no room for the records: this
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // pass does the batch
+        for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += gridDim.x * 4u) {   // in the wave-per-
+            wave_chain(A, ch);                                    // chain form, the combine pass
+        }                                                         // returns at once
+        return;
+    }
+    if (blockIdx.x >= ntiles) {
+        return;
+    }
+    // this block's tiles: blockIdx.x, + gridDim.x, ...; group g takes pieces tile*64 + g + 16 k
+    const uint32_t iters = ((ntiles - blockIdx.x + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
+    auto piece_at = [&](uint32_t i) -> uint32_t {                 // the group's i-th piece
+        return (blockIdx.x + (i / kPTile) * gridDim.x) * tile + g + gpb * (i % kPTile);
+    };
+    const uintptr_t base = (uintptr_t)A.base;
+    auto desc = [&](uint32_t j, uint64_t& off, uint32_t& len) {
+        const uint32_t jc = j < np ? j : 0u;                       // clamped, branch-free prefetch
+        off = A.off[jc];
+        len = j < np ? (uint32_t)A.len[jc] : 0u;
+    };
+    uint64_t dn_o, dnn_o;
+    uint32_t dn_l, dnn_l;
+    uint32_t jA = piece_at(0u);
+    desc(jA, dn_o, dn_l);
+    desc(piece_at(1u), dnn_o, dnn_l);                              // two ahead
+    PieceStage SA, SB;
+    piece_issue(SA, base + dn_o, dn_l, lane);
+    dn_o = dnn_o;
+    dn_l = dnn_l;
+    uint32_t b, h;
+    for (uint32_t i = 0u; i < iters; i += 2u) {
+        const uint32_t jB = piece_at(i + 1u);
+        desc(piece_at(i + 2u), dnn_o, dnn_l);
+        piece_issue(SB, base + dn_o, dn_l, lane);
+        dn_o = dnn_o;
+        dn_l = dnn_l;
+        piece_consume(SA, lane, b, h);
+        piece_store(eo, jA, b, h, lane, jA < np);
+        jA = piece_at(i + 2u);
+        desc(piece_at(i + 3u), dnn_o, dnn_l);
+        piece_issue(SA, base + dn_o, dn_l, lane);
+        dn_o = dnn_o;
+        dn_l = dnn_l;
+        piece_consume(SB, lane, b, h);
+        piece_store(eo, jB, b, h, lane, jB < np);
+    }
+}
+
+// A 16-lane group per chain (4 chains per wave, independent loads in flight for all four), 16
+// pieces per step.
+constexpr int kCG = 16;
+
+__global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, const uint64_t* eo, uint32_t cap) {
+    const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
+    if (np > cap) {
+        return;                                                   // pass 1 did the batch
+    }
+    const int lane = (int)(threadIdx.x & (kCG - 1));
+    const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(kCG - 1);          // the group's ballot bits
+    const uint32_t below = (1u << lane) - 1u;
+    const uint32_t ngr = gridDim.x * (256u / kCG);
+    // wave-uniform trip count: the wave's 4 groups take chains c0 .. c0 + 3 of each round
+    const uint32_t c0 = blockIdx.x * (256u / kCG) + (threadIdx.x & ~63u) / kCG;
+    const uint32_t rounds = c0 < A.n ? (A.n - c0 + ngr - 1u) / ngr : 0u;
+    for (uint32_t r = 0u; r < rounds; ++r) {
+        const uint32_t ch = c0 + r * ngr + (threadIdx.x & 63u) / kCG;
+        const bool live = ch < A.n;
+        const uint32_t p0 = live ? A.first[ch] : 0u;
+        const uint32_t p1 = live ? A.first[ch + 1u] : 0u;
+        uint64_t E = 0u, O = 0u;
+        uint32_t par = 0u;                                        // stream parity at the next piece
+        if (live && A.pseudo && A.pseudo_len) {
+            uint32_t plen = A.pseudo_len;
+            if (p0 == p1 && (plen & 1u)) {
+                plen -= 1u;                                       // NULL chain quirk
+            }
+            const uintptr_t pa = (uintptr_t)A.pseudo + (uint64_t)ch * A.pseudo_stride;
+            const EO s = span_eo<kCG>(pa, plen, lane);
+            if (pa & 1u) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
+            par = A.pseudo_len & 1u;                              // pieces follow ALL pseudo bytes
+        }
+        const uint32_t npc = p1 - p0;
+        uint32_t steps = (npc + kCG - 1u) / kCG;
+#pragma unroll
+        for (int m = 32; m >= kCG; m >>= 1) {                     // the wave's longest chain
+            steps = max(steps, (uint32_t)__shfl_xor((int)steps, m, 64));
+        }
+        for (uint32_t t = 0u; t < steps; ++t) {
+            const uint32_t j = p0 + t * kCG + (uint32_t)lane;
+            const bool v = j < p1;
+            const uint32_t len = v ? (uint32_t)A.len[j] : 0u;
+            const uint64_t off = v ? A.off[j] : 0u;
+            const uint64_t rec = v ? eo[j] : 0u;
+            const uint32_t odd = (uint32_t)(__ballot((len & 1u) != 0u) >> sh) & 0xFFFFu;
+            const uint32_t spar = par ^ ((uint32_t)__popc(odd & below) & 1u);
+            const uint32_t swap = ((uint32_t)((uintptr_t)A.base + off) & 1u) ^ spar;
+            const uint32_t e = (uint32_t)rec, o = (uint32_t)(rec >> 32);
+            E += swap ? o : e;
+            O += swap ? e : o;
+            par ^= (uint32_t)__popc(odd) & 1u;
+        }
+        E = group_sum64<kCG>(E);
+        O = group_sum64<kCG>(O);
+        if (live && lane == 0) {
+            chain_out(A, ch, E, O);
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s) {
+    // pass 1: exactly the resident blocks (so that at any time they work on neighbouring tiles),
+    // taking tiles of 64 consecutive pieces round-robin (the piece count lives on the device; blocks
+    // past the last tile return); pass 2: a 16-lane group per chain
+    static int per_cu = 0;
+    if (per_cu <= 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+        per_cu = nb;
+    }
+    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)(std::max(cus, 1) * per_cu)), dim3(256), 0, s, a, eo, cap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;
+    const unsigned g2 = (unsigned)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 64u);
+    hipLaunchKernelGGL(chain_combine_kernel, dim3(g2), dim3(256), 0, s, a, (const uint64_t*)eo, cap);
+    return hipGetLastError();
+}
 
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s) {
     switch (group) {

@@ -111,6 +111,9 @@ struct ChainBatchArgs {
 };
 
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
+// Two-pass form (default): per-piece even/odd sums into `eo` (cap records), then a combine pass per
+// chain; batches of more than `cap` pieces fall back to the wave-per-chain form inside pass 2.
+hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s);
 
 // CRC-32 batches (netcsum_crc.hip; net_util.c:485-636).
 struct CrcBatchArgs {
