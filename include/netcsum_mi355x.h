@@ -451,6 +451,11 @@ NET_ERR  NetUtil_MI355X_TxBurstHost        (void            *h_base,
  * reference's pdata_buf == NULL case (an odd pseudo-header loses its last octet,
  * net_util.c:1601-1611); describe a chain of empty buffers with one zero-length piece.
  * op: NETCSUM_OP_DATA_CALC (u16 out) or NETCSUM_OP_DATA_VERIFY (u8 DEF_OK/DEF_FAIL out).
+ * Forms: by default two launches on the stream — per-piece sums in piece order into this thread's
+ * device scratch for the stream (8 B per piece, room for max(2^20, 128 * n_chains) pieces; a batch
+ * with more pieces is done in the wave-per-chain form instead, same results), then one combine per
+ * chain; NETCSUM_TUNE_KERNEL 1 selects the wave-per-chain form, NETCSUM_TUNE_GROUP_LANES 16 / 32 / 64
+ * a lane group per chain. Graph capture: as for the Tx scratch (one uncaptured call first).
  * ============================================================================================ */
 NET_ERR  NetUtil_MI355X_ChkSumBatchChains  (const void      *d_base,
                                             const uint64_t  *d_piece_off,
@@ -590,7 +595,8 @@ typedef enum netcsum_tune_key {
                                          len, base a multiple of 4, no pseudo-header; else 7;
                                          CHUNKS 4 / 8 = pieces in flight; TILE = headers per run,
                                          auto: the most that fit 4 KiB from any 128-B lead, 192 for
-                                         20-B headers)                                              */
+                                         20-B headers). Chain batches: 1 = the wave-per-chain form
+                                         (default: two passes, see (2c))                            */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),
                                          2 run-stream form of the checksum kernels (24-KiB runs per
