@@ -609,9 +609,11 @@ typedef enum netcsum_tune_key {
                                          IPv4 packet batches: packets per wave run of the run-stream
                                          form (<= 64; auto 8); TUNE_KERNEL 2 forces the lane-group
                                          packet kernel                                              */
-    NETCSUM_TUNE_TX_PASSES     = 10,  /* run-stream Tx finalize: 0 auto (2), 1 checksum fields written
-                                         by the checksum pass, 2 checksum pass writes 8-B records,
-                                         a scatter pass writes the fields                            */
+    NETCSUM_TUNE_TX_PASSES     = 10,  /* run-stream Tx finalize: 0 auto (2 from 64 Ki datagrams up,
+                                         else 1), 1 checksum fields written by the checksum pass
+                                         (IPv6 chains past the window walked in the same launch),
+                                         2 checksum pass writes 8-B records, a scatter pass writes
+                                         the fields (then a walk pass for IPv6 / mixed batches)      */
     NETCSUM_TUNE_STREAM_WAVES  = 11,  /* run-stream kernels (segments, packets): resident waves per
                                          SIMD, 3..8, enforced by reserving LDS per workgroup; 0 = as
                                          many as registers allow; -1 = each kernel's default (dense

@@ -244,7 +244,8 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     rx, tx, txf, d_rx, d_tx = _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
     tag = "v6" if ver == 6 else "mixed"
     assert d_rx.startswith("pkt_stream_kernel") and f",rx,{tag}>" in d_rx and f",tx,{tag}>" in d_tx, (d_rx, d_tx)
-    assert d_rx.endswith(" +pkt_v6_walk_kernel") and d_tx.endswith(" +pkt_v6_walk_kernel"), (d_rx, d_tx)
+    assert d_rx.endswith(" +inline_v6_walk"), d_rx
+    assert d_tx.endswith(" +pkt_v6_walk_kernel" if passes == 2 else " +inline_v6_walk"), d_tx
     bad = np.nonzero(rx != rx_w)[0]
     assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
     bad = np.nonzero(tx != tx_w)[0]
@@ -256,11 +257,15 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
 
 
 @pytest.mark.parametrize("lead", list(range(16)))
-def test_pkt_stream_v6_extension_chains_of_any_length(lead):
+@pytest.mark.parametrize("tile", [0, 8, 64])
+def test_pkt_stream_v6_extension_chains_of_any_length(lead, tile):
     """Destination Options / Routing chains before TCP / UDP / ICMPv6 at every lead: one header of
     1..40 units (8..320 B, inside and past the lane's 96 - lead bytes) or 4..9 headers — every chain
-    walked to its transport header (the batch kernel's window, then the walk pass), Rx verdicts and
-    Tx bytes + flags equal the oracle's, no EXT_HDR left."""
+    walked to its transport header (the batch kernel's window, then the walk: inside the Rx kernel by
+    the wave's 16-lane groups, in the walk pass after Tx), Rx verdicts and Tx bytes + flags equal the
+    oracle's, no EXT_HDR left. tile: datagrams per wave (0: the default; 8 / 64: many deferred
+    datagrams per wave, up to four walked at once)."""
+    netcsum.tune(netcsum.TUNE_TILE, tile if tile else -1)
     from packets import make_packet_v6
     rng = random.Random(900 + lead)
     stride = pkt_len = 1024
@@ -322,15 +327,23 @@ def test_pkt_stream_v6_c2_shape_round_trip_1M():
 
 @pytest.mark.parametrize("stride,pkt_len,run", [(1500, 1500, 8), (1000, 1000, 16), (577, 577, 32), (256, 200, 64),
                                                 (128, 128, 64), (9000, 9000, 8)])
-def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run):
-    """Default run: about 20 KB of datagrams per wave in multiples of 8, 8..64 (r2zq sweep); results equal the
-    lane-group kernel's."""
+@pytest.mark.parametrize("copies", [1, 1000])
+def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run, copies):
+    """Default run: about 20 KB of datagrams per wave in multiples of 8, 8..64 (r2zq sweep), halved while the
+    batch has fewer than 2048 runs (small bursts are latency-bound); results equal the lane-group kernel's.
+    copies: the 300-datagram batch repeated (300 000 datagrams keep the full run)."""
     rng = random.Random(stride)
-    n = 300
-    buf = _batch(rng, n, stride, pkt_len, 2)
+    n0 = 300
+    buf0 = _batch(rng, n0, stride, pkt_len, 2)
+    body = buf0[2:2 + n0 * stride]
+    buf = np.concatenate([buf0[:2], np.tile(body, copies), buf0[2 + n0 * stride:]])
+    n = n0 * copies
+    spw = run
+    while spw > 1 and n < 2048 * spw:
+        spw //= 2
     netcsum.tune(netcsum.TUNE_KERNEL, 2)
     rx_ref, tx_ref, txf_ref, _, _ = _run(buf, n, stride, pkt_len, 2, True)
     netcsum.tune(netcsum.TUNE_KERNEL, 0)
     rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, 2, True)
-    assert f"pkts_per_wave={run}" in d_rx and f"pkts_per_wave={run}" in d_tx, (d_rx, d_tx)
+    assert f"pkts_per_wave={spw}" in d_rx and f"pkts_per_wave={spw}" in d_tx, (d_rx, d_tx)
     assert np.array_equal(rx, rx_ref) and np.array_equal(tx, tx_ref) and np.array_equal(txf, txf_ref)

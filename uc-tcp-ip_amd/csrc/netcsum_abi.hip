@@ -940,33 +940,48 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const uint64_t per = std::max<uint64_t>(a.stride, 1u);
         const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
                                          : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
-        const uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : run;
+        // small batches (NIC bursts) are latency-bound: a run costs ~run x len / 4 KiB memory round
+        // trips, so runs halve until the batch spreads over >= 2048 waves (burst of 256 mixed frames:
+        // Rx 19.9 -> 13.3 us, Tx 22.8 -> 15.7 us; 16 Ki frames: runs of 8, 19.2 -> 17.2 us;
+        // profiles/r3t_burst_run_probe.jsonl); batches of >= 2048 runs keep the run length above
+        uint32_t spw = (tile > 0 && tile <= 64) ? (uint32_t)tile : run;
+        if (!(tile > 0 && tile <= 64)) {
+            while (spw > 1u && (uint64_t)n_pkt < 2048ull * spw) spw >>= 1;
+        }
         const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
-        const bool two = tx && g_tune_tx_passes.load() != 1;
+        // Tx passes: auto = two (8-B records, then a scatter pass: 1 M x 1500 B 0.2918 against 0.2954
+        // ms in one pass) from 64 Ki datagrams up, one below (a burst is then a single launch)
+        const int tp = g_tune_tx_passes.load();
+        const bool two = tx && (tp == 2 || (tp == 0 && n_pkt >= 65536u));
+        // IPv6 / mixed: Rx and one-pass Tx kernels finish their deferred datagrams themselves (no
+        // deferral word, no second launch, no scratch); two-pass Tx keeps the walk pass, which must
+        // follow the scatter pass
+        const bool walk_s = walk && two;
+        const bool own_flags_s = walk_s && d_flags == nullptr;
         char desc[136];
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s", d, snt ? ",nt" : "",
                  tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
-                 walk ? " +pkt_v6_walk_kernel" : "");
+                 walk_s ? " +pkt_v6_walk_kernel" : (walk ? " +inline_v6_walk" : ""));
         netcsum::set_last_launch(desc);
         // scratch: [deferral word (IPv6 / mixed), 256 B | records (two-pass Tx) | flags (own_flags)]
         ScratchLease scratch;
-        const size_t word_bytes = walk ? 256u : 0u;
+        const size_t word_bytes = walk_s ? 256u : 0u;
         const size_t rec_bytes = two ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
-        if (walk || two) {
-            NC_HIP(scratch.acquire(dev, hs, word_bytes + rec_bytes + (own_flags ? n_pkt : 0u)));
+        if (walk_s || two) {
+            NC_HIP(scratch.acquire(dev, hs, word_bytes + rec_bytes + (own_flags_s ? n_pkt : 0u)));
             uint8_t* sp = static_cast<uint8_t*>(scratch.ptr());
-            if (walk) {
+            if (walk_s) {
                 a.defer_word = reinterpret_cast<uint32_t*>(sp);
                 a.defer_tag = scratch.next_tag();
             }
-            if (own_flags) a.flags_out = sp + word_bytes + rec_bytes;
+            if (own_flags_s) a.flags_out = sp + word_bytes + rec_bytes;
         }
         NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs,
                                           two ? reinterpret_cast<netcsum::PktTxRecord*>(
                                                     static_cast<uint8_t*>(scratch.ptr()) + word_bytes)
                                               : nullptr));
-        if (walk) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
+        if (walk_s) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }

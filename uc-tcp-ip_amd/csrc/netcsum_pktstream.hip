@@ -42,6 +42,7 @@
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
 #include "netcsum_stream.h"
+#include "netcsum_v6walk.h"
 
 namespace netcsum {
 
@@ -473,9 +474,13 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     touch_retire(touch);
 
-    if (!mine) {
-        return;
-    }
+    // IPv6 / mixed rings without a deferral word (Rx, and one-pass Tx): the wave finishes its own
+    // deferred datagrams (EXT_HDR: chains past the window) after the epilogue, all 64 lanes together
+    // (walk_wave). Two-pass Tx keeps the walk pass, which must follow the scatter pass.
+    constexpr bool kWalkHere = !REC && VER != 4;
+    const bool walk_here = kWalkHere && A.defer_word == nullptr;           // wave-uniform
+    bool need = false;
+    if (mine) {
     // vector epilogue: lane k = packet s_begin + k (pkt_consume's verdicts / values)
     uint32_t acc_ip = pk.ip_sum, acc_l4 = tot_v - pk.ip_sum;
     if (TX && !pk.malformed) {
@@ -513,6 +518,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         }
     }
     const uint32_t idx = s_begin + lane;
+    need = walk_here && (f & NETCSUM_PKT_EXT_HDR) != 0u;               // walk_one writes its verdict
     if (A.defer_word != nullptr && (f & NETCSUM_PKT_EXT_HDR)) {
         *A.defer_word = A.defer_tag;                             // the walk pass has work (benign race)
     }
@@ -523,12 +529,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                            ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) | ((uint64_t)(f & 0xFFu) << 48) |
                            ((uint64_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u)) << 56);
         reinterpret_cast<uint64_t*>(rec)[idx] = r;
-        return;
-    }
-    if (A.flags_out) {
+    } else {
+    if (A.flags_out && !need) {
         A.flags_out[idx] = (uint8_t)f;
     }
-    if (!TX && A.action_out) {
+    if (!TX && A.action_out && !need) {
         A.action_out[idx] = (uint8_t)rx_action(f, pk.proto, pk.v6, A.rx_cfg);
     }
     if constexpr (TX) {
@@ -539,8 +544,15 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         if (cl4 != ~0u) {
             store_field(p + pk.l4_csum_off, cl4);
         }
-        if (A.fieldpos_out) {
+        if (A.fieldpos_out && !need) {
             A.fieldpos_out[idx] = (cip != ~0u ? kFieldIP : 0u) | (cl4 != ~0u ? kFieldL4 | (pk.l4_csum_off & 0xFFFFu) : 0u);
+        }
+    }
+    }
+    }
+    if constexpr (kWalkHere) {
+        if (walk_here) {
+            v6walk::walk_wave<TX>(A, s_begin, need, lane);
         }
     }
 }
