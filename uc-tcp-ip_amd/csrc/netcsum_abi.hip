@@ -214,7 +214,10 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
                 // device to about RUN_BYTES (launch_batch), the grid covering the shortest run, or take
                 // runs of 8 (r2ct) with VARLEN_RUN_BYTES 0
                 c.run_bytes = varlen ? netcsum::varlen_run_bytes() : 0u;
-                const uint64_t run = !varlen ? 16u : c.run_bytes ? netcsum::kVarlenSpwMin : 8u;
+                uint64_t run = !varlen ? 16u : c.run_bytes ? netcsum::kVarlenSpwMin : 8u;
+                if (!varlen) {                         // small batches: latency-bound runs halve until
+                    while (run > 1u && (uint64_t)a.n_seg < 2048u * run) run >>= 1;   // >= 2048 waves
+                }                                      // (as the packet batches, pkt_batch)
                 waves = ((uint64_t)a.n_seg + run - 1u) / run;
             }
             c.stream_spw = netcsum::stream_spw(a, waves);
