@@ -502,12 +502,11 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     // pass 1: exactly the resident blocks (so that at any time they work on neighbouring tiles),
     // taking tiles of 64 consecutive pieces round-robin (the piece count lives on the device; blocks
     // past the last tile return); pass 2: a 16-lane group per chain
-    static int per_cu = 0;
-    if (per_cu <= 0) {
+    static const int per_cu = [] {                                // thread-safe one-time query
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel, 256, 0) != hipSuccess || nb <= 0) nb = 4;
-        per_cu = nb;
-    }
+        return nb;
+    }();
     hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)(std::max(cus, 1) * per_cu)), dim3(256), 0, s, a, eo, cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
