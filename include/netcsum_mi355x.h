@@ -380,12 +380,16 @@ NET_ERR  NetUtil_MI355X_RxBurstTally       (const uint8_t   *h_action,
 /* ============================================================================================
  * (2e) Host-memory forms (the path starts in NIC Rx buffers, IF/net_if.c:6593,
  * and socket Tx buffers, Source/net_sock.c:5531). Same arguments and results as the device forms
- * above with every pointer in HOST memory; the call splits the batch into n_chunks chunks (0 = 1)
- * and pipelines, on three streams of the calling thread's context, H2D of each chunk's byte span
- * [min offset, max end) (plus its descriptors) -> the device form -> D2H of the results (Tx: of the
- * span itself, written back in place, so the call owns those bytes while it runs; an offset/length
- * Tx batch whose chunk spans overlap runs as one chunk). Host buffers should be pinned
- * (hipHostMalloc / hipHostRegister) for the copies to overlap. Returns when every result is in
+ * above with every pointer in HOST memory. The call splits the batch into n_chunks chunks and
+ * pipelines, on three streams of the calling thread's context, H2D of each chunk's byte span
+ * [min offset, max end) (plus its descriptors) -> the device form -> D2H of the results (Tx: one
+ * 8-B record of the fields written per datagram, which the call writes into the host buffer, so
+ * the call owns those bytes while it runs; a Tx batch's datagrams must not overlap one another,
+ * as the stack's buffers do not). n_chunks 0 = the library's choice: one chunk, except TxFinalizeIPHost /
+ * TxBurstHost from 32 Ki datagrams (n / 16 Ki chunks, at most 16). Every chunk adds 15-20 us to a
+ * call and PCIe stays the bound, so bursts of a few thousand frames are fastest in one
+ * (tools/burst_latency.c). Host buffers should be pinned (hipHostMalloc / hipHostRegister) for the
+ * copies to run at PCIe rate. Returns when every result is in
  * host memory. IP = mixed IPv4 / IPv6 (per datagram by the version nibble).
  * ============================================================================================ */
 NET_ERR  NetUtil_MI355X_ChkSumBatchVarLenHost(const void      *h_base,

@@ -1223,8 +1223,13 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
     HostCtx& c = *cp;
     std::vector<HostChunk> ch;
     bool disjoint = true;
-    if (n_chunks > 0 && n_pkt / n_chunks > (1u << 28)) n_chunks = (n_pkt >> 28) + 1u;   // records: 32-bit offsets
-    const uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks == 0 ? 1u : n_chunks, ch, &disjoint);
+    // n_chunks 0 = the library's choice (tools/burst_latency.c, profiles/r3x_burst_latency.jsonl): each
+    // chunk adds 15-20 us per call and PCIe stays the bound, so one chunk, except Tx from 32 Ki
+    // datagrams, whose host-side field write-back overlaps the later chunks' copies (262 144 frames:
+    // 16 chunks 7.4 ms, one 8.4 ms)
+    if (n_chunks == 0) n_chunks = tx ? std::min(16u, std::max(1u, n_pkt / 16384u)) : 1u;
+    if (n_pkt / n_chunks > (1u << 28)) n_chunks = (n_pkt >> 28) + 1u;   // records: 32-bit offsets
+    const uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks, ch, &disjoint);
     const bool varlen = h_off != nullptr;
     const uint32_t per = ch[0].ns;
     // device slot: [bytes | offsets | lengths | flags | actions | field positions | records];

@@ -450,7 +450,7 @@ def batch_varlen(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_se
 
 
 def batch_strided_host(seg, seg_stride, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out,
-                       op=OP_DATA_CALC, n_chunks=8, check=True):
+                       op=OP_DATA_CALC, n_chunks=0, check=True):
     if n_seg:
         _require(seg, (n_seg - 1) * seg_stride + seg_len, "segments")
         if pseudo is not None and pseudo_len:
@@ -591,7 +591,7 @@ def rx_burst_tally(actions):
 
 # ------------------------------------------------------------------ host-memory forms ((2e))
 def batch_varlen_host(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len, n_seg, out, op=OP_DATA_CALC,
-                      n_chunks=8, check=True):
+                      n_chunks=0, check=True):
     if n_seg:
         _require(seg_off, 8 * n_seg, "segment offsets")
         _require(seg_len, 2 * n_seg, "segment lengths")
@@ -603,7 +603,7 @@ def batch_varlen_host(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len,
     return err
 
 
-def rx_validate_ip_host(base, n, flags, off=None, lens=None, stride=0, pkt_len=0, n_chunks=8, check=True):
+def rx_validate_ip_host(base, n, flags, off=None, lens=None, stride=0, pkt_len=0, n_chunks=0, check=True):
     _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
     err = lib().NetUtil_MI355X_RxValidateIPHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags), n_chunks)
     if check:
@@ -611,7 +611,7 @@ def rx_validate_ip_host(base, n, flags, off=None, lens=None, stride=0, pkt_len=0
     return err
 
 
-def tx_finalize_ip_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, udp_tx_csum=True, n_chunks=8,
+def tx_finalize_ip_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, udp_tx_csum=True, n_chunks=0,
                         check=True):
     _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
     err = lib().NetUtil_MI355X_TxFinalizeIPHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags),
@@ -621,7 +621,7 @@ def tx_finalize_ip_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_
     return err
 
 
-def rx_burst_host(base, n, action, flags=None, off=None, lens=None, stride=0, pkt_len=0, rx_cfg=0, n_chunks=8,
+def rx_burst_host(base, n, action, flags=None, off=None, lens=None, stride=0, pkt_len=0, rx_cfg=0, n_chunks=0,
                   check=True):
     _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
     if n:
@@ -633,7 +633,7 @@ def rx_burst_host(base, n, action, flags=None, off=None, lens=None, stride=0, pk
     return err
 
 
-def tx_burst_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, n_chunks=8, check=True):
+def tx_burst_host(base, n, flags=None, off=None, lens=None, stride=0, pkt_len=0, n_chunks=0, check=True):
     _pkt_bounds(base, off, lens, stride, pkt_len, n, flags)
     err = lib().NetUtil_MI355X_TxBurstHost(_p(base), _p(off), _p(lens), stride, pkt_len, n, _p(flags), n_chunks)
     if check:
