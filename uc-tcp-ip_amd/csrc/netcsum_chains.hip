@@ -499,15 +499,20 @@ __global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, co
 }  // namespace
 
 hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s) {
-    // pass 1: exactly the resident blocks (so that at any time they work on neighbouring tiles),
-    // taking tiles of 64 consecutive pieces round-robin (the piece count lives on the device; blocks
-    // past the last tile return); pass 2: a 16-lane group per chain
+    // pass 1: blocks take tiles of 64 consecutive pieces round-robin (the piece count lives on the
+    // device; blocks past the last tile return). Grid: 2 blocks per chain, at least the resident
+    // blocks, at most one per tile the scratch holds — so a batch of up to 32 pieces per chain gets
+    // one block per tile, which the dispatcher hands out as blocks finish: 16 Ki x 45 fragments
+    // 0.1857 -> 0.1807 ms against the resident-sized grid, 21 248 empty blocks included
+    // (profiles/r3w_chain_grid_ab.log, tools/r3w_cmd.sh). Pass 2: a 16-lane group per chain.
     static const int per_cu = [] {                                // thread-safe one-time query
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel, 256, 0) != hipSuccess || nb <= 0) nb = 4;
         return nb;
     }();
-    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)(std::max(cus, 1) * per_cu)), dim3(256), 0, s, a, eo, cap);
+    const uint64_t resident = (uint64_t)std::max(cus, 1) * (uint64_t)per_cu;
+    const uint64_t g1 = std::min<uint64_t>(((uint64_t)cap + 63u) / 64u, std::max<uint64_t>(resident, 2ull * a.n));
+    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, a, eo, cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;
