@@ -511,7 +511,9 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
         return nb;
     }();
     const uint64_t resident = (uint64_t)std::max(cus, 1) * (uint64_t)per_cu;
-    const uint64_t g1 = std::min<uint64_t>(((uint64_t)cap + 63u) / 64u, std::max<uint64_t>(resident, 2ull * a.n));
+    // (at most 2^20 blocks = 2^28 threads, within the launch limit; the tiles go round-robin beyond)
+    const uint64_t g1 = std::min<uint64_t>(std::min<uint64_t>(((uint64_t)cap + 63u) / 64u, 1ull << 20),
+                                           std::max<uint64_t>(resident, 2ull * a.n));
     hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, a, eo, cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
