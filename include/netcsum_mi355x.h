@@ -617,7 +617,7 @@ typedef enum netcsum_tune_key {
                                          else 1), 1 checksum fields written by the checksum pass
                                          (IPv6 chains past the window walked in the same launch),
                                          2 checksum pass writes 8-B records, a scatter pass writes
-                                         the fields (then a walk pass for IPv6 / mixed batches)      */
+                                         the fields (and walks IPv6 chains past the window)      */
     NETCSUM_TUNE_STREAM_WAVES  = 11,  /* run-stream kernels (segments, packets): resident waves per
                                          SIMD, 3..8, enforced by reserving LDS per workgroup; 0 = as
                                          many as registers allow; -1 = each kernel's default (dense

@@ -234,7 +234,7 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     extension-header chains inside and beyond the lane's window, Hop-by-Hop after the first, Fragment,
     opaque extension headers, malformed versions / lengths, corrupted bytes), alone (VER 6) or mixed
     with every IPv4 kind (VER 0), Rx verdicts and Tx bytes + verdicts against the oracle (chains past
-    the lane's 96-B prologue finished by the walk pass)."""
+    the lane's 96-B prologue finished inside the run-stream launches)."""
     netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
     rng = random.Random(ver * 1000 + stride * 7 + pkt_len + lead * 131 + passes)
     n = 600 if stride < 5000 else 150
@@ -245,7 +245,8 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     tag = "v6" if ver == 6 else "mixed"
     assert d_rx.startswith("pkt_stream_kernel") and f",rx,{tag}>" in d_rx and f",tx,{tag}>" in d_tx, (d_rx, d_tx)
     assert d_rx.endswith(" +inline_v6_walk"), d_rx
-    assert d_tx.endswith(" +pkt_v6_walk_kernel" if passes == 2 else " +inline_v6_walk"), d_tx
+    assert d_tx.endswith(" +pkt_scatter_kernel +inline_v6_walk" if passes == 2 else "> block=256 pkts_per_wave="
+                         + d_tx.split("pkts_per_wave=")[1].split(" ")[0] + " +inline_v6_walk"), d_tx
     bad = np.nonzero(rx != rx_w)[0]
     assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
     bad = np.nonzero(tx != tx_w)[0]

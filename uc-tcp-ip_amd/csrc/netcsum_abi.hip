@@ -931,9 +931,10 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // run in multiples of 8 datagrams, 8..64 (40 KB in multiples of 16 for mixed rings); r2zq sweep
     // (tools/pkt_run_probe.py): Rx of 256-B datagrams 0.891 -> 0.567 ms, 576-B 0.424 -> 0.29,
     // 1000-B 0.259 -> 0.222; 1500-B keeps 8.
-    // IPv6 / mixed batches: a second pass walks the extension-header chains the batch kernel left as
-    // EXT_HDR (netcsum_v6walk.hip). It reads the flags, so a Tx batch without d_flags gets them in the
-    // stream's scratch buffer (after the two-pass records when there are records).
+    // IPv6 / mixed batches through the lane-group kernel: a second pass walks the extension-header
+    // chains the batch kernel left as EXT_HDR (netcsum_v6walk.hip). It reads the flags, so a Tx batch
+    // without d_flags gets them in the stream's scratch buffer. (The run-stream path below walks them
+    // inside its own launches.)
     // (an Rx burst without d_flags keeps them there too, or nowhere for IPv4, whose kernels write
     // each action directly)
     const bool walk = ip_ver != 4;
@@ -957,34 +958,18 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // ms in one pass) from 64 Ki datagrams up, one below (a burst is then a single launch)
         const int tp = g_tune_tx_passes.load();
         const bool two = tx && (tp == 2 || (tp == 0 && n_pkt >= 65536u));
-        // IPv6 / mixed: Rx and one-pass Tx kernels finish their deferred datagrams themselves (no
-        // deferral word, no second launch, no scratch); two-pass Tx keeps the walk pass, which must
-        // follow the scatter pass
-        const bool walk_s = walk && two;
-        const bool own_flags_s = walk_s && d_flags == nullptr;
+        // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
+        // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
         char desc[136];
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s", d, snt ? ",nt" : "",
                  tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
-                 walk_s ? " +pkt_v6_walk_kernel" : (walk ? " +inline_v6_walk" : ""));
+                 walk ? " +inline_v6_walk" : "");
         netcsum::set_last_launch(desc);
-        // scratch: [deferral word (IPv6 / mixed), 256 B | records (two-pass Tx) | flags (own_flags)]
+        // scratch: the records of two-pass Tx
         ScratchLease scratch;
-        const size_t word_bytes = walk_s ? 256u : 0u;
-        const size_t rec_bytes = two ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
-        if (walk_s || two) {
-            NC_HIP(scratch.acquire(dev, hs, word_bytes + rec_bytes + (own_flags_s ? n_pkt : 0u)));
-            uint8_t* sp = static_cast<uint8_t*>(scratch.ptr());
-            if (walk_s) {
-                a.defer_word = reinterpret_cast<uint32_t*>(sp);
-                a.defer_tag = scratch.next_tag();
-            }
-            if (own_flags_s) a.flags_out = sp + word_bytes + rec_bytes;
-        }
+        if (two) NC_HIP(scratch.acquire(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord)));
         NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs,
-                                          two ? reinterpret_cast<netcsum::PktTxRecord*>(
-                                                    static_cast<uint8_t*>(scratch.ptr()) + word_bytes)
-                                              : nullptr));
-        if (walk_s) NC_HIP(netcsum::launch_pkt_v6_walk(a, tx, cu_count(dev), hs));
+                                          two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }

@@ -476,7 +476,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 
     // IPv6 / mixed rings without a deferral word (Rx, and one-pass Tx): the wave finishes its own
     // deferred datagrams (EXT_HDR: chains past the window) after the epilogue, all 64 lanes together
-    // (walk_wave). Two-pass Tx keeps the walk pass, which must follow the scatter pass.
+    // (walk_wave). Two-pass Tx: the scatter pass walks them (pkt_scatter_kernel<WALK>).
     constexpr bool kWalkHere = !REC && VER != 4;
     const bool walk_here = kWalkHere && A.defer_word == nullptr;           // wave-uniform
     bool need = false;
@@ -561,17 +561,22 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 // WT (NETCSUM_TUNE_TX_FLUSH 1): the field bytes are stored at system scope, i.e. written through the
 // L2 to HBM during this pass instead of sitting dirty in the L2 until a later launch evicts them.
 // WB (TX_FLUSH 2): every wave ends with an agent-scope release (the L2 write-back of its XCD).
-template <bool WT, bool WB>
+// WALK (IPv6 / mixed rings): the wave then finishes its datagrams whose record says EXT_HDR (chains
+// past pass 1's window) with its four 16-lane groups (walk_wave, after its own field stores), so
+// two-pass Tx needs no walk launch and no deferral word either.
+template <bool WT, bool WB, bool WALK>
 __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const PktTxRecord* rec) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    bool need = false;
     if (i < A.n) {
         const uint64_t r = reinterpret_cast<const uint64_t*>(rec)[i];      // PktTxRecord, one 8-B load
         const uint32_t vals = (uint32_t)r, l4_off = (uint32_t)(r >> 32) & 0xFFFFu;
         const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
-        if (A.flags_out) {
+        need = WALK && A.defer_word == nullptr && (flags & NETCSUM_PKT_EXT_HDR) != 0u;   // walk_one writes
+        if (A.flags_out && !need) {                                                     // its verdict
             A.flags_out[i] = (uint8_t)flags;
         }
-        if (A.fieldpos_out) {
+        if (A.fieldpos_out && !need) {
             A.fieldpos_out[i] = ((store & 1u) ? kFieldIP : 0u) | ((store & 2u) ? kFieldL4 | l4_off : 0u);
         }
         uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
@@ -591,6 +596,11 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
             if (store & 2u) {
                 store_field(p + l4_off, vals >> 16);
             }
+        }
+    }
+    if constexpr (WALK) {
+        if (A.defer_word == nullptr) {                                  // uniform
+            v6walk::walk_wave<true>(A, blockIdx.x * 256u + (threadIdx.x & ~63u), need, threadIdx.x & 63u);
         }
     }
     if constexpr (WB) {
@@ -634,15 +644,16 @@ int tx_flush_mode() {
     return m < 0 ? 0 : m;
 }
 
+template <bool WALK>
 hipError_t launch_scatter(const PktBatchArgs& a, const PktTxRecord* rec, hipStream_t s) {
     const int m = tx_flush_mode();
     const dim3 g((a.n + 255u) / 256u), b(256);
     if (m == 1) {
-        hipLaunchKernelGGL((pkt_scatter_kernel<true, false>), g, b, 0, s, a, rec);
+        hipLaunchKernelGGL((pkt_scatter_kernel<true, false, WALK>), g, b, 0, s, a, rec);
     } else if (m == 2) {
-        hipLaunchKernelGGL((pkt_scatter_kernel<false, true>), g, b, 0, s, a, rec);
+        hipLaunchKernelGGL((pkt_scatter_kernel<false, true, WALK>), g, b, 0, s, a, rec);
     } else {
-        hipLaunchKernelGGL((pkt_scatter_kernel<false, false>), g, b, 0, s, a, rec);
+        hipLaunchKernelGGL((pkt_scatter_kernel<false, false, WALK>), g, b, 0, s, a, rec);
     }
     return hipGetLastError();
 }
@@ -669,7 +680,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        e = launch_scatter(a, rec, s);
+        e = launch_scatter<VER != 4>(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
     hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
