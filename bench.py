@@ -38,9 +38,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # CPU baseline: the OpenMP workers are pinned (OMP_PROC_BIND=close over cores); set
 # before torch loads libgomp, which reads them once. Single-rank runs only (the baseline is rank 0 at
 # N = 1; ranks of an N > 1 run would pin their threads onto the same cores).
+_OMP_PINNED_HERE = []
 if os.environ.get("WORLD_SIZE", "1") == "1":
-    os.environ.setdefault("OMP_PROC_BIND", "close")
-    os.environ.setdefault("OMP_PLACES", "cores")
+    for _k, _v in (("OMP_PROC_BIND", "close"), ("OMP_PLACES", "cores")):
+        if _k not in os.environ:
+            os.environ[_k] = _v
+            _OMP_PINNED_HERE.append(_k)
 sys.path.insert(0, os.path.join(REPO, "uc-tcp-ip_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
@@ -67,7 +70,119 @@ def parse():
                     help="roofline.traffic source: live rocprofv3 --pmc passes over a child run (rank 0, N=1; "
                          "falls back to the committed summaries), committed file only, or none")
     ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block)")
+    ap.add_argument("--no-c5-point", action="store_true",
+                    help="N=1: skip the same-workload retention point (the C5 16 M-segment shard on this GPU)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="launcher (--gpus N > 1 without WORLD_SIZE): seconds before the rank processes are killed")
+    # CPU test of the launcher only: each rank prints its rendezvous environment and exits before any
+    # torch import ("ok"), or rank 1 exits 3 ("fail1"); tests/test_bench_launch_cpu.py
+    ap.add_argument("--launcher-selftest", choices=["ok", "fail1"], default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def rank_environments(n, port, base=None):
+    """The environment of each of the N rank processes the launcher starts: one rank per GPU of this
+    node, rendezvous over 127.0.0.1 (torch.distributed env:// reads these six variables)."""
+    base = dict(os.environ if base is None else base)
+    for k in _OMP_PINNED_HERE:                      # the CPU-baseline pinning is for a single rank only
+        base.pop(k, None)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        envs.append(e)
+    return envs
+
+
+def world_check(gpus, env=None):
+    """--gpus N against the rank environment: returns "launch" (no WORLD_SIZE and N > 1: this process
+    starts the N ranks), "rank" (run as one rank) or raises SystemExit(2) when an externally launched
+    world (torchrun) disagrees with --gpus — the run would otherwise measure a different N than asked."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} must be >= 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "rank"
+    if int(ws) != gpus:
+        print(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: refusing to measure a different world size than "
+              f"asked", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    return "rank"
+
+
+def launch_ranks(args):
+    """--gpus N > 1 with no WORLD_SIZE: start N fresh rank processes of this script (one per GPU),
+    wait for all of them, print rank 0's JSON line and return non-zero if any rank failed or timed out.
+    This process never touches the GPU (no torch import): the ranks own the devices."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs, outs = [], []
+    for r, env in enumerate(rank_environments(args.gpus, port)):
+        f = tempfile.TemporaryFile(mode="w+")
+        outs.append(f)
+        procs.append(subprocess.Popen(argv, env=env, stdout=f, start_new_session=True))
+    deadline = time.monotonic() + args.launch_timeout
+    rc = [None] * len(procs)
+    failed = None
+    while any(c is None for c in rc):
+        for r, p in enumerate(procs):
+            if rc[r] is None:
+                rc[r] = p.poll()
+                if rc[r] not in (None, 0) and failed is None:
+                    failed = f"rank {r} exited {rc[r]}"
+        if failed or time.monotonic() > deadline:
+            failed = failed or f"timeout after {args.launch_timeout:.0f} s"
+            for r, p in enumerate(procs):        # end every rank's own process group, nothing else
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+            for r, p in enumerate(procs):
+                rc[r] = p.wait()
+            break
+        time.sleep(0.05)
+    line = None
+    for r, f in enumerate(outs):
+        f.seek(0)
+        text = f.read()
+        if r == 0:
+            lines = [x for x in text.splitlines() if x.startswith("{")]
+            line = lines[-1] if lines else None
+            rest = [x for x in text.splitlines() if not x.startswith("{")]
+            if rest:
+                print("\n".join(rest), file=sys.stderr, flush=True)
+        elif text.strip():
+            print("\n".join(f"[rank {r}] {x}" for x in text.splitlines()), file=sys.stderr, flush=True)
+    if failed or any(c != 0 for c in rc):
+        print(f"bench.py launcher: {failed or 'a rank failed'}; exit codes {rc}", file=sys.stderr, flush=True)
+        return 1
+    if line is None:
+        print("bench.py launcher: rank 0 printed no JSON line", file=sys.stderr, flush=True)
+        return 1
+    print(line, flush=True)
+    return 0
+
+
+def launcher_selftest(mode):
+    """Rank side of --launcher-selftest: report the rendezvous environment, no torch, no GPU."""
+    rank = int(os.environ["RANK"])
+    if mode == "fail1" and rank == 1:
+        print("selftest: rank 1 fails on purpose", file=sys.stderr, flush=True)
+        return 3
+    print(json.dumps({k: os.environ.get(k) for k in RANK_ENV}), flush=True)
+    return 0
 
 
 def c2_pseudo_headers(start, n, L, plen):
@@ -105,6 +220,64 @@ def make_c2_shard(torch, netcsum, start, n, L, plen, dev):
 def host_c2_shard(oracle, start, n, L, plen):
     """The same shard regenerated on the host (test / parity use)."""
     return oracle.fill(start * L, n * L, SEED, 0), (c2_pseudo_headers(start, n, L, plen) if plen else None)
+
+
+C5_SHARD = 1 << 24                  # BASELINE configs[4]: 128 M segments over 8 GPUs = 16 M per GPU
+
+
+def c5_point(torch, netcsum, args, dev, stream):
+    """Same-workload retention denominator, measured at N = 1 OUTSIDE the timed region: the per-GPU
+    rate of one C5 shard (16 M x 1500 B + 12 B, rank 0's slice of the global batch) on this GPU, by
+    the headline's own method (K launches between two synchronizes, wall clock) and by HIP events on
+    the launch stream. The driver's N > 1 runs measure exactly this workload per rank, so
+    per-GPU@N / this value is retention on ONE workload (the headline's N = 1 point is C2)."""
+    import numpy as np
+    L, plen, n = args.seg_len, args.pseudo_len, C5_SHARD
+    seg, ph = make_c2_shard(torch, netcsum, 0, n, L, plen, dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+
+    def step():
+        netcsum.batch_strided(seg, L, L, ph, plen, plen, n, out, netcsum.OP_DATA_CALC, stream=stream)
+    t = time.perf_counter()
+    while time.perf_counter() - t < 0.3:
+        step()
+        torch.cuda.synchronize()
+    k = max(10, min(args.steps, 50))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / k
+    parity = None
+    try:
+        import oracle
+        sample = np.sort(np.random.default_rng(5).choice(n, size=64, replace=False))
+        sidx = torch.from_numpy(sample).to(dev)
+        segs = seg[: n * L].view(n, L)[sidx].cpu().numpy().reshape(-1)
+        phs = ph.view(n, plen)[sidx].cpu().numpy().reshape(-1) if plen else None
+        want = oracle.batch_strided(segs, L, L, phs, plen, plen, len(sample), 0)
+        parity = bool(np.array_equal(out.cpu().numpy().view(np.uint16)[sample], want))
+    except Exception as e:                        # noqa: BLE001
+        parity = f"unchecked: {e}"
+    desc = "netcsum::" + netcsum.last_launch()
+    del seg, ph, out
+    torch.cuda.empty_cache()
+    algo = n * (L + plen + 2)
+    return {"workload": f"C5 shard: {n} x {L} B TCP segments + {plen} B pseudo-header on one GPU "
+                        "(rank 0's slice of the 128 M global batch)",
+            "value_per_gpu": round(n * (L + plen) * k / wall / 2 ** 30, 2), "unit": "GiB/s",
+            "ms_per_step": round(wall / k * 1e3, 4), "steps": k, "kernel": desc,
+            "kernel_ms": round(kern_ms, 4), "roofline_frac": round(algo / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "parity_sample_ok": parity,
+            "use": "retention denominator for the driver's N > 1 runs (same workload per GPU)"}
 
 
 def cpu_model():
@@ -343,6 +516,10 @@ def load_traffic(path, n_seg, kernel_desc):
 
 def main():
     args = parse()
+    if world_check(args.gpus) == "launch":
+        return launch_ranks(args)
+    if args.launcher_selftest:
+        return launcher_selftest(args.launcher_selftest)
     import torch
     import torch.distributed as dist
 
@@ -351,11 +528,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU; a box with fewer GPUs than local ranks (a rehearsal) folds them onto its devices
-    local = local % max(1, torch.cuda.device_count())
     # RCCL ("nccl") carries the barrier and the two reductions; NETCSUM_BENCH_DIST_BACKEND=gloo (host
     # tensors) lets several ranks share one GPU to rehearse the N > 1 path (RCCL refuses duplicate GPUs)
     backend = os.environ.get("NETCSUM_BENCH_DIST_BACKEND", "nccl")
+    # one rank per GPU: only the gloo rehearsal may fold several ranks onto fewer devices
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        if backend != "gloo" or ndev == 0:
+            print(f"bench.py: rank {rank} has LOCAL_RANK {local} but this node shows {ndev} GPU(s); refusing to "
+                  f"fold ranks onto shared devices (only NETCSUM_BENCH_DIST_BACKEND=gloo rehearses that)",
+                  file=sys.stderr, flush=True)
+            return 2
+        local = local % ndev
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -374,7 +558,7 @@ def main():
 
     n, L, plen = args.segments, args.seg_len, args.pseudo_len
     if n is None:
-        n = (1 << 20) if world == 1 else (1 << 24)       # C2 at N=1; the C5 shard (16 M) at N>1
+        n = (1 << 20) if world == 1 else C5_SHARD         # C2 at N=1; the C5 shard (16 M) at N>1
     start, n = shard_range(rank, n)
     seg, ph = make_c2_shard(torch, netcsum, start, n, L, plen, dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
@@ -459,6 +643,15 @@ def main():
     rs_ms = probe_ms[1]
     run_probe_gbps = n16 / (probe_ms[2] * 1e-3) / 1e9
 
+    c5 = None
+    if world == 1 and not args.no_c5_point and n != C5_SHARD:
+        del seg, ph, out, sink
+        torch.cuda.empty_cache()
+        try:
+            c5 = c5_point(torch, netcsum, args, dev, stream)
+        except Exception as e:                    # noqa: BLE001 — report, the headline stands without it
+            c5 = {"error": str(e)}
+
     parity_all = parity_ok
     if world > 1:                                  # every rank's sample must match its oracle
         t = torch.tensor([1 if parity_ok is True else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
@@ -495,7 +688,7 @@ def main():
             "dtype": "u16",
             "data": "synthetic (device-generated splitmix64 bytes, seed 0x5EED0001, rank shard = slice of one global stream; IPv4 pseudo-headers from the global index)",
             "config": {"workload": (("C2: 1 M x " if world == 1 and n == 1 << 20 else
-                                     f"C5 shard: {n} x " if n == 1 << 24 else f"{n} x ")
+                                     f"C5 shard: {n} x " if n == C5_SHARD else f"{n} x ")
                                     + f"{L} B TCP segments + {plen} B IPv4 pseudo-header per GPU, device-resident, "
                                     "NetUtil_16BitOnesCplChkSumDataCalc per segment"),
                        "segments_per_gpu": n, "seg_len": L, "pseudo_len": plen,
@@ -516,6 +709,13 @@ def main():
                          "frac_of_run_stream_read_probe": round(achieved / run_probe_gbps, 4)},
             "parity_sample_ok": parity_all,
         }
+        if c5 is not None:
+            line["c5_shard_point"] = c5
+        if world == 1:
+            line["config"]["dist"] = "single rank"
+        else:
+            line["config"]["dist"] = f"{world} ranks, backend {backend}, devices: " + (
+                "one per rank" if backend == "nccl" else f"{ndev} shared (rehearsal)")
         if world == 1 and not args.no_cpu_baseline:
             try:
                 import oracle
@@ -531,7 +731,8 @@ def main():
 
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
