@@ -650,9 +650,17 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_HDR_BURST     = 19,  /* header stream kernel (C3): 1 = a run's results gathered in LDS
                                          and written as whole 16-B pieces, 0 = one store per piece,
                                          -1 = the default                                             */
-    NETCSUM_TUNE_VARLEN_RUN_BYTES = 20 /* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
+    NETCSUM_TUNE_VARLEN_RUN_BYTES = 20,/* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
                                          run length chosen on the device from sampled lengths; 0 =
                                          runs of 8 segments; -1 = the default (16 KiB)                 */
+    NETCSUM_TUNE_PKT_BOUND     = 21,  /* strided packet batches (run-stream form): which bytes of a slot
+                                         are read. 0 = the whole slot (pkt_len bytes), 1 = the first
+                                         pieces whole, then only each datagram's parsed extent, 2 = the
+                                         parse first, then only the parsed extents; -1 = the default (2) */
+    NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory Rx batches with n_chunks 0 of <= 4096 frames whose
+                                         ring is pinned host memory: 1 (default) the kernel reads the ring
+                                         in place and the host polls a completion word; 0 = the copy
+                                         pipeline (H2D, kernel, D2H, stream synchronisation)           */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

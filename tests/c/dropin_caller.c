@@ -10,7 +10,8 @@
  *   - NetUtil_MI355X_ChainToSpans against the caller's own concatenation of the chain,
  *   - the four functions against an RFC 1071 sum of that concatenation written here,
  *   - the error paths (invalid protocol; with DBG: NULL, size 0, zero-length chain, ix NONE),
- *   - two threads calling the drop-in at once (each its own chains).
+ *   - two threads calling the drop-in at once (each its own chains), their first CRC calls racing
+ *     for the host table's one-time build (the tsan variant checks for data races).
  * Without a GPU every device call must FAIL with NET_UTIL_ERR_MI355X_DEV (no CPU fallback); with
  * one (NETCSUM_EXPECT_GPU=1) every call must succeed and match. Exit status 0 = all checks passed.
  */
@@ -287,10 +288,22 @@ static void check_crc(void)
     CHECK(NetUtil_32BitReflect(0x12345678u) == 0x1E6A2C48u, "Reflect(0x12345678)");
 }
 
+static pthread_barrier_t g_start;
+
+/* Both threads start together, so their first CRC calls race for the host table's one-time build
+ * (pthread_once in net_util_mi355x.c); the -fsanitize=thread variant (tsan) checks that race and the
+ * chain walks for data races. */
 static void *thread_main(void *arg)
 {
-    uint32_t t = (uint32_t)(uintptr_t)arg, k;
-    (void)t;
+    uint32_t t = (uint32_t)(uintptr_t)arg, k, i;
+    uint8_t buf[300];
+    NET_ERR err;
+    pthread_barrier_wait(&g_start);
+    for (k = 0; k < 64; ++k) {
+        for (i = 0; i < sizeof buf; ++i) buf[i] = (uint8_t)(i * 7u + k + t);
+        CHECK(NetUtil_32BitCRC_Calc(buf, 6u + k * 4u, &err) == crc_bitwise(buf, 6u + k * 4u) &&
+              (unsigned)err == NET_UTIL_ERR_NONE, "thread %u CRC %u", t, k);
+    }
     for (k = 0; k < 40; ++k) check_chain(1u + (k % 9u) * 7u, (uint16_t)((k & 1u) ? 12u : 11u));
     NetUtil_MI355X_ThreadRelease();
     return NULL;
@@ -304,15 +317,18 @@ int main(void)
     uint32_t i, j;
     pthread_t th[2];
     g_expect_gpu = e && e[0] == '1';
+    /* two host threads on the same device, each with its own chains and context, started first so
+     * that they make the process's first CRC calls */
+    pthread_barrier_init(&g_start, NULL, 2);
+    for (i = 0; i < 2; ++i) pthread_create(&th[i], NULL, thread_main, (void *)(uintptr_t)i);
+    for (i = 0; i < 2; ++i) pthread_join(th[i], NULL);
+    pthread_barrier_destroy(&g_start);
     for (i = 0; i < sizeof lens / sizeof lens[0]; ++i) {
         for (j = 0; j < sizeof plens / sizeof plens[0]; ++j) check_chain(lens[i], plens[j]);
     }
     check_headers();
     check_errors();
     check_crc();
-    /* two host threads on the same device, each with its own chains and context */
-    for (i = 0; i < 2; ++i) pthread_create(&th[i], NULL, thread_main, (void *)(uintptr_t)i);
-    for (i = 0; i < 2; ++i) pthread_join(th[i], NULL);
     NetUtil_MI355X_ThreadRelease();
     printf("%s checks=%d failed=%d device_ok=%d device_missing=%d\n", g_fail ? "FAIL" : "ok",
            g_checks, g_fail, g_dev_ok, g_dev_missing);

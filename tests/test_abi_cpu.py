@@ -110,7 +110,10 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(21, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(23, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_ZERO_COPY, 2) == 219       # 0 or 1
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, 3) == 219             # -1..2
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, -1) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_VARLEN_RUN_BYTES, -2) == 219     # -1 .. 2^20
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_HDR_BURST, 2) == 219             # 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CRC_KERNEL, 4) == 219            # 0..3
@@ -164,6 +167,12 @@ def test_binding_rejects_undersized_buffers_before_launch():
         netcsum.batch_strided(seg, 100, 100, ph, 12, 12, 10, out, 0, stream=0)      # 120 B pseudo > 100
     with pytest.raises(ValueError):
         netcsum.batch_varlen(seg, np.zeros(9, np.uint64), np.zeros(10, np.uint16), None, 0, 0, 10, out, 0, stream=0)
+    # host-memory varlen: pseudo-headers and the segments' extent are checked too (the C side copies them)
+    off, ln = np.arange(10, dtype=np.uint64) * 90, np.full(10, 90, np.uint16)
+    with pytest.raises(ValueError):
+        netcsum.batch_varlen_host(seg, off, ln, ph, 12, 12, 10, out)                 # 120 B pseudo > 100
+    with pytest.raises(ValueError):
+        netcsum.batch_varlen_host(seg[:899], off, ln, None, 0, 0, 10, out)           # extent 900 B > 899
 
 
 def test_host_memory_forms_check_arguments_before_device_work():

@@ -7,7 +7,9 @@
 * host/net_util_mi355x.c compiles -Wall -Wextra -Werror -pedantic in both modes — standalone and
   -DNETCSUM_IN_STACK against stack headers whose NET_BUF layout differs from the template mirror —
   with and without the NET_ERR_CFG_ARG_CHK_DBG_EN checks (tests/c/Makefile);
-* a plain C caller (tests/c/dropin_caller.c) runs every variant under -fsanitize=address,undefined:
+* a plain C caller (tests/c/dropin_caller.c) runs every variant under -fsanitize=address,undefined
+  (and once under -fsanitize=thread: two threads racing for the CRC table's one-time build, then
+  walking chains):
   chains of 0-1000 buffers walked and compared with its own concatenation, the error paths of
   net_util.c:168-179,1566-1577,1637-1672 through the drop-in, two threads at once; without a GPU
   every device call must fail with NET_UTIL_ERR_MI355X_DEV (no fallback);
@@ -24,7 +26,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/Source"
 CDIR = os.path.join(REPO, "tests", "c")
-VARIANTS = ["standalone_asan", "dbg_asan", "instack_asan", "instack_dbg_asan", "burst_asan", "burst_instack_asan"]
+VARIANTS = ["standalone_asan", "dbg_asan", "instack_asan", "instack_dbg_asan", "burst_asan", "burst_instack_asan", "tsan"]
 FUNCS = ["NetUtil_16BitOnesCplChkSumHdrCalc", "NetUtil_16BitOnesCplChkSumHdrVerify",
          "NetUtil_16BitOnesCplChkSumDataCalc", "NetUtil_16BitOnesCplChkSumDataVerify",
          "NetUtil_32BitCRC_Calc", "NetUtil_32BitCRC_CalcCpl", "NetUtil_32BitReflect"]
@@ -71,12 +73,13 @@ def callers():
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_c_caller_under_sanitizers(callers, variant):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
-               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1:exitcode=66")
     env.pop("NETCSUM_EXPECT_GPU", None)
     r = subprocess.run([callers[variant]], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert r.stdout.startswith("ok "), r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+    assert "ThreadSanitizer" not in r.stderr
 
 
 def test_burst_caller_requires_the_offload_configuration():

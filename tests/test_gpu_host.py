@@ -181,3 +181,79 @@ def test_tx_host_records_every_kernel_form(kernel, passes, chunks):
     assert bad.size == 0, [(int(j), (int(j) - lead) // stride, (int(j) - lead) % stride) for j in bad[:8]]
     assert np.array_equal(fl, want_f)
     assert (want_f & op.L4_CHECKED).any() and (want_f & op.MALFORMED).any()
+
+
+@pytest.mark.parametrize("n", [1, 2, 17, 64, 256, 4096, 4097])
+@pytest.mark.parametrize("form", ["strided", "offlen"])
+def test_rx_burst_host_zero_copy(n, form):
+    """NIC-burst sizes with n_chunks 0 from a pinned ring: the kernel reads the ring in place and the
+    host polls a completion word (rx_burst_zero_copy, up to 4096 frames; 4097 takes the copy path);
+    the same results as the copy pipeline (TUNE_BURST_ZERO_COPY 0), a pageable ring (copy path) and
+    the oracle, for RxBurstHost and RxValidateIPHost; the ring is never written."""
+    rng = random.Random(900 + n + (form == "offlen"))
+    stride = 1520
+    pkts = [p[:stride - 14] for p in _mixed(rng, n, 1400)]
+    buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
+    for i, p in enumerate(pkts):
+        buf[i * stride + 14:i * stride + 14 + len(p)] = np.frombuffer(p, np.uint8)
+    if form == "strided":
+        frames = [bytes(buf[i * stride + 14:(i + 1) * stride]) for i in range(n)]
+        kw = {"stride": stride, "pkt_len": stride - 14}
+        base = lambda b: b[14:]                                     # noqa: E731
+    else:
+        offs = np.arange(n, dtype=np.uint64) * stride + 14
+        lens = np.array([max(len(p), 46) for p in pkts], np.uint16)
+        frames = [bytes(buf[o:o + m]) for o, m in zip(offs.tolist(), lens.tolist())]
+        kw = {"off": offs, "lens": lens}
+        base = lambda b: b                                          # noqa: E731
+    want_f = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
+    want_a = np.array([netcsum.rx_action(int(x), oo.transport_proto(f), len(f) and f[0] >> 4 == 6)
+                       for x, f in zip(want_f, frames)], np.uint8)
+    for zc, ring in ((1, _pinned(buf)), (0, _pinned(buf)), (1, buf.copy())):
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
+        try:
+            act = np.full(n, 0xEE, np.uint8)
+            fl = np.zeros(n, np.uint8)
+            netcsum.rx_burst_host(base(ring), n, act, flags=fl, **kw)
+            assert np.array_equal(act, want_a) and np.array_equal(fl, want_f), (zc, type(ring))
+            fl2 = np.zeros(n, np.uint8)
+            netcsum.rx_validate_ip_host(base(ring), n, fl2, **kw)
+            assert np.array_equal(fl2, want_f)
+            act2 = np.full(n, 0xEE, np.uint8)
+            netcsum.rx_burst_host(base(ring), n, act2, **kw)           # actions only
+            assert np.array_equal(act2, want_a)
+        finally:
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 1)
+        r = ring.numpy() if hasattr(ring, "numpy") else ring
+        assert np.array_equal(r, buf)
+
+
+def test_rx_burst_host_zero_copy_many_calls_and_threads():
+    """Back-to-back zero-copy bursts reuse one completion word per thread (tags never repeat a stale
+    value), from two threads at once, each with its own ring."""
+    import threading
+    errs = []
+
+    def worker(seed):
+        try:
+            rng = random.Random(seed)
+            n, stride = 48, 1520
+            for it in range(60):
+                pkts = [p[:stride] for p in _mixed(rng, n, 1400)]
+                buf = np.frombuffer(rng.randbytes(n * stride), np.uint8).copy()
+                for i, p in enumerate(pkts):
+                    buf[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
+                want = np.array([op.rx_validate_ip(bytes(buf[i * stride:(i + 1) * stride])) for i in range(n)], np.uint8)
+                fl = np.zeros(n, np.uint8)
+                netcsum.rx_validate_ip_host(_pinned(buf), n, fl, stride=stride, pkt_len=stride)
+                if not np.array_equal(fl, want):
+                    errs.append((seed, it))
+            netcsum.thread_release()
+        except Exception as e:                                        # noqa: BLE001
+            errs.append(repr(e))
+    th = [threading.Thread(target=worker, args=(s,)) for s in (1, 2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs

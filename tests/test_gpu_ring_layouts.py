@@ -1,0 +1,205 @@
+"""GPU parity of the packet batches on NIC-ring layouts, against the packet oracle
+(oracle/oracle_packets.py): frames of mixed sizes in fixed-size slots — the reference's pool
+buffers (Cfg/Template/net_dev_cfg.c:146-149: 1518-B buffers, 4-B aligned, so 1520-B slots; the
+IPv4 header after a 14-B Ethernet header) and 2-KiB slots with the header at +64 — passed either
+strided with the slot's present bytes as pkt_len, or by per-frame offset/length descriptors (the
+frame length the driver reports, IF/net_if.c:6593, minus the Ethernet header; at least 46 B).
+
+The strided form runs under every NETCSUM_TUNE_PKT_BOUND: 0 reads whole slots, 1 and 2 read only
+each datagram's parsed extent (netcsum_pktstream.hip bounded_voff). The bytes a bounded stream
+skips are random here, so a kernel that summed any of them would disagree with the oracle; the bytes
+outside the checksum fields must come back untouched by Tx."""
+import random
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle_packets as op
+from packets import KINDS, KINDS6, make_packet, make_packet_v6
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _defaults():
+    def reset():
+        netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
+        netcsum.tune(netcsum.TUNE_TILE, -1)
+        netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
+        netcsum.tune(netcsum.TUNE_CHUNKS, 0)
+    reset()
+    yield
+    reset()
+
+
+def _frame(rng, v6=False):
+    """A datagram of the ring's size mix (ACK-sized / 576 B / full size), or a random kind."""
+    r = rng.random()
+    if r < 0.45:
+        payload = rng.randint(0, 12)
+    elif r < 0.75:
+        payload = rng.randint(500, 560)
+    elif r < 0.85:
+        payload = rng.randint(1400, 1460)
+    else:
+        payload = rng.randint(0, 1460)
+    if v6:
+        return make_packet_v6(rng, rng.choice(KINDS6), payload=payload)
+    kind = rng.choice(KINDS + ["tcp", "tcp", "udp"])
+    return make_packet(rng, kind, payload=payload)
+
+
+def _ring(rng, n, slot, lead, v6mix=False):
+    buf = np.frombuffer(rng.randbytes(n * slot + 64), np.uint8).copy()
+    lens = np.zeros(n, np.uint16)
+    for i in range(n):
+        p = _frame(rng, v6=v6mix and rng.random() < 0.5)[: slot - lead]
+        o = i * slot + lead
+        buf[o:o + len(p)] = np.frombuffer(p, np.uint8)
+        lens[i] = max(len(p), 46) if rng.random() < 0.95 else rng.randint(0, len(p))   # a few truncated
+    return buf, lens
+
+
+def _want(buf, n, slot, lead, present, udp_tx_csum, lens=None):
+    rx = np.zeros(n, np.uint8)
+    tx = buf.copy()
+    txf = np.zeros(n, np.uint8)
+    for i in range(n):
+        o = i * slot + lead
+        m = present if lens is None else int(lens[i])
+        pkt = bytes(buf[o:o + m])
+        rx[i] = op.rx_validate(pkt)
+        q, txf[i] = op.tx_finalize(pkt, udp_tx_csum)
+        tx[o:o + m] = np.frombuffer(q, np.uint8)
+    return rx, tx, txf
+
+
+def _want_ip(buf, n, slot, lead, present, udp_tx_csum):
+    rx = np.zeros(n, np.uint8)
+    tx = buf.copy()
+    txf = np.zeros(n, np.uint8)
+    for i in range(n):
+        o = i * slot + lead
+        pkt = bytes(buf[o:o + present])
+        rx[i] = op.rx_validate_ip(pkt)
+        q, txf[i] = op.tx_finalize_ip(pkt, udp_tx_csum)
+        tx[o:o + present] = np.frombuffer(q, np.uint8)
+    return rx, tx, txf
+
+
+def _check(got, want, what):
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (what, [(int(i), int(got[i]), int(want[i])) for i in bad[:6]])
+
+
+@pytest.mark.parametrize("bound", [0, 1, 2])
+@pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64), (1536, 1)])
+@pytest.mark.parametrize("passes", [1, 2])
+def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    rng = random.Random(slot * 7 + lead * 3 + bound)
+    n, present = 1500, slot - lead
+    buf, _ = _ring(rng, n, slot, lead)
+    rx_w, tx_w, txf_w = _want(buf, n, slot, lead, present, True)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv4(b[lead:], n, f, stride=slot, pkt_len=present)
+    torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith("pkt_stream_kernel"), netcsum.last_launch()
+    _check(f.cpu().numpy(), rx_w, "rx")
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b[lead:], n, ft, stride=slot, pkt_len=present)
+    torch.cuda.synchronize()
+    _check(b.cpu().numpy(), tx_w, "tx bytes")
+    _check(ft.cpu().numpy(), txf_w, "tx flags")
+
+
+@pytest.mark.parametrize("bound", [0, 1, 2])
+@pytest.mark.parametrize("spw", [1, 8, 64])
+def test_mixed_version_ring_every_bound_vs_oracle(bound, spw):
+    """IPv4 and IPv6 frames in one 1520-B-slot ring (RxValidateIP / TxFinalizeIP), runs of 1..64."""
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
+    netcsum.tune(netcsum.TUNE_TILE, spw)
+    rng = random.Random(1000 + 10 * bound + spw)
+    n, slot, lead = 900, 1520, 14
+    present = slot - lead
+    buf, _ = _ring(rng, n, slot, lead, v6mix=True)
+    rx_w, tx_w, txf_w = _want_ip(buf, n, slot, lead, present, True)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ip(b[lead:], n, f, stride=slot, pkt_len=present)
+    torch.cuda.synchronize()
+    _check(f.cpu().numpy(), rx_w, "rx")
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ip(b[lead:], n, ft, stride=slot, pkt_len=present)
+    torch.cuda.synchronize()
+    _check(b.cpu().numpy(), tx_w, "tx bytes")
+    _check(ft.cpu().numpy(), txf_w, "tx flags")
+
+
+@pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64)])
+def test_offset_length_ring_vs_oracle(slot, lead):
+    """The same rings by per-frame descriptors: each frame's reported length, some truncated."""
+    rng = random.Random(77 + slot)
+    n = 1500
+    buf, lens = _ring(rng, n, slot, lead)
+    rx_w, tx_w, txf_w = _want(buf, n, slot, lead, None, True, lens=lens)
+    b = torch.from_numpy(buf).to(DEV)
+    off = torch.from_numpy((np.arange(n, dtype=np.int64) * slot + lead)).to(DEV)
+    ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ipv4(b, n, f, off=off, lens=ln)
+    torch.cuda.synchronize()
+    _check(f.cpu().numpy(), rx_w, "rx")
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tx_finalize_ipv4(b, n, ft, off=off, lens=ln)
+    torch.cuda.synchronize()
+    _check(b.cpu().numpy(), tx_w, "tx bytes")
+    _check(ft.cpu().numpy(), txf_w, "tx flags")
+
+
+def test_bounded_stream_full_size_ring_properties():
+    """1 M frames of the 40/576/1500-B mix in 1520-B slots (the probe's ring, tools/ring_layouts.py
+    shape, built here): Tx under every bound writes the same bytes, then every frame verifies; a
+    corrupted byte inside a datagram is caught, one in a slot's unused tail is not read."""
+    n, slot, lead = 1 << 20, 1520, 14
+    rng = np.random.default_rng(3)
+    sizes = np.array([40, 576, 1500])[rng.choice(3, size=n, p=[7 / 12, 4 / 12, 1 / 12])]
+    b = torch.randint(0, 256, (n * slot + 64,), dtype=torch.uint8, device=DEV)
+    h = rng.integers(0, 256, size=(n, 40), dtype=np.uint8)
+    udp = sizes == 576
+    h[:, 0], h[:, 1], h[:, 2], h[:, 3] = 0x45, 0, sizes >> 8, sizes & 0xFF
+    h[:, 6], h[:, 7], h[:, 9], h[:, 10], h[:, 11] = 0x40, 0, np.where(udp, 17, 6), 0, 0
+    h[:, 32] = np.where(udp, h[:, 32], 0x50)
+    h[:, 24], h[:, 25] = np.where(udp, (sizes - 20) >> 8, h[:, 24]), np.where(udp, (sizes - 20) & 0xFF, h[:, 25])
+    b[: n * slot].view(n, slot)[:, lead:lead + 40] = torch.from_numpy(h).to(DEV)
+    base = b[lead:]
+    outs = []
+    for bound in (0, 1, 2):
+        netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
+        c = b.clone()
+        netcsum.tx_finalize_ipv4(c[lead:], n, None, stride=slot, pkt_len=slot - lead)
+        outs.append(c)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    b.copy_(outs[2])
+    del outs
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
+    netcsum.rx_validate_ipv4(base, n, f, stride=slot, pkt_len=slot - lead)
+    torch.cuda.synchronize()
+    assert bool(((f & 0x07) == 0x07).all().item())
+    # corrupt one payload byte inside datagram k, and one byte past the end of datagram j
+    k, j = 12345, int(np.nonzero(sizes == 40)[0][100])
+    bv = b[: n * slot].view(n, slot)
+    bv[k, lead + int(sizes[k]) - 1] ^= 0x5A
+    bv[j, lead + 60] ^= 0xA5
+    netcsum.rx_validate_ipv4(base, n, f, stride=slot, pkt_len=slot - lead)
+    torch.cuda.synchronize()
+    fl = f.cpu().numpy()
+    assert (fl[k] & 0x07) == 0x05                                # L4 checked, not OK
+    assert (np.delete(fl, k) & 0x07 == 0x07).all()

@@ -8,8 +8,10 @@
  * TxBurst. Per burst size n, the median wall time of 300 calls (after 20 warm-up calls) of
  *   rx_dev / tx_dev    RxBurst / TxBurst on a device-resident ring + hipStreamSynchronize
  *   rx_host / tx_host  RxBurstHost / TxBurstHost on a pinned host ring in one chunk, which return
- *                      with the results in host memory (_auto: n_chunks 0, the library's choice;
- *                      from 1024 frames also in 2-16 chunks: _cK)
+ *                      with the results in host memory (_auto: n_chunks 0, the library's choice —
+ *                      up to 4096 frames the kernel reads the pinned ring in place and the host
+ *                      polls a completion word; _auto_copy: the same with NETCSUM_TUNE_BURST_ZERO_COPY
+ *                      0; from 1024 frames also in 2-16 chunks: _cK)
  * and a check that every Rx action is DELIVER. One JSON line per n on stdout.
  *
  * Built here (the binary travels with the tree; tools/build/ is git-ignored), run on the GPU box:
@@ -145,7 +147,7 @@ static double time_us(kind_t k, uint32_t n)
 
 int main(void)
 {
-    static const uint32_t sizes[] = {1u, 16u, 64u, 256u, 1024u, 4096u, 16384u, 65536u, 262144u};
+    static const uint32_t sizes[] = {1u, 10u, 16u, 32u, 64u, 128u, 256u, 1024u, 4096u, 16384u, 65536u, 262144u};
     const size_t bytes = (size_t)NMAX * SLOT;
     uint32_t i, s;
     HIP_OK(hipSetDevice(0));
@@ -176,12 +178,18 @@ int main(void)
         printf("{\"frames\": %u, \"rx_dev_sync_us\": %.2f, \"tx_dev_sync_us\": %.2f, \"rx_host_us\": %.2f, "
                "\"tx_host_us\": %.2f, \"all_delivered\": %s", n, rx_dev, tx_dev, rx_host, tx_host, ok ? "true" : "false");
         g_chunks = 0u;                                          /* the library's choice */
+        memset(g_hact, 0xEE, NMAX);
         printf(", \"rx_host_us_auto\": %.2f, \"tx_host_us_auto\": %.2f", time_us(RX_HOST, n), time_us(TX_HOST, n));
+        for (i = 0; i < n; ++i) ok &= g_hact[i] == NETCSUM_RX_DELIVER;
+        /* n_chunks 0 without the zero-copy burst path (the copy pipeline in one chunk) */
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 0));
+        printf(", \"rx_host_us_auto_copy\": %.2f", time_us(RX_HOST, n));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 1));
         for (g_chunks = 2u; g_chunks <= 16u && n >= 1024u; g_chunks *= 2u) {
             printf(", \"rx_host_us_c%u\": %.2f", g_chunks, time_us(RX_HOST, n));
             printf(", \"tx_host_us_c%u\": %.2f", g_chunks, time_us(TX_HOST, n));
         }
-        printf("}\n");
+        printf(", \"all_delivered_auto\": %s}\n", ok ? "true" : "false");
         fflush(stdout);
         if (!ok) return 1;
     }

@@ -13,6 +13,10 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
        in one 64-B line)
   rx_sNNNN / tx_sNNNN  the 1500-B datagrams at stride NNNN (1500 = packed), 1500 B present
   rxb / txb  the offload-seam bursts (RxBurst / TxBurst) on 1 M x 1500-B alternating IPv4 / IPv6
+  rx_ring / tx_ring  1 M mixed 40/576/1500-B datagrams (7:4:1) in 1520-B slots at +14, strided,
+       pkt_len 1506; rx_ringv / tx_ringv the same ring by offset/length descriptors; rx_nb2kv /
+       tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
+  suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run (e.g. rx_ring.b0.s32)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
@@ -32,9 +36,33 @@ from bench import SEED, c2_pseudo_headers  # noqa: E402
 def main():
     name = sys.argv[1]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    # suffixes: ".bN" = NETCSUM_TUNE_PKT_BOUND N, ".sN" = TUNE_TILE N (packets per wave run)
+    for part in name.split(".")[1:]:
+        if part[:1] == "b":
+            netcsum.tune(netcsum.TUNE_PKT_BOUND, int(part[1:]))
+        elif part[:1] == "s":
+            netcsum.tune(netcsum.TUNE_TILE, int(part[1:]))
+    name = name.split(".")[0]
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
-    if name in ("c2", "c5"):
+    if name in ("rx_ring", "tx_ring", "rx_ringv", "tx_ringv", "rx_nb2kv", "tx_nb2kv"):
+        # the NIC-ring layouts of tools/ring_layouts.py: mixed 40/576/1500-B datagrams in 1520-B
+        # slots at +14 (ring) or 1500-B datagrams in 2-KiB slots at +64 (nb2k); strided with the
+        # slot's present bytes as pkt_len, or "v": offset/length descriptors (frame length - 14)
+        import ring_layouts as rl
+        n = 1 << 20
+        r = (rl.mixed_ring(torch, netcsum, dev, n) if "ring" in name else rl.uniform_ring(torch, netcsum, dev, n, 2048, 64))
+        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        kw = ({"off": r["off"], "lens": r["lens"]} if name.endswith("v") else {"stride": r["slot"], "pkt_len": r["present"]})
+        base = r["buf"] if name.endswith("v") else r["base"]
+        netcsum.tx_finalize_ipv4(base, n, None, stream=st, **kw)
+        if name.startswith("tx"):
+            fn = lambda: netcsum.tx_finalize_ipv4(base, n, None, stream=st, **kw)  # noqa: E731
+            algo = r["datagram_bytes"] + 4 * n
+        else:
+            fn = lambda: netcsum.rx_validate_ipv4(base, n, flags, stream=st, **kw)  # noqa: E731
+            algo = r["datagram_bytes"] + n
+    elif name in ("c2", "c5"):
         n, L = (1 << 20) if name == "c2" else (1 << 24), 1500
         seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(seg, n * L, SEED, 0)

@@ -33,6 +33,8 @@ thread_local netcsum::TuneKnob g_tune_chunks{0};
 thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read probe by default
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
+thread_local netcsum::TuneKnob g_tune_burst_zc{1};              // host bursts read pinned rings in place
+thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto (2), 0, 1, 2
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
@@ -295,8 +297,11 @@ NET_ERR check_op(NETCSUM_OP op, const void* d_pseudo, CPU_INT16U pseudo_len) {
 // A lease records an event on the stream after the launches that use its buffer; evicting (least
 // recently used, beyond kScratchSlots) or growing a buffer waits for that event — never for the whole
 // device — and a new lease whose earlier launches are still pending makes the stream wait for it, so
-// a stream created with the handle of a destroyed one whose work is still running cannot overtake it. Under stream capture no event is recorded and the
-// slot is pinned (the captured graph keeps its address): capture needs one uncaptured call first.
+// a stream created with the handle of a destroyed one whose work is still running cannot overtake it.
+// Under stream capture no event is recorded and the slot is pinned (the captured graph keeps its
+// address): capture needs one uncaptured call first. Later uncaptured calls on that stream get a slot
+// of their own. A graph's replays share its pinned buffer with each other, so replays of one graph
+// must be ordered (one stream, or events) — as for any graph that writes a buffer.
 constexpr int kScratchSlots = 16;
 struct ScratchSlot {
     int                dev = -1;
@@ -364,7 +369,9 @@ public:
         ScratchSlot* hit = nullptr;
         ScratchSlot* lru = nullptr;
         for (ScratchSlot& sl : c.slots) {
-            if (sl.p != nullptr && sl.dev == dev && sl.stream == st) {
+            // a slot pinned by a capture belongs to its graph: a direct (uncaptured) call on the same
+            // stream takes a slot of its own, so it can grow it and never shares the graph's buffer
+            if (sl.p != nullptr && sl.dev == dev && sl.stream == st && (capturing_ || !sl.pinned)) {
                 hit = &sl;
                 break;
             }
@@ -478,9 +485,14 @@ struct HostCtx {
     size_t               pipe_cap = 0;
     uint8_t*             h_pipe[3] = {nullptr, nullptr, nullptr};   // pinned descriptor staging per slot
     size_t               hpipe_cap = 0;
+    // zero-copy bursts (burst_zero_copy): device results, and coherent pinned memory holding the
+    // completion word, the results the completion kernel copies out, and the burst's descriptors
+    uint8_t*             d_burst = nullptr;
+    uint8_t*             h_burst = nullptr;
+    uint8_t*             h_burst_dev = nullptr;
 
     bool empty() const {
-        if (stream || h_stage || d_stage || d_sum || h_sum) return false;
+        if (stream || h_stage || d_stage || d_sum || h_sum || d_burst || h_burst) return false;
         for (int j = 0; j < 3; ++j) {
             if (pstream[j] || d_pipe[j] || h_pipe[j]) return false;
         }
@@ -504,6 +516,8 @@ struct HostCtx {
         if (d_stage) (void)hipFree(d_stage);
         if (d_sum) (void)hipFree(d_sum);
         if (h_sum) (void)hipHostFree(h_sum);
+        if (d_burst) (void)hipFree(d_burst);
+        if (h_burst) (void)hipHostFree(h_burst);
         for (int j = 0; j < 3; ++j) {
             if (pstream[j]) (void)hipStreamDestroy(pstream[j]);
             if (d_pipe[j]) (void)hipFree(d_pipe[j]);
@@ -581,6 +595,20 @@ NET_ERR ensure_pipe(HostCtx& c, size_t dev_bytes, size_t host_bytes) {
 
 size_t al256(size_t x) { return (x + 255u) & ~(size_t)255u; }
 
+// A host-memory batch that returns early (any error) first waits for its three pipeline streams, so
+// no copy into the caller's memory is still in flight when the call returns. (A Tx batch that fails
+// may leave the caller's buffer with some chunks finalized and others not.)
+struct PipeDrainOnExit {
+    HostCtx& c;
+    bool     done = false;
+    ~PipeDrainOnExit() {
+        if (done) return;
+        for (int j = 0; j < 3; ++j) {
+            if (c.pstream[j]) (void)hipStreamSynchronize(c.pstream[j]);
+        }
+    }
+};
+
 // One chunk of a host-memory batch: items [s0, s0 + ns) whose bytes are [lo, hi) of the caller's buffer.
 struct HostChunk {
     uint32_t s0, ns;
@@ -589,9 +617,9 @@ struct HostChunk {
 
 // Chunks of about n / n_chunks items each; items of a strided batch (h_off == NULL) are
 // [i * stride, i * stride + len), of an offset/length batch [h_off[i], h_off[i] + h_len[i]).
-// Returns the largest chunk's byte span; *disjoint = no two chunks' spans overlap.
+// Returns the largest chunk's byte span.
 uint64_t plan_chunks(const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, uint32_t len, uint32_t n,
-                     uint32_t n_chunks, std::vector<HostChunk>& out, bool* disjoint) {
+                     uint32_t n_chunks, std::vector<HostChunk>& out) {
     if (n_chunks == 0) n_chunks = 1;
     if (n_chunks > n) n_chunks = n;
     const uint32_t per = (n + n_chunks - 1u) / n_chunks;
@@ -612,12 +640,6 @@ uint64_t plan_chunks(const uint64_t* h_off, const uint16_t* h_len, uint64_t stri
         }
         maxb = std::max<uint64_t>(maxb, k.hi - k.lo);
         out.push_back(k);
-    }
-    std::vector<HostChunk> by_lo(out);
-    std::sort(by_lo.begin(), by_lo.end(), [](const HostChunk& a, const HostChunk& b) { return a.lo < b.lo; });
-    *disjoint = true;
-    for (size_t k = 1; k < by_lo.size(); ++k) {
-        if (by_lo[k].lo < by_lo[k - 1].hi && by_lo[k].hi > by_lo[k].lo) *disjoint = false;
     }
     return maxb;
 }
@@ -968,7 +990,8 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // scratch: the records of two-pass Tx
         ScratchLease scratch;
         if (two) NC_HIP(scratch.acquire(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord)));
-        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, hs,
+        const int bound = g_tune_pkt_bound.load() < 0 ? 2 : g_tune_pkt_bound.load();
+        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d == 8 ? 8 : 4, spw, snt, tx, d == 8 ? 2 : bound, hs,
                                           two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
@@ -1022,15 +1045,20 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
     // done by the wave-per-chain form inside the combine pass).
     int g = g_tune_group.load();
     g = (g == 16 || g == 32 || g == 64) ? g : 0;
+    // The records are capped at 2^24 pieces (128 MiB per thread and stream): a larger batch runs its
+    // pieces past the cap in the wave-per-chain form inside pass 1, and a thread whose scratch cannot
+    // be allocated (or is pinned by a stream capture) takes the wave-per-chain kernel instead.
     if (g == 0 && g_tune_kernel.load() != 1) {
-        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 20, 128ull * n_chains), 0xFFFFFFFFull);
-        netcsum::set_last_launch("chain_piece_kernel<G=16,K=6,tile=64,nt> +chain_combine_kernel");
+        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 20, 128ull * n_chains), 1ull << 24);
         ScratchLease scratch;
-        NC_HIP(scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * 8u));
-        NC_HIP(netcsum::launch_chain_two_pass(a, static_cast<uint64_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
-                                              static_cast<hipStream_t>(hip_stream)));
-        NC_HIP(scratch.end());
-        return NET_UTIL_ERR_NONE;
+        if (scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * 8u) == hipSuccess) {
+            netcsum::set_last_launch("chain_piece_kernel<G=16,K=6,tile=64,nt> +chain_combine_kernel");
+            NC_HIP(netcsum::launch_chain_two_pass(a, static_cast<uint64_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
+                                                  static_cast<hipStream_t>(hip_stream)));
+            NC_HIP(scratch.end());
+            return NET_UTIL_ERR_NONE;
+        }
+        (void)hipGetLastError();                          // a failed allocation is not this launch's error
     }
     netcsum::set_last_launch(g ? "chain_batch_kernel" : "chain_wave_kernel");
     const uint32_t gpb = g ? 256u / (uint32_t)g : 4u;
@@ -1123,8 +1151,7 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
     const size_t elt = verify ? 1u : 2u;
     const bool has_ph = h_pseudo != nullptr && pseudo_len != 0;
     std::vector<HostChunk> ch;
-    bool disjoint = true;
-    const uint64_t maxb = plan_chunks(h_seg_off, h_seg_len, 0, 0, n_seg, n_chunks, ch, &disjoint);
+    const uint64_t maxb = plan_chunks(h_seg_off, h_seg_len, 0, 0, n_seg, n_chunks, ch);
     const uint32_t per = ch[0].ns;
     const size_t ph_bytes = has_ph ? (size_t)(per - 1u) * pseudo_stride + pseudo_len : 0u;
     // device slot: [bytes | offsets | lengths | pseudo-headers | outputs]; host slot: [offsets | lengths]
@@ -1132,8 +1159,7 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
     const size_t o_out = o_ph + al256(ph_bytes), dev_need = o_out + al256((size_t)per * elt);
     e = ensure_pipe(c, dev_need, al256((size_t)per * 8u) + (size_t)per * 2u);
     if (e != NET_UTIL_ERR_NONE) return e;
-    int dev = 0;
-    NC_HIP(hipGetDevice(&dev));
+    PipeDrainOnExit guard{c};
     for (size_t k = 0; k < ch.size(); ++k) {
         const HostChunk& q = ch[k];
         const int j = (int)(k % 3u);
@@ -1171,6 +1197,97 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
                               hipMemcpyDeviceToHost, st));
     }
     for (int j = 0; j < 3; ++j) NC_HIP(hipStreamSynchronize(c.pstream[j]));
+    guard.done = true;
+    return NET_UTIL_ERR_NONE;
+}
+
+// ---- zero-copy bursts (NetUtil_MI355X_RxBurstHost / RxValidateIPHost up to kBurstZC frames)
+// A driver's burst is a few to a few hundred frames (the template's Rx ring holds 10 buffers,
+// Cfg/Template/net_dev_cfg.c:147), so its cost is fixed, not bandwidth: an H2D copy, a launch, a D2H
+// copy and a stream synchronisation took 19.3 us for one frame (profiles/r3x_burst_latency.jsonl).
+// When the caller's ring is pinned (device-accessible host memory) the kernel reads it in place over
+// PCIe; its flags and actions go to device memory, and a one-wave completion kernel copies them into
+// coherent pinned memory and then stores a tagged completion word there (system-scope release, after
+// the wave's own stores); the host polls that word, as the drop-in's single-block sums do, instead of
+// synchronising the stream, and copies the results out. A pageable ring takes the copy path.
+constexpr uint32_t kBurstZC = 4096u;                    // frames
+constexpr uint64_t kBurstZCSpan = 64ull << 20;          // ring bytes the kernel may read in place
+constexpr size_t kBurstWord = 0, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
+                 kBurstOff = kBurstAct + kBurstZC, kBurstLen = kBurstOff + 8u * kBurstZC,
+                 kBurstHostBytes = kBurstLen + 2u * kBurstZC;
+
+// The device address of host bytes [h, h + span) when they are one pinned (device-mapped) host
+// allocation, else nullptr.
+static const uint8_t* pinned_alias(const void* h, uint64_t span) {
+    if (h == nullptr || span == 0) return nullptr;
+    hipPointerAttribute_t a0{}, a1{};
+    const uint8_t* last = static_cast<const uint8_t*>(h) + (span - 1u);
+    if (hipPointerGetAttributes(&a0, h) != hipSuccess || hipPointerGetAttributes(&a1, last) != hipSuccess) {
+        (void)hipGetLastError();                        // pageable memory: not an error of this call
+        return nullptr;
+    }
+    if (a0.type != hipMemoryTypeHost || a1.type != hipMemoryTypeHost || a0.devicePointer == nullptr ||
+        static_cast<const uint8_t*>(a1.devicePointer) != static_cast<const uint8_t*>(a0.devicePointer) + (span - 1u)) {
+        return nullptr;
+    }
+    return static_cast<const uint8_t*>(a0.devicePointer);
+}
+
+static NET_ERR ensure_burst(HostCtx& c) {
+    if (c.h_burst != nullptr) return NET_UTIL_ERR_NONE;
+    NC_HIP(hipMalloc(&c.d_burst, 2u * kBurstZC));
+    NC_HIP(hipHostMalloc(&c.h_burst, kBurstHostBytes, hipHostMallocMapped | hipHostMallocCoherent));
+    NC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.h_burst_dev), c.h_burst, 0));
+    return NET_UTIL_ERR_NONE;
+}
+
+// Rx over a pinned ring in place. *taken = false: the burst does not qualify (the caller takes the
+// copy path); else the call's result.
+static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t* h_off, const uint16_t* h_len,
+                                  uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags,
+                                  uint8_t* h_action, uint32_t rx_cfg, bool* taken) {
+    *taken = false;
+    if (n_pkt > kBurstZC) return NET_UTIL_ERR_NONE;
+    uint64_t span = 0;
+    if (h_off == nullptr) {
+        span = (uint64_t)(n_pkt - 1u) * stride + pkt_len;
+    } else {
+        for (uint32_t i = 0; i < n_pkt; ++i) span = std::max<uint64_t>(span, h_off[i] + h_len[i]);
+    }
+    if (span > kBurstZCSpan) return NET_UTIL_ERR_NONE;
+    const uint8_t* d_ring = pinned_alias(h_base, span);
+    if (d_ring == nullptr) return NET_UTIL_ERR_NONE;
+    *taken = true;
+    NET_ERR e = ensure_burst(c);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    const uint64_t* d_off = nullptr;
+    const uint16_t* d_len = nullptr;
+    if (h_off != nullptr) {                             // descriptors: staged in coherent pinned memory
+        std::memcpy(c.h_burst + kBurstOff, h_off, (size_t)n_pkt * 8u);
+        std::memcpy(c.h_burst + kBurstLen, h_len, (size_t)n_pkt * 2u);
+        d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
+        d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
+    }
+    uint8_t* d_fl = c.d_burst;
+    uint8_t* d_act = h_action ? c.d_burst + kBurstZC : nullptr;
+    e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, d_fl, 1u, false, 0, c.stream, d_act, rx_cfg);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (++c.seq == 0u) c.seq = 1u;
+    const uint32_t tag = c.seq;
+    volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord);
+    *w = 0ull;
+    NC_HIP(netcsum::launch_burst_done(d_fl, d_act, n_pkt, c.h_burst_dev + kBurstFlags, c.h_burst_dev + kBurstAct,
+                                      reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstWord), tag, c.stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; (uint32_t)*w != tag; ++spin) {
+        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            NC_HIP(hipStreamSynchronize(c.stream));     // reports a failed launch; else the word is there
+            if ((uint32_t)*w != tag) return dev_fail("burst completion word", hipErrorUnknown);
+            break;
+        }
+    }
+    if (h_flags) std::memcpy(h_flags, c.h_burst + kBurstFlags, n_pkt);
+    if (h_action) std::memcpy(h_action, c.h_burst + kBurstAct, n_pkt);
     return NET_UTIL_ERR_NONE;
 }
 
@@ -1206,15 +1323,19 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
     NET_ERR e = host_ctx(&cp);
     if (e != NET_UTIL_ERR_NONE) return e;
     HostCtx& c = *cp;
+    if (!tx && n_chunks == 0 && g_tune_burst_zc.load() != 0) {   // a burst from a pinned ring: in place
+        bool taken = false;
+        e = rx_burst_zero_copy(c, h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, &taken);
+        if (taken) return e;
+    }
     std::vector<HostChunk> ch;
-    bool disjoint = true;
     // n_chunks 0 = the library's choice (tools/burst_latency.c, profiles/r3x_burst_latency.jsonl): each
     // chunk adds 15-20 us per call and PCIe stays the bound, so one chunk, except Tx from 32 Ki
     // datagrams, whose host-side field write-back overlaps the later chunks' copies (262 144 frames:
     // 16 chunks 7.4 ms, one 8.4 ms)
     if (n_chunks == 0) n_chunks = tx ? std::min(16u, std::max(1u, n_pkt / 16384u)) : 1u;
     if (n_pkt / n_chunks > (1u << 28)) n_chunks = (n_pkt >> 28) + 1u;   // records: 32-bit offsets
-    const uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks, ch, &disjoint);
+    const uint64_t maxb = plan_chunks(h_off, h_len, stride, pkt_len, n_pkt, n_chunks, ch);
     const bool varlen = h_off != nullptr;
     const uint32_t per = ch[0].ns;
     // device slot: [bytes | offsets | lengths | flags | actions | field positions | records];
@@ -1225,6 +1346,7 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
     const size_t h_rec = varlen ? al256((size_t)per * 8u) + al256((size_t)per * 2u) : 0u;
     e = ensure_pipe(c, o_rec + al256(tx ? (size_t)per * 8u : 0u), h_rec + (tx ? (size_t)per * 8u : 0u));
     if (e != NET_UTIL_ERR_NONE) return e;
+    PipeDrainOnExit guard{c};
     uint8_t* hb = static_cast<uint8_t*>(h_base);
     auto drain = [&](size_t k) -> NET_ERR {                  // chunk k's stream has finished: apply its records
         NC_HIP(hipStreamSynchronize(c.pstream[k % 3u]));
@@ -1278,6 +1400,7 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
         e = drain(k);
         if (e != NET_UTIL_ERR_NONE) return e;
     }
+    guard.done = true;
     return NET_UTIL_ERR_NONE;
 }
 
@@ -1425,6 +1548,14 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_CRC_NT:
         if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_crc_nt(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_BURST_ZERO_COPY:
+        if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_burst_zc.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_PKT_BOUND:
+        if (value < -1 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_pkt_bound.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:
         if (value != 0 && value != 64 && value != 128 && value != 256) {   // __launch_bounds__(256)

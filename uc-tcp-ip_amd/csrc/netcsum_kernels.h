@@ -164,8 +164,14 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream p
 // stores at system scope, 2 release at the end of every scatter wave, 3 / 4 a write-back launch of
 // 8 / 256 workgroups after the Tx launch(es).
 void set_tx_flush(int mode);
-hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx,
+// bound (NETCSUM_TUNE_PKT_BOUND): 0 slots streamed whole, 1 refills bounded by the parsed ends, 2 parse
+// first and every piece bounded (depth 8 only with bound 2)
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec = nullptr);   // rec: two-pass Tx (records + scatter)
+// Zero-copy host bursts: one wave copies n result bytes (flags, and actions if act != nullptr) from
+// device memory into coherent pinned host memory, then stores `tag` into *word (system scope).
+hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, uint8_t* h_fl, uint8_t* h_act,
+                             unsigned long long* word, uint32_t tag, hipStream_t s);
 // IPv6 extension-header chains past the batch kernels' window (flags EXT_HDR): walked to the end and
 // finished in place (netcsum_v6walk.hip); a.flags_out holds the batch kernel's flags.
 hipError_t launch_pkt_v6_walk(const PktBatchArgs& a, bool tx, int cus, hipStream_t s);

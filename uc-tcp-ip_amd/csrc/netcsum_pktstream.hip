@@ -346,6 +346,37 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memc
     q[1] = (uint8_t)(v >> 8);
 }
 
+// Bounded stream (BND >= 1). A NIC ring's slots are larger than most of its frames: 1518 / 1520-B
+// pool buffers holding 40-B ACKs (Cfg/Template/net_dev_cfg.c:146-149, one NET_BUF per frame,
+// Source/net_buf.h:595-598, the frame length per frame from the driver, IF/net_if.c:6593), or 2-KiB
+// buffers whose present bytes the caller passes as pkt_len. Streaming the whole run fetches every
+// slot whole. Here a lane's 16-B chunk at run offset x is loaded only when it holds a byte that some
+// packet of the run sums — [lead0 + p*st, lead0 + p*st + end_p), end_p parsed in the prologue —
+// and otherwise gets the out-of-range offset (zeros, no memory request). The stream's sums only ever
+// take differences of prefixes inside [start, end) ranges, so zero-filled bytes outside them change
+// nothing. The chunk overlaps the slot of packet p0 = floor((x - lead0) / st) and perhaps the start of
+// p0 + 1 (st >= 64 > 16); their ends come from lanes p0 and p0 + 1 by ds_bpermute.
+struct RunBound {
+    uint32_t lead0, st, nres;
+    float inv_st;
+};
+
+__device__ __forceinline__ uint32_t bounded_voff(uint32_t x, const RunBound& b, uint32_t end_v) {
+    const bool before = x < b.lead0;                               // only in the run's first line
+    const uint32_t rel = x - b.lead0;
+    uint32_t p = (uint32_t)((float)(before ? 0u : rel) * b.inv_st);   // rel < 2^23: off by <= 1
+    p = (p * b.st > rel) ? p - 1u : p;
+    p = ((p + 1u) * b.st <= rel) ? p + 1u : p;
+    const uint32_t p0 = before ? 0u : p, p1 = before ? 0u : p + 1u;
+    const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p0 & 63u) << 2), (int)end_v);
+    const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p1 & 63u) << 2), (int)end_v);
+    const uint32_t s0 = b.lead0 + p0 * b.st;
+    const uint32_t s1 = b.lead0 + p1 * b.st;
+    const bool live0 = !before && p0 < b.nres && x < s0 + e0;
+    const bool live1 = p1 < b.nres && s1 < x + 16u && e1 != 0u;
+    return (live0 || live1) ? x : kOOB;
+}
+
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
 template <int VER, bool TX>
@@ -364,7 +395,9 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 }
 
 // VER 4 / 6: one IP version per batch; VER 0: per datagram by the version nibble (a mixed ring).
-template <int D, bool NT, bool TX, bool REC, int VER>
+// BND 0: every piece of the run streamed whole (the round-3 form); 1: the first D pieces whole, the
+// refills bounded by the parsed ends; 2: the parse first, then every piece bounded.
+template <int D, bool NT, bool TX, bool REC, int VER, int BND>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -387,9 +420,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     const uint32_t lane16 = 16u * lane;
 
     u32x4 dv[D];
+    if constexpr (BND < 2) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) {                              // first D pieces in flight ...
-        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+        for (int j = 0; j < D; ++j) {                          // first D pieces in flight ...
+            dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+        }
     }
 
     // ... while lane k parses packet k from its own 96-B window.
@@ -417,6 +452,13 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     // the prologue's peak to 73 = 6 waves/SIMD).
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
+    const RunBound rb{lead0, st, nres, 1.0f / (float)st};
+    if constexpr (BND == 2) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            dv[j] = buf_load16<NT>(rd, bounded_voff(((uint32_t)j << 10) + lane16, rb, end_v));
+        }
+    }
 
     uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k
     uint32_t cur = s_begin;                                    // next packet to finish
@@ -467,7 +509,8 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         for (int j = 0; j < D; ++j) {
             const uint32_t q = r * (uint32_t)D + (uint32_t)j;
             consume(q, opaque_tuple(dv[j]));
-            dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
+            const uint32_t x = ((q + (uint32_t)D) << 10) + lane16;            // past the run: zeros
+            dv[j] = buf_load16<NT>(rd, BND ? bounded_voff(x, rb, end_v) : x);
             asm volatile("" ::: "memory");
         }
     }
@@ -637,6 +680,24 @@ __global__ void __launch_bounds__(64) l2_writeback_kernel() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Completion of a zero-copy host burst (netcsum_abi.hip rx_burst_zero_copy): ONE wave, so the
+// system-scope release of the completion store waits for every result store before it (vmcnt is
+// per wave). Results are copied as whole 16-B chunks (the device buffers hold whole chunks).
+__global__ void __launch_bounds__(64) burst_done_kernel(const uint8_t* fl, const uint8_t* act, uint32_t n,
+                                                        uint8_t* h_fl, uint8_t* h_act, unsigned long long* word,
+                                                        uint32_t tag) {
+    const uint32_t chunks = (n + 15u) >> 4;
+    for (uint32_t c = threadIdx.x; c < chunks; c += 64u) {
+        reinterpret_cast<u32x4*>(h_fl)[c] = reinterpret_cast<const u32x4*>(fl)[c];
+        if (act != nullptr) {
+            reinterpret_cast<u32x4*>(h_act)[c] = reinterpret_cast<const u32x4*>(act)[c];
+        }
+    }
+    if (threadIdx.x == 0u) {
+        __hip_atomic_store(word, (unsigned long long)tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 thread_local TuneKnob g_tx_flush{-1};
 
 int tx_flush_mode() {
@@ -667,7 +728,7 @@ hipError_t launch_tx_flush(hipStream_t s) {
     return hipSuccess;
 }
 
-template <int D, bool NT, bool TX, int VER>
+template <int D, bool NT, bool TX, int VER, int BND>
 hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
     PktBatchArgs a = a0;
     // no piece touch by default: the header prologue already loads each packet's first bytes with
@@ -677,13 +738,13 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     if (TX && rec != nullptr) {
-        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         e = launch_scatter<VER != 4>(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
     hipError_t e = hipGetLastError();
     return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }
@@ -694,6 +755,12 @@ hipError_t launch_pkt_field_gather(const PktBatchArgs& a, uint64_t* rec_out, hip
     if (a.n == 0u) return hipSuccess;
     if (a.fieldpos_out == nullptr || rec_out == nullptr) return hipErrorInvalidValue;
     hipLaunchKernelGGL(pkt_field_gather_kernel, dim3((unsigned)(((uint64_t)a.n + 255u) / 256u)), dim3(256), 0, s, a, rec_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, uint8_t* h_fl, uint8_t* h_act,
+                             unsigned long long* word, uint32_t tag, hipStream_t s) {
+    hipLaunchKernelGGL(burst_done_kernel, dim3(1), dim3(64), 0, s, fl, act, n, h_fl, h_act, word, tag);
     return hipGetLastError();
 }
 
@@ -708,17 +775,20 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver) {
            a.stride <= a.len_u + 64u && (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
 
-hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, hipStream_t s,
-                             PktTxRecord* rec) {
-    if (spw == 0u || spw > kMaxRunPkts) return hipErrorInvalidValue;
-#define NETCSUM_P(V_, D_, NT_, TX_) \
-    if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_) return launch_pkt_stream_t<D_, NT_, TX_, V_>(a, spw, s, rec);
-#define NETCSUM_PV(V_)                                                                                      \
-    NETCSUM_P(V_, 4, true, false) NETCSUM_P(V_, 4, false, false) NETCSUM_P(V_, 4, true, true)                \
-    NETCSUM_P(V_, 4, false, true) NETCSUM_P(V_, 8, true, false) NETCSUM_P(V_, 8, false, false)               \
-    NETCSUM_P(V_, 8, true, true) NETCSUM_P(V_, 8, false, true)
+hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
+                             hipStream_t s, PktTxRecord* rec) {
+    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 2) return hipErrorInvalidValue;
+    // every bound with 4 pieces in flight; 8 pieces only in the default bound (2)
+#define NETCSUM_P(V_, D_, NT_, TX_, B_)                                                                   \
+    if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_ && bound == B_)                              \
+        return launch_pkt_stream_t<D_, NT_, TX_, V_, B_>(a, spw, s, rec);
+#define NETCSUM_PB(V_, D_, B_)                                                                            \
+    NETCSUM_P(V_, D_, true, false, B_) NETCSUM_P(V_, D_, false, false, B_) NETCSUM_P(V_, D_, true, true, B_) \
+    NETCSUM_P(V_, D_, false, true, B_)
+#define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0) NETCSUM_PB(V_, 4, 1) NETCSUM_PB(V_, 4, 2) NETCSUM_PB(V_, 8, 2)
     NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
 #undef NETCSUM_PV
+#undef NETCSUM_PB
 #undef NETCSUM_P
     return hipErrorInvalidValue;
 }

@@ -44,6 +44,7 @@
 #endif
 #endif
 
+#include <pthread.h>
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -299,20 +300,25 @@ static uint32_t crc_step_table(uint32_t v)
     return v;
 }
 
+/* The 256-entry table is built once per process (pthread_once): the drop-in may be called from
+ * several host threads (one per device), and the table must be complete before any lookup. */
+static uint32_t crc_tab[256];
+static pthread_once_t crc_tab_once = PTHREAD_ONCE_INIT;
+
+static void crc_tab_build(void)
+{
+    uint32_t i;
+    for (i = 0u; i < 256u; ++i) {
+        crc_tab[i] = crc_step_table(i);
+    }
+}
+
 static uint32_t crc_host(const CPU_INT08U *p, uint32_t n)
 {
-    static uint32_t tab[256];
-    static volatile int ready = 0;
     uint32_t crc = 0xFFFFFFFFu, i;                          /* NET_UTIL_32_BIT_ONES_CPL_NEG_ZERO */
-    if (!ready) {                                           /* idempotent: racing threads write equal values */
-        for (i = 0u; i < 256u; ++i) {
-            tab[i] = crc_step_table(i);
-        }
-        __atomic_store_n(&ready, 1, __ATOMIC_RELEASE);
-    }
-    (void)__atomic_load_n(&ready, __ATOMIC_ACQUIRE);
+    (void)pthread_once(&crc_tab_once, crc_tab_build);
     for (i = 0u; i < n; ++i) {
-        crc = (crc >> 8) ^ tab[(crc ^ p[i]) & 0xFFu];       /* :518, :527 */
+        crc = (crc >> 8) ^ crc_tab[(crc ^ p[i]) & 0xFFu];   /* :518, :527 */
     }
     return crc;
 }

@@ -68,6 +68,8 @@ TUNE_CRC_LANES = 17
 TUNE_CRC_WIDE = 18
 TUNE_HDR_BURST = 19
 TUNE_VARLEN_RUN_BYTES = 20
+TUNE_PKT_BOUND = 21
+TUNE_BURST_ZERO_COPY = 22
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
@@ -595,7 +597,15 @@ def batch_varlen_host(base, seg_off, seg_len, pseudo, pseudo_stride, pseudo_len,
     if n_seg:
         _require(seg_off, 8 * n_seg, "segment offsets")
         _require(seg_len, 2 * n_seg, "segment lengths")
+        if pseudo is not None and pseudo_len:
+            _require(pseudo, (n_seg - 1) * pseudo_stride + pseudo_len, "pseudo-headers")
         _require(out, n_seg * (2 if op in (OP_DATA_CALC, OP_HDR_CALC) else 1), "out")
+        # host arrays: the segments' extent is readable here (the C side copies [min off, max off+len))
+        import numpy as _np
+        if isinstance(seg_off, _np.ndarray) and isinstance(seg_len, _np.ndarray) and _nbytes(base) is not None:
+            o = seg_off[:n_seg].view(_np.uint64)
+            ln = _np.asarray(seg_len[:n_seg]).view(_np.uint16).astype(_np.uint64)
+            _require(base, int((o + ln).max()), "segments")
     err = lib().NetUtil_MI355X_ChkSumBatchVarLenHost(_p(base), _p(seg_off), _p(seg_len), _p(pseudo), pseudo_stride,
                                                      pseudo_len, n_seg, _p(out), op, n_chunks)
     if check:
