@@ -6,7 +6,8 @@ strided with the slot's present bytes as pkt_len, or by per-frame offset/length 
 frame length the driver reports, IF/net_if.c:6593, minus the Ethernet header; at least 46 B).
 
 The strided form runs under every NETCSUM_TUNE_PKT_BOUND: 0 reads whole slots, 1 and 2 read only
-each datagram's parsed extent (netcsum_pktstream.hip bounded_voff). The bytes a bounded stream
+each datagram's parsed extent (netcsum_pktstream.hip bounded_voff), 3 (the default) only the pieces
+and 64-B sectors holding summed bytes (live pieces, dead pieces skipped). The bytes a bounded stream
 skips are random here, so a kernel that summed any of them would disagree with the oracle; the bytes
 outside the checksum fields must come back untouched by Tx."""
 import random
@@ -95,14 +96,14 @@ def _check(got, want, what):
     assert bad.size == 0, (what, [(int(i), int(got[i]), int(want[i])) for i in bad[:6]])
 
 
-@pytest.mark.parametrize("bound", [0, 1, 2])
-@pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64), (1536, 1)])
+@pytest.mark.parametrize("bound", [0, 1, 2, 3])
+@pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64), (1536, 1), (9216, 2)])
 @pytest.mark.parametrize("passes", [1, 2])
 def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
     netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
     netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
     rng = random.Random(slot * 7 + lead * 3 + bound)
-    n, present = 1500, slot - lead
+    n, present = (1500 if slot < 4096 else 300), slot - lead
     buf, _ = _ring(rng, n, slot, lead)
     rx_w, tx_w, txf_w = _want(buf, n, slot, lead, present, True)
     b = torch.from_numpy(buf).to(DEV)
@@ -118,7 +119,7 @@ def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
     _check(ft.cpu().numpy(), txf_w, "tx flags")
 
 
-@pytest.mark.parametrize("bound", [0, 1, 2])
+@pytest.mark.parametrize("bound", [0, 1, 2, 3])
 @pytest.mark.parametrize("spw", [1, 8, 64])
 def test_mixed_version_ring_every_bound_vs_oracle(bound, spw):
     """IPv4 and IPv6 frames in one 1520-B-slot ring (RxValidateIP / TxFinalizeIP), runs of 1..64."""
@@ -179,14 +180,14 @@ def test_bounded_stream_full_size_ring_properties():
     b[: n * slot].view(n, slot)[:, lead:lead + 40] = torch.from_numpy(h).to(DEV)
     base = b[lead:]
     outs = []
-    for bound in (0, 1, 2):
+    for bound in (0, 1, 2, 3):
         netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
         c = b.clone()
         netcsum.tx_finalize_ipv4(c[lead:], n, None, stride=slot, pkt_len=slot - lead)
         outs.append(c)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
-    b.copy_(outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    b.copy_(outs[3])
     del outs
     f = torch.zeros(n, dtype=torch.uint8, device=DEV)
     netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)

@@ -132,14 +132,21 @@ def test_thread_contexts_released():
 
 
 def test_scratch_buffers_many_threads_many_streams():
-    """The packet / varlen scratch (two-pass Tx records, the varlen run word) is per thread and per
-    stream (netcsum_abi.hip ScratchLease): 4 threads x 24 streams each — more streams than a
-    thread's 16 slots, so slots are evicted and re-created while launches on other streams are in
-    flight — run two-pass Tx finalize and adaptive-run varlen batches at once; every result equals
-    the oracle's."""
+    """Every scratch lease is per thread and per stream (netcsum_abi.hip ScratchLease): 4 threads x 24
+    streams each — more streams than a thread's 16 slots, so slots are evicted and re-created while
+    launches on other streams are in flight — run at once, per stream:
+      * two-pass Tx finalize (TUNE_TX_PASSES 2, per thread): the event-ordered 8-B records lease;
+      * a two-pass chain batch: the event-ordered per-piece records lease;
+      * an IPv6 lane-group Rx batch without a flags array (TUNE_KERNEL 2 around it): the event-ordered
+        deferral word + flags lease, with datagrams whose extension chains the walk pass finishes;
+      * an adaptive-run varlen batch: the unordered run-word lease.
+    Every result equals the oracle's."""
+    import struct
+
     import numpy as np
     import oracle_packets as op
-    from packets import make_packet, packed_batch
+    from chains import make_chain_batch
+    from packets import ext_body, make_packet, make_packet_v6, packed_batch
 
     rng = random.Random(77)
     stride, n_pkt = 1500, 96
@@ -153,33 +160,68 @@ def test_scratch_buffers_many_threads_many_streams():
     segs = [rng.randbytes(rng.randint(40, 3000)) for _ in range(400)]
     vbuf, voff, vlen = packed_batch(segs, rng, trailer=False)
     vwant = oracle.batch_varlen(vbuf, voff, vlen, None, 0, 0)
+    cb = make_chain_batch(rng, 64, max_pieces=12)
+    cwant = cb.expect(0)
+    v6 = []
+    for i in range(128):                                  # every 4th behind a long Destination Options header
+        inner = make_packet_v6(rng, rng.choice(["tcp", "udp", "icmp_echo"]), payload=rng.randint(24, 900))
+        if i % 4 == 0:
+            u = rng.randint(8, 30)
+            body = struct.pack("!BB", inner[6], u - 1) + ext_body(rng, 60, u * 8 - 2) + inner[40:]
+            inner = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40] + body
+        v6.append(inner)
+    v6buf, v6off, v6len = packed_batch(v6, rng)
+    v6want = np.array([op.rx_validate_v6(bytes(v6buf[o:o + n])) for o, n in zip(v6off.tolist(), v6len.tolist())], np.uint8)
+    import oracle_offload as oo
+    v6frames = [bytes(v6buf[o:o + n]) for o, n in zip(v6off.tolist(), v6len.tolist())]
+    v6act = np.array([netcsum.rx_action(int(f), oo.transport_proto(fr), True) for f, fr in zip(v6want, v6frames)],
+                     np.uint8)
     errors = []
 
     def worker(seed):
         try:
             torch.cuda.set_device(0)
+            netcsum.tune(netcsum.TUNE_TX_PASSES, 2)       # per thread: Tx records even for 96 datagrams
             streams = [torch.cuda.Stream() for _ in range(24)]
             with torch.cuda.stream(streams[0]):
                 vb = torch.from_numpy(vbuf).cuda()
                 vo = torch.from_numpy(voff.astype(np.int64)).cuda()
                 vl = torch.from_numpy(vlen.view(np.int16)).cuda()
+                cbase = torch.from_numpy(cb.base).cuda()
+                coff = torch.from_numpy(cb.piece_off.view(np.int64)).cuda()
+                clen = torch.from_numpy(cb.piece_len.view(np.int16)).cuda()
+                cfirst = torch.from_numpy(cb.chain_first.view(np.int32)).cuda()
+                cph = torch.from_numpy(cb.pseudo).cuda()
+                v6b = torch.from_numpy(v6buf).cuda()
+                v6o = torch.from_numpy(v6off.view(np.int64)).cuda()
+                v6l = torch.from_numpy(v6len.view(np.int16)).cuda()
             streams[0].synchronize()
             for rnd in range(3):
-                bufs, outs = [], []
+                res = []
                 for s in streams:
                     with torch.cuda.stream(s):
                         b = torch.from_numpy(tx_in).cuda()
                         o = torch.empty(len(segs), dtype=torch.int16, device="cuda")
+                        co = torch.empty(cb.n, dtype=torch.int16, device="cuda")
+                        act = torch.full((len(v6),), 0xEE, dtype=torch.uint8, device="cuda")
                         netcsum.tx_finalize_ipv4(b, n_pkt, stride=stride, pkt_len=stride, stream=s)
+                        netcsum.batch_chains(cbase, coff, clen, cfirst, cph, cb.pseudo_stride, cb.pseudo_len, cb.n,
+                                             co, stream=s)
+                        netcsum.tune(netcsum.TUNE_KERNEL, 2)
+                        netcsum.rx_burst(v6b, len(v6), act, off=v6o, lens=v6l, stream=s)
+                        netcsum.tune(netcsum.TUNE_KERNEL, 0)
                         netcsum.batch_varlen(vb, vo, vl, None, 0, 0, len(segs), o, stream=s)
-                        bufs.append(b)
-                        outs.append(o)
-                for s, b, o in zip(streams, bufs, outs):
+                        res.append((b, o, co, act))
+                for s, (b, o, co, act) in zip(streams, res):
                     s.synchronize()
                     if not np.array_equal(b.cpu().numpy(), tx_want):
                         errors.append((seed, rnd, "tx"))
                     if not np.array_equal(o.cpu().numpy().view(np.uint16), vwant):
                         errors.append((seed, rnd, "varlen"))
+                    if not np.array_equal(co.cpu().numpy().view(np.uint16), cwant):
+                        errors.append((seed, rnd, "chains"))
+                    if not np.array_equal(act.cpu().numpy(), v6act):
+                        errors.append((seed, rnd, "v6 lane-group rx"))
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e))
         finally:
@@ -189,7 +231,7 @@ def test_scratch_buffers_many_threads_many_streams():
     for t in ths:
         t.start()
     for t in ths:
-        t.join(timeout=100)
+        t.join(timeout=200)
     assert not any(t.is_alive() for t in ths)
     assert errors == []
 

@@ -34,7 +34,7 @@ thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read 
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 thread_local netcsum::TuneKnob g_tune_burst_zc{1};              // host bursts read pinned rings in place
-thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto (2), 0, 1, 2
+thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto (3), 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
@@ -900,7 +900,7 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                          CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, uint32_t udp_mode, bool tx,
                          int ip_ver, void* hip_stream, uint8_t* d_action = nullptr, uint32_t rx_cfg = 0u,
-                         uint32_t* d_fieldpos = nullptr) {
+                         uint32_t* d_fieldpos = nullptr, netcsum::PktTxRecord* rec_only = nullptr) {
     if (n_pkt == 0) return NET_UTIL_ERR_NONE;
     if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr && d_action == nullptr)) {
@@ -979,23 +979,35 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // Tx passes: auto = two (8-B records, then a scatter pass: 1 M x 1500 B 0.2918 against 0.2954
         // ms in one pass) from 64 Ki datagrams up, one below (a burst is then a single launch)
         const int tp = g_tune_tx_passes.load();
-        const bool two = tx && (tp == 2 || (tp == 0 && n_pkt >= 65536u));
+        const bool two = tx && (rec_only != nullptr || tp == 2 || (tp == 0 && n_pkt >= 65536u));
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
-        char desc[136];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u%s%s", d, snt ? ",nt" : "",
-                 tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, two ? " +pkt_scatter_kernel" : "",
-                 walk ? " +inline_v6_walk" : "");
+        // which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND; 3 = live pieces, whose runs span
+        // at most 128 KiB)
+        const int bound = d == 8 ? 3 : (g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load());
+        if (bound == 3) {
+            const uint64_t cap = (128u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+            spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
+        }
+        char desc[144];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s,bound=%d> block=256 pkts_per_wave=%u%s%s", d,
+                 snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", bound, spw,
+                 two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "");
         netcsum::set_last_launch(desc);
+        if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
+            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs, rec_only,
+                                              false));
+            return NET_UTIL_ERR_NONE;
+        }
         // scratch: the records of two-pass Tx
         ScratchLease scratch;
         if (two) NC_HIP(scratch.acquire(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord)));
-        const int bound = g_tune_pkt_bound.load() < 0 ? 2 : g_tune_pkt_bound.load();
-        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d == 8 ? 8 : 4, spw, snt, tx, d == 8 ? 2 : bound, hs,
+        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs,
                                           two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }
+    if (rec_only != nullptr) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;   // (callers check the domain)
     a.tile = tile >= 0 ? (uint32_t)tile : (c.grid > 0 ? 0u : 2u);      // tile 2: best Rx/Tx point (r1m sweep)
     char desc[120];
     snprintf(desc, sizeof desc, "pkt_batch_kernel<G=%d,K=%d%s,%s,v%d> block=256 tile=%u%s", c.group_lanes,
@@ -1214,7 +1226,9 @@ constexpr uint32_t kBurstZC = 4096u;                    // frames
 constexpr uint64_t kBurstZCSpan = 64ull << 20;          // ring bytes the kernel may read in place
 constexpr size_t kBurstWord = 0, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
                  kBurstOff = kBurstAct + kBurstZC, kBurstLen = kBurstOff + 8u * kBurstZC,
-                 kBurstHostBytes = kBurstLen + 2u * kBurstZC;
+                 kBurstRec = kBurstLen + 2u * kBurstZC, kBurstHostBytes = kBurstRec + 8u * kBurstZC;
+// device side: [flags | actions | Tx records]
+constexpr size_t kBurstDevRec = 2u * kBurstZC, kBurstDevBytes = kBurstDevRec + 8u * kBurstZC;
 
 // The device address of host bytes [h, h + span) when they are one pinned (device-mapped) host
 // allocation, else nullptr.
@@ -1235,9 +1249,23 @@ static const uint8_t* pinned_alias(const void* h, uint64_t span) {
 
 static NET_ERR ensure_burst(HostCtx& c) {
     if (c.h_burst != nullptr) return NET_UTIL_ERR_NONE;
-    NC_HIP(hipMalloc(&c.d_burst, 2u * kBurstZC));
+    NC_HIP(hipMalloc(&c.d_burst, kBurstDevBytes));
     NC_HIP(hipHostMalloc(&c.h_burst, kBurstHostBytes, hipHostMallocMapped | hipHostMallocCoherent));
     NC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.h_burst_dev), c.h_burst, 0));
+    return NET_UTIL_ERR_NONE;
+}
+
+// Polls the completion word of tag (2 s, then a stream synchronisation reports a failed launch).
+static NET_ERR burst_wait(HostCtx& c, uint32_t tag) {
+    volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; (uint32_t)*w != tag; ++spin) {
+        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            NC_HIP(hipStreamSynchronize(c.stream));
+            if ((uint32_t)*w != tag) return dev_fail("burst completion word", hipErrorUnknown);
+            break;
+        }
+    }
     return NET_UTIL_ERR_NONE;
 }
 
@@ -1274,20 +1302,81 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
     if (e != NET_UTIL_ERR_NONE) return e;
     if (++c.seq == 0u) c.seq = 1u;
     const uint32_t tag = c.seq;
-    volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord);
-    *w = 0ull;
+    *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
     NC_HIP(netcsum::launch_burst_done(d_fl, d_act, n_pkt, c.h_burst_dev + kBurstFlags, c.h_burst_dev + kBurstAct,
                                       reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstWord), tag, c.stream));
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 0; (uint32_t)*w != tag; ++spin) {
-        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-            NC_HIP(hipStreamSynchronize(c.stream));     // reports a failed launch; else the word is there
-            if ((uint32_t)*w != tag) return dev_fail("burst completion word", hipErrorUnknown);
-            break;
-        }
-    }
+    e = burst_wait(c, tag);
+    if (e != NET_UTIL_ERR_NONE) return e;
     if (h_flags) std::memcpy(h_flags, c.h_burst + kBurstFlags, n_pkt);
     if (h_action) std::memcpy(h_action, c.h_burst + kBurstAct, n_pkt);
+    return NET_UTIL_ERR_NONE;
+}
+
+static NET_ERR pkt_host_copy(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                             CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg,
+                             uint32_t udp_mode, bool tx, uint32_t n_chunks);
+
+// Tx over a pinned strided ring: the checksum pass reads the ring in place and writes one 8-B
+// record per datagram (PktTxRecord) to device memory — never into the ring —, the completion kernel
+// copies the records into coherent pinned memory, and the host writes the fields into its ring (as
+// the copy pipeline's gather records do). Datagrams whose IPv6 extension chain runs past the
+// kernel's window (flag EXT_HDR: walked by a later pass in the device forms) are finished by the copy
+// path afterwards, as an offset/length batch of just those datagrams. *taken as for Rx.
+static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_off, uint64_t stride, CPU_INT16U pkt_len,
+                                  uint32_t n_pkt, uint8_t* h_flags, uint32_t udp_mode, bool* taken) {
+    *taken = false;
+    if (n_pkt > kBurstZC || h_off != nullptr) return NET_UTIL_ERR_NONE;
+    netcsum::PktBatchArgs a{};
+    a.stride = stride;
+    a.len_u = pkt_len;
+    a.n = n_pkt;
+    if (!netcsum::pkt_stream_supported(a, 0) || g_tune_kernel.load() == 2) return NET_UTIL_ERR_NONE;
+    const uint64_t span = (uint64_t)(n_pkt - 1u) * stride + pkt_len;
+    if (span > kBurstZCSpan) return NET_UTIL_ERR_NONE;
+    const uint8_t* d_ring = pinned_alias(h_base, span);
+    if (d_ring == nullptr) return NET_UTIL_ERR_NONE;
+    *taken = true;
+    NET_ERR e = ensure_burst(c);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    netcsum::PktTxRecord* d_rec = reinterpret_cast<netcsum::PktTxRecord*>(c.d_burst + kBurstDevRec);
+    e = pkt_batch(d_ring, nullptr, nullptr, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
+                  nullptr, d_rec);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    if (++c.seq == 0u) c.seq = 1u;
+    const uint32_t tag = c.seq;
+    *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
+    NC_HIP(netcsum::launch_burst_done(reinterpret_cast<const uint8_t*>(d_rec), nullptr, n_pkt * 8u,
+                                      c.h_burst_dev + kBurstRec, nullptr,
+                                      reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstWord), tag, c.stream));
+    e = burst_wait(c, tag);
+    if (e != NET_UTIL_ERR_NONE) return e;
+    uint8_t* hb = static_cast<uint8_t*>(h_base);
+    const uint64_t* rec = reinterpret_cast<const uint64_t*>(c.h_burst + kBurstRec);
+    std::vector<uint64_t> walk_off;
+    for (uint32_t i = 0; i < n_pkt; ++i) {
+        const uint64_t r = rec[i];                      // PktTxRecord: vals | l4_off << 32 | flags << 48 | store << 56
+        const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
+        if (flags & NETCSUM_PKT_EXT_HDR) {
+            walk_off.push_back((uint64_t)i * stride);
+            continue;
+        }
+        uint8_t* p = hb + (uint64_t)i * stride;
+        const uint16_t ip = (uint16_t)r, l4 = (uint16_t)(r >> 16);
+        if (store & 1u) std::memcpy(p + 10, &ip, 2);
+        if (store & 2u) std::memcpy(p + ((r >> 32) & 0xFFFFu), &l4, 2);
+        if (h_flags) h_flags[i] = (uint8_t)flags;
+    }
+    if (!walk_off.empty()) {                            // the rare long IPv6 chains: the copy path
+        const uint32_t m = (uint32_t)walk_off.size();
+        std::vector<uint16_t> lens(m, pkt_len);
+        std::vector<uint8_t> fl(m);
+        e = pkt_host_copy(h_base, walk_off.data(), lens.data(), 0, 0, m, h_flags ? fl.data() : nullptr, nullptr, 0u,
+                          udp_mode, true, 1u);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        if (h_flags) {
+            for (uint32_t k = 0; k < m; ++k) h_flags[walk_off[k] / stride] = fl[k];
+        }
+    }
     return NET_UTIL_ERR_NONE;
 }
 
@@ -1311,23 +1400,13 @@ static void apply_field_records(uint8_t* h_base, const uint64_t* h_off, uint64_t
 // (fieldpos); a gather pass packs them into 8-B records, only those return D2H, and the host writes
 // the fields into its own buffer once the chunk's stream has drained (before its slot is reused,
 // and at the end) — 8 B per datagram over PCIe instead of the chunk's bytes.
-static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, CPU_INT16U pkt_len,
-                        uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg, uint32_t udp_mode, bool tx,
-                        uint32_t n_chunks) {
-    if (n_pkt == 0) return NET_UTIL_ERR_NONE;
-    if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
-    if (h_base == nullptr || (h_off != nullptr) != (h_len != nullptr) || (!tx && h_flags == nullptr && h_action == nullptr)) {
-        return NET_ERR_FAULT_NULL_PTR;
-    }
+static NET_ERR pkt_host_copy(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
+                             CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg,
+                             uint32_t udp_mode, bool tx, uint32_t n_chunks) {
     HostCtx* cp = nullptr;
     NET_ERR e = host_ctx(&cp);
     if (e != NET_UTIL_ERR_NONE) return e;
     HostCtx& c = *cp;
-    if (!tx && n_chunks == 0 && g_tune_burst_zc.load() != 0) {   // a burst from a pinned ring: in place
-        bool taken = false;
-        e = rx_burst_zero_copy(c, h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, &taken);
-        if (taken) return e;
-    }
     std::vector<HostChunk> ch;
     // n_chunks 0 = the library's choice (tools/burst_latency.c, profiles/r3x_burst_latency.jsonl): each
     // chunk adds 15-20 us per call and PCIe stays the bound, so one chunk, except Tx from 32 Ki
@@ -1402,6 +1481,26 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
     }
     guard.done = true;
     return NET_UTIL_ERR_NONE;
+}
+
+static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride, CPU_INT16U pkt_len,
+                        uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg, uint32_t udp_mode, bool tx,
+                        uint32_t n_chunks) {
+    if (n_pkt == 0) return NET_UTIL_ERR_NONE;
+    if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+    if (h_base == nullptr || (h_off != nullptr) != (h_len != nullptr) || (!tx && h_flags == nullptr && h_action == nullptr)) {
+        return NET_ERR_FAULT_NULL_PTR;
+    }
+    if (n_chunks == 0 && g_tune_burst_zc.load() != 0) {   // a burst from a pinned ring: in place
+        HostCtx* cp = nullptr;
+        NET_ERR e = host_ctx(&cp);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        bool taken = false;
+        e = tx ? tx_burst_zero_copy(*cp, h_base, h_off, stride, pkt_len, n_pkt, h_flags, udp_mode, &taken)
+               : rx_burst_zero_copy(*cp, h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, &taken);
+        if (taken) return e;
+    }
+    return pkt_host_copy(h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, udp_mode, tx, n_chunks);
 }
 
 NET_ERR NetUtil_MI355X_RxValidateIPHost(const void* h_base, const uint64_t* h_off, const uint16_t* h_len, uint64_t stride,
@@ -1554,7 +1653,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_burst_zc.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
-        if (value < -1 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_pkt_bound.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:

@@ -166,8 +166,10 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream p
 void set_tx_flush(int mode);
 // bound (NETCSUM_TUNE_PKT_BOUND): 0 slots streamed whole, 1 refills bounded by the parsed ends, 2 parse
 // first and every piece bounded (depth 8 only with bound 2)
+// rec: two-pass Tx (records + scatter); scatter = false: the records only (zero-copy host bursts, whose
+// host applies them)
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
-                             hipStream_t s, PktTxRecord* rec = nullptr);   // rec: two-pass Tx (records + scatter)
+                             hipStream_t s, PktTxRecord* rec = nullptr, bool scatter = true);
 // Zero-copy host bursts: one wave copies n result bytes (flags, and actions if act != nullptr) from
 // device memory into coherent pinned host memory, then stores `tag` into *word (system scope).
 hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, uint8_t* h_fl, uint8_t* h_act,

@@ -396,7 +396,20 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 
 // VER 4 / 6: one IP version per batch; VER 0: per datagram by the version nibble (a mixed ring).
 // BND 0: every piece of the run streamed whole (the round-3 form); 1: the first D pieces whole, the
-// refills bounded by the parsed ends; 2: the parse first, then every piece bounded.
+// refills bounded by the parsed ends; 2: the parse first, then every piece bounded; 3: live pieces
+// (below): the parse first, then only the pieces holding summed bytes, each masked to its live
+// 64-B sectors (runs of <= 128 pieces).
+//
+// Live pieces (BND 3). After the parse each lane marks its datagram's summed bytes [a, a + end) as
+// 64-B sectors (the HBM access unit) in a per-wave bitmap in LDS (2048 bits: a run spans <= 128 KiB),
+// by ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfwords l and
+// l + 64, and a ballot of their non-zero values gives the run's live pieces as two uniform 64-bit
+// masks. The stream then pops live pieces in address order (scalar find-first-set), skipping dead
+// ones entirely (no load, no consume), and lane l of piece q loads its 16 B only if sector l / 4 of
+// the piece's mask (one readlane) is set. The consume walk is unchanged except that offsets below
+// the piece clamp to 0: a datagram with nothing to sum (malformed: end 0) may start in a skipped
+// piece, and its event then falls in a later one with an empty range.
+constexpr uint32_t kNoPiece = 0x3FFFFu;                 // past every run (qb < 2^28)
 template <int D, bool NT, bool TX, bool REC, int VER, int BND>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -453,6 +466,54 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
     const RunBound rb{lead0, st, nres, 1.0f / (float)st};
+    uint64_t lm0 = 0u, lm1 = 0u;                               // BND 3: live pieces 0-63 / 64-127
+    uint32_t pm0 = 0u, pm1 = 0u;                               // BND 3: sector masks of pieces l, l + 64
+    uint32_t nlive = npieces;
+    if constexpr (BND == 3) {
+        __shared__ uint32_t sect_all[4][64];
+        uint32_t* sect = sect_all[w];
+        sect[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (end_v != 0u) {
+            const uint32_t s0 = prel >> 6, s1 = (prel + end_v - 1u) >> 6;
+            for (uint32_t d = s0 >> 5; d <= (s1 >> 5); ++d) {
+                const uint32_t lo = max(s0, d << 5) - (d << 5), hi = min(s1, (d << 5) + 31u) - (d << 5);
+                atomicOr(&sect[d], (2u << hi) - (1u << lo));   // bits lo..hi (hi = 31: 2 << 31 wraps to 0)
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint16_t* s16 = reinterpret_cast<const uint16_t*>(sect);
+        pm0 = s16[lane];
+        pm1 = s16[lane + 64u];
+        lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
+        lm1 = __builtin_amdgcn_ballot_w64(pm1 != 0u);
+        nlive = (uint32_t)__builtin_popcountll(lm0) + (uint32_t)__builtin_popcountll(lm1);
+    }
+    const uint32_t lsect = lane >> 2;                          // the lane's 64-B sector in a piece
+    auto pop = [&]() -> uint32_t {                             // BND 3: next live piece (uniform)
+        // selects only (a branch choosing which mask to clear made the compiler address the two
+        // masks through a pointer, i.e. scratch memory)
+        const bool z0 = lm0 == 0u;
+        const uint32_t q = !z0 ? (uint32_t)__builtin_ctzll(lm0) : (lm1 != 0u ? 64u + (uint32_t)__builtin_ctzll(lm1) : kNoPiece);
+        const uint64_t n1 = lm1 & (lm1 - 1u);
+        lm1 = z0 ? n1 : lm1;
+        lm0 &= lm0 - 1u;
+        return q;
+    };
+    auto live_voff = [&](uint32_t q) -> uint32_t {             // BND 3: lane's offset in piece q, or OOB
+        const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)(q & 63u));
+        const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)pm1, (int)(q & 63u));
+        const uint32_t sm = q < 64u ? r0 : (q < 128u ? r1 : 0u);
+        return ((sm >> lsect) & 1u) ? (q << 10) + lane16 : kOOB;
+    };
+    uint32_t qd[D];                                            // BND 3: the piece in flight in slot j
+    if constexpr (BND == 3) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            qd[j] = pop();
+            dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+        }
+    }
     if constexpr (BND == 2) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -480,7 +541,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
             uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
 #pragma clang loop vectorize(disable) unroll(disable)
             do {
-                const uint32_t Pe = piece_prefix(v, full, lane16, e - qb);
+                const uint32_t Pe = piece_prefix(v, full, lane16, e <= qb ? 0u : e - qb);
                 const uint32_t T = wave_total(a + (Pe - Ps));
                 t = (lane == u - s_begin) ? T : t;
                 a = 0u;
@@ -490,7 +551,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                 if (u < s_end) {
                     e = c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin));
                 }
-                Ps = adj ? Pe : piece_prefix(v, full, lane16, min(c - qb, 1024u));
+                Ps = adj ? Pe : piece_prefix(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
             } while (u < s_end && e <= pend);
             if (u < s_end) {
                 a = full - Ps;
@@ -503,14 +564,20 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         tot_v = t;
     };
 
-    const uint32_t rounds = (npieces + (uint32_t)D - 1u) / (uint32_t)D;
+    const uint32_t rounds = (nlive + (uint32_t)D - 1u) / (uint32_t)D;
     for (uint32_t r = 0; r < rounds; ++r) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const uint32_t q = r * (uint32_t)D + (uint32_t)j;
-            consume(q, opaque_tuple(dv[j]));
-            const uint32_t x = ((q + (uint32_t)D) << 10) + lane16;            // past the run: zeros
-            dv[j] = buf_load16<NT>(rd, BND ? bounded_voff(x, rb, end_v) : x);
+            if constexpr (BND == 3) {
+                consume(qd[j], opaque_tuple(dv[j]));
+                qd[j] = pop();                                                // none left: OOB, zeros
+                dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+            } else {
+                const uint32_t q = r * (uint32_t)D + (uint32_t)j;
+                consume(q, opaque_tuple(dv[j]));
+                const uint32_t x = ((q + (uint32_t)D) << 10) + lane16;        // past the run: zeros
+                dv[j] = buf_load16<NT>(rd, BND ? bounded_voff(x, rb, end_v) : x);
+            }
             asm volatile("" ::: "memory");
         }
     }
@@ -729,7 +796,7 @@ hipError_t launch_tx_flush(hipStream_t s) {
 }
 
 template <int D, bool NT, bool TX, int VER, int BND>
-hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec) {
+hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec, bool scatter) {
     PktBatchArgs a = a0;
     // no piece touch by default: the header prologue already loads each packet's first bytes with
     // the plain policy, and touching every piece on top is slower (r2ct: Rx 0.2174 -> 0.2315 ms)
@@ -740,7 +807,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     if (TX && rec != nullptr) {
         hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || !scatter) return e;
         e = launch_scatter<VER != 4>(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
@@ -776,16 +843,19 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver) {
 }
 
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
-                             hipStream_t s, PktTxRecord* rec) {
-    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 2) return hipErrorInvalidValue;
-    // every bound with 4 pieces in flight; 8 pieces only in the default bound (2)
+                             hipStream_t s, PktTxRecord* rec, bool scatter) {
+    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3) return hipErrorInvalidValue;
+    // live pieces: a run spans at most 128 pieces (the host sizes runs for it)
+    if (bound == 3 && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) return hipErrorInvalidValue;
+    // every bound with 4 pieces in flight; 8 pieces only in the default bound (3)
 #define NETCSUM_P(V_, D_, NT_, TX_, B_)                                                                   \
     if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_ && bound == B_)                              \
-        return launch_pkt_stream_t<D_, NT_, TX_, V_, B_>(a, spw, s, rec);
+        return launch_pkt_stream_t<D_, NT_, TX_, V_, B_>(a, spw, s, rec, scatter);
 #define NETCSUM_PB(V_, D_, B_)                                                                            \
     NETCSUM_P(V_, D_, true, false, B_) NETCSUM_P(V_, D_, false, false, B_) NETCSUM_P(V_, D_, true, true, B_) \
     NETCSUM_P(V_, D_, false, true, B_)
-#define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0) NETCSUM_PB(V_, 4, 1) NETCSUM_PB(V_, 4, 2) NETCSUM_PB(V_, 8, 2)
+#define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0) NETCSUM_PB(V_, 4, 1) NETCSUM_PB(V_, 4, 2) NETCSUM_PB(V_, 4, 3) \
+    NETCSUM_PB(V_, 8, 3)
     NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
 #undef NETCSUM_PV
 #undef NETCSUM_PB
