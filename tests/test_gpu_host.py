@@ -277,8 +277,8 @@ def test_tx_burst_host_zero_copy(n):
             body = struct.pack("!BB", inner[6], u - 1) + ext_body(rng, 60, u * 8 - 2) + inner[40:]
             pkt = inner[:4] + struct.pack("!HB", len(body), 60) + inner[7:40] + body
         else:
-            pkt = (make_packet if i % 2 else make_packet_v6)(rng, rng.choice(["tcp", "udp", "udp", "icmp"]),
-                                                             payload=rng.randint(0, 1400))
+            pkt = (make_packet(rng, rng.choice(["tcp", "udp", "udp", "icmp"]), payload=rng.randint(0, 1400)) if i % 2
+                   else make_packet_v6(rng, rng.choice(["tcp", "udp", "udp", "icmp_echo"]), payload=rng.randint(0, 1400)))
         pkt = pkt[:stride - lead]
         csum = rng.random() < 0.8
         pairs.append((oo.tx_stack_offload(pkt, csum), op.tx_finalize_ip(pkt, csum)))
