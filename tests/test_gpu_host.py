@@ -260,7 +260,8 @@ def test_rx_burst_host_zero_copy_many_calls_and_threads():
 
 
 @pytest.mark.parametrize("n", [1, 3, 64, 500, 4096])
-def test_tx_burst_host_zero_copy(n):
+@pytest.mark.parametrize("form", ["strided", "offlen"])
+def test_tx_burst_host_zero_copy(n, form):
     """TxBurstHost with n_chunks 0 on a pinned strided ring (the IPv4 header at +14 of 1520-B slots):
     the checksum pass reads the ring in place and returns 8-B records that the host applies
     (tx_burst_zero_copy); IPv6 datagrams behind a long Destination Options header (flag EXT_HDR) are
@@ -297,7 +298,12 @@ def test_tx_burst_host_zero_copy(n):
         try:
             hb = _pinned(buf)
             fl = np.zeros(n, np.uint8)
-            netcsum.tx_burst_host(hb[lead:], n, fl, stride=stride, pkt_len=stride - lead)
+            if form == "strided":
+                netcsum.tx_burst_host(hb[lead:], n, fl, stride=stride, pkt_len=stride - lead)
+            else:                                          # per-frame lengths (whole present bytes)
+                offs = np.arange(n, dtype=np.uint64) * stride + lead
+                lens = np.full(n, stride - lead, np.uint16)
+                netcsum.tx_burst_host(hb, n, fl, off=offs, lens=lens)
         finally:
             netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 1)
         got = hb.numpy()

@@ -11,6 +11,7 @@ and 64-B sectors holding summed bytes (live pieces, dead pieces skipped). The by
 skips are random here, so a kernel that summed any of them would disagree with the oracle; the bytes
 outside the checksum fields must come back untouched by Tx."""
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -204,3 +205,65 @@ def test_bounded_stream_full_size_ring_properties():
     fl = f.cpu().numpy()
     assert (fl[k] & 0x07) == 0x05                                # L4 checked, not OK
     assert (np.delete(fl, k) & 0x07 == 0x07).all()
+
+
+@pytest.mark.parametrize("order", ["sorted", "reversed", "shuffled", "duplicates", "far", "packed"])
+@pytest.mark.parametrize("spw", [-1, 1, 7, 64])
+def test_offset_length_runs_every_order_vs_oracle(order, spw):
+    """Offset/length batches in the live-piece stream (netcsum_pktstream.hip, VL): a run of
+    descriptors in increasing address order within 128 KiB streams; any other run (reversed or
+    shuffled rings, the same datagram listed twice, slots > 128 KiB apart) is done datagram by
+    datagram. Mixed IPv4 / IPv6 (RxValidateIP, TxFinalizeIP, RxBurst), results equal the oracle's."""
+    netcsum.tune(netcsum.TUNE_TILE, spw)
+    rng = random.Random(zlib.crc32(f"{order}/{spw}".encode()))
+    n, slot, lead = 700, 1520, 14
+    buf, lens = _ring(rng, n, slot, lead, v6mix=True)
+    offs = np.arange(n, dtype=np.int64) * slot + lead
+    if order == "reversed":
+        offs, lens = offs[::-1].copy(), lens[::-1].copy()
+    elif order == "shuffled":
+        perm = np.random.default_rng(spw + 5).permutation(n)
+        offs, lens = offs[perm].copy(), lens[perm].copy()
+    elif order == "duplicates":
+        offs[1::9] = offs[0::9][: len(offs[1::9])]
+        lens[1::9] = lens[0::9][: len(lens[1::9])]
+    elif order == "far":                                          # every 5th slot 200 KiB further on
+        big = np.frombuffer(rng.randbytes(len(buf) + (n // 5 + 1) * 200 * 1024), np.uint8).copy()
+        shift = (np.arange(n) // 5) * 200 * 1024
+        for i in range(n):
+            big[offs[i] + shift[i] - lead:offs[i] + shift[i] - lead + slot] = buf[i * slot:(i + 1) * slot]
+        buf, offs = big, offs + shift
+    elif order == "packed":                                       # back to back, odd starts, no gaps
+        frames = [bytes(buf[o:o + int(m)]) for o, m in zip(offs.tolist(), lens.tolist())]
+        pos, parts, new = 1, [b"\x00"], []
+        for f in frames:
+            new.append(pos)
+            parts.append(f)
+            pos += len(f)
+        buf = np.frombuffer(b"".join(parts) + rng.randbytes(64), np.uint8).copy()
+        offs = np.array(new, np.int64)
+    frames = [bytes(buf[o:o + int(m)]) for o, m in zip(offs.tolist(), lens.tolist())]
+    want_f = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
+    b = torch.from_numpy(buf).to(DEV)
+    o_d = torch.from_numpy(offs).to(DEV)
+    l_d = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    netcsum.rx_validate_ip(b, n, f, off=o_d, lens=l_d)
+    torch.cuda.synchronize()
+    assert netcsum.last_launch().startswith("pkt_stream_kernel") and "offlen" in netcsum.last_launch()
+    _check(f.cpu().numpy(), want_f, "rx")
+    if order == "duplicates":
+        return                                                    # Tx of one datagram twice: a race by contract
+    tx_w = buf.copy()
+    txf_w = np.zeros(n, np.uint8)
+    for i, (o, m) in enumerate(zip(offs.tolist(), lens.tolist())):
+        q, txf_w[i] = op.tx_finalize_ip(bytes(buf[o:o + int(m)]), True)
+        tx_w[o:o + int(m)] = np.frombuffer(q, np.uint8)
+    for passes in (1, 2):
+        netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+        bt = torch.from_numpy(buf).to(DEV)
+        ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        netcsum.tx_finalize_ip(bt, n, ft, off=o_d, lens=l_d)
+        torch.cuda.synchronize()
+        _check(bt.cpu().numpy(), tx_w, f"tx bytes ({passes} passes)")
+        _check(ft.cpu().numpy(), txf_w, f"tx flags ({passes} passes)")

@@ -9,7 +9,8 @@ For 1 M datagrams per layout (tools/ring_layouts.py):
   ring       40 / 576 / 1500-B datagrams at 7 : 4 : 1 in 1520-B slots at +14, 1506 B present
 each as a strided batch (pkt_len = bytes present) under NETCSUM_TUNE_PKT_BOUND 0 / 2 / 3 (the
 run-stream kernel reading whole slots / parse first and every chunk bounded / live pieces) and as an
-offset/length batch (per-frame descriptors: the lane-group kernel), fused Rx and Tx finalize; the
+offset/length batch (per-frame descriptors: the live-piece stream, and the lane-group kernel with
+TUNE_KERNEL 2), fused Rx and Tx finalize; the
 ring and the 2-KiB layout also at 16 / 32 / 64 datagrams per wave run. Variants interleaved, two passes; median
 HIP-event time of 20 launches after a timed warm-up. After the first Tx every Rx flag must read
 IP_OK | L4_OK | L4_CHECKED (valid), and the three bounds and both forms must write identical bytes.
@@ -64,14 +65,15 @@ def main():
         torch.cuda.synchronize()
         ref = r["buf"].clone()
         variants = [("strided.b0", 0, -1, strided), ("strided.b2", 2, -1, strided), ("strided.b3", 3, -1, strided),
-                    ("offlen", -1, -1, desc)]
+                    ("offlen", -1, -1, desc), ("offlen.lanegroup", -1, -2, desc)]
         if name in ("ring", "nb2k"):
             variants += [(f"strided.b3.s{s}", 3, s, strided) for s in (16, 32, 64)]
         res = {}
         for p in range(2):
             for tag, bound, spw, kw in variants:
                 netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
-                netcsum.tune(netcsum.TUNE_TILE, spw)
+                netcsum.tune(netcsum.TUNE_TILE, max(spw, -1))
+                netcsum.tune(netcsum.TUNE_KERNEL, 2 if spw == -2 else 0)   # the lane-group packet kernel
                 base = r["buf"] if kw is desc else r["base"]
                 for op in ("rx", "tx"):
                     if op == "rx":
@@ -88,6 +90,7 @@ def main():
                         d["bytes_equal_first_tx"] = bool(torch.equal(r["buf"], ref))
         netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
         netcsum.tune(netcsum.TUNE_TILE, -1)
+        netcsum.tune(netcsum.TUNE_KERNEL, 0)
         for (tag, op), d in res.items():
             algo = r["datagram_bytes"] + n * (1 if op == "rx" else 4)
             ms = min(d["ms"])

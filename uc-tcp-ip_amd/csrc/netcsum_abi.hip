@@ -962,8 +962,14 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     const bool walk = ip_ver != 4;
     const bool own_flags = walk && d_flags == nullptr;
     hipStream_t hs = static_cast<hipStream_t>(hip_stream);
-    if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver)) {
-        const uint64_t per = std::max<uint64_t>(a.stride, 1u);
+    // which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND; 3 = live pieces, whose runs span at
+    // most 128 KiB); offset/length batches stream in the live-piece form only
+    const int d = g_tune_chunks.load() == 8 ? 8 : 4;
+    const int bound = d == 8 ? 3 : (g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load());
+    if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver, bound)) {
+        // offset/length runs: 16 datagrams (their lengths are on the device; the device checks each
+        // run's order and reach, and takes a run datagram by datagram otherwise)
+        const uint64_t per = d_off ? 1280u : std::max<uint64_t>(a.stride, 1u);
         const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
                                          : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
         // small batches (NIC bursts) are latency-bound: a run costs ~run x len / 4 KiB memory round
@@ -974,7 +980,6 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         if (!(tile > 0 && tile <= 64)) {
             while (spw > 1u && (uint64_t)n_pkt < 2048ull * spw) spw >>= 1;
         }
-        const int d = g_tune_chunks.load() == 8 ? 8 : 4;
         const bool snt = nt >= 0 ? (nt != 0) : true;
         // Tx passes: auto = two (8-B records, then a scatter pass: 1 M x 1500 B 0.2918 against 0.2954
         // ms in one pass) from 64 Ki datagrams up, one below (a burst is then a single launch)
@@ -982,16 +987,14 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const bool two = tx && (rec_only != nullptr || tp == 2 || (tp == 0 && n_pkt >= 65536u));
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
-        // which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND; 3 = live pieces, whose runs span
-        // at most 128 KiB)
-        const int bound = d == 8 ? 3 : (g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load());
-        if (bound == 3) {
+        if (bound == 3 && d_off == nullptr) {
             const uint64_t cap = (128u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
         }
         char desc[144];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s,bound=%d> block=256 pkts_per_wave=%u%s%s", d,
-                 snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", bound, spw,
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s,bound=%d%s> block=256 pkts_per_wave=%u%s%s", d,
+                 snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", bound,
+                 d_off ? ",offlen" : "", spw,
                  two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "");
         netcsum::set_last_launch(desc);
         if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
@@ -1316,30 +1319,48 @@ static NET_ERR pkt_host_copy(void* h_base, const uint64_t* h_off, const uint16_t
                              CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags, uint8_t* h_action, uint32_t rx_cfg,
                              uint32_t udp_mode, bool tx, uint32_t n_chunks);
 
-// Tx over a pinned strided ring: the checksum pass reads the ring in place and writes one 8-B
+// Tx over a pinned ring: the checksum pass reads the ring in place and writes one 8-B
 // record per datagram (PktTxRecord) to device memory — never into the ring —, the completion kernel
 // copies the records into coherent pinned memory, and the host writes the fields into its ring (as
 // the copy pipeline's gather records do). Datagrams whose IPv6 extension chain runs past the
 // kernel's window (flag EXT_HDR: walked by a later pass in the device forms) are finished by the copy
 // path afterwards, as an offset/length batch of just those datagrams. *taken as for Rx.
-static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_off, uint64_t stride, CPU_INT16U pkt_len,
-                                  uint32_t n_pkt, uint8_t* h_flags, uint32_t udp_mode, bool* taken) {
+static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_off, const uint16_t* h_len,
+                                  uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* h_flags,
+                                  uint32_t udp_mode, bool* taken) {
     *taken = false;
-    if (n_pkt > kBurstZC || h_off != nullptr) return NET_UTIL_ERR_NONE;
+    if (n_pkt > kBurstZC || g_tune_kernel.load() == 2) return NET_UTIL_ERR_NONE;
     netcsum::PktBatchArgs a{};
     a.stride = stride;
     a.len_u = pkt_len;
     a.n = n_pkt;
-    if (!netcsum::pkt_stream_supported(a, 0) || g_tune_kernel.load() == 2) return NET_UTIL_ERR_NONE;
-    const uint64_t span = (uint64_t)(n_pkt - 1u) * stride + pkt_len;
+    a.off = h_off;                                      // (only tested against nullptr here)
+    a.len = h_len;
+    if (!netcsum::pkt_stream_supported(a, 0, g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load())) {
+        return NET_UTIL_ERR_NONE;
+    }
+    uint64_t span = 0;
+    if (h_off == nullptr) {
+        span = (uint64_t)(n_pkt - 1u) * stride + pkt_len;
+    } else {
+        for (uint32_t i = 0; i < n_pkt; ++i) span = std::max<uint64_t>(span, h_off[i] + h_len[i]);
+    }
     if (span > kBurstZCSpan) return NET_UTIL_ERR_NONE;
     const uint8_t* d_ring = pinned_alias(h_base, span);
     if (d_ring == nullptr) return NET_UTIL_ERR_NONE;
     *taken = true;
     NET_ERR e = ensure_burst(c);
     if (e != NET_UTIL_ERR_NONE) return e;
+    const uint64_t* d_off = nullptr;
+    const uint16_t* d_len = nullptr;
+    if (h_off != nullptr) {                             // descriptors: staged in coherent pinned memory
+        std::memcpy(c.h_burst + kBurstOff, h_off, (size_t)n_pkt * 8u);
+        std::memcpy(c.h_burst + kBurstLen, h_len, (size_t)n_pkt * 2u);
+        d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
+        d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
+    }
     netcsum::PktTxRecord* d_rec = reinterpret_cast<netcsum::PktTxRecord*>(c.d_burst + kBurstDevRec);
-    e = pkt_batch(d_ring, nullptr, nullptr, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
+    e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
                   nullptr, d_rec);
     if (e != NET_UTIL_ERR_NONE) return e;
     if (++c.seq == 0u) c.seq = 1u;
@@ -1353,14 +1374,19 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
     uint8_t* hb = static_cast<uint8_t*>(h_base);
     const uint64_t* rec = reinterpret_cast<const uint64_t*>(c.h_burst + kBurstRec);
     std::vector<uint64_t> walk_off;
+    std::vector<uint16_t> walk_len;
+    std::vector<uint32_t> walk_idx;
     for (uint32_t i = 0; i < n_pkt; ++i) {
         const uint64_t r = rec[i];                      // PktTxRecord: vals | l4_off << 32 | flags << 48 | store << 56
         const uint32_t flags = (uint32_t)(r >> 48) & 0xFFu, store = (uint32_t)(r >> 56);
+        const uint64_t o = h_off ? h_off[i] : (uint64_t)i * stride;
         if (flags & NETCSUM_PKT_EXT_HDR) {
-            walk_off.push_back((uint64_t)i * stride);
+            walk_off.push_back(o);
+            walk_len.push_back(h_off ? h_len[i] : pkt_len);
+            walk_idx.push_back(i);
             continue;
         }
-        uint8_t* p = hb + (uint64_t)i * stride;
+        uint8_t* p = hb + o;
         const uint16_t ip = (uint16_t)r, l4 = (uint16_t)(r >> 16);
         if (store & 1u) std::memcpy(p + 10, &ip, 2);
         if (store & 2u) std::memcpy(p + ((r >> 32) & 0xFFFFu), &l4, 2);
@@ -1368,13 +1394,12 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
     }
     if (!walk_off.empty()) {                            // the rare long IPv6 chains: the copy path
         const uint32_t m = (uint32_t)walk_off.size();
-        std::vector<uint16_t> lens(m, pkt_len);
         std::vector<uint8_t> fl(m);
-        e = pkt_host_copy(h_base, walk_off.data(), lens.data(), 0, 0, m, h_flags ? fl.data() : nullptr, nullptr, 0u,
-                          udp_mode, true, 1u);
+        e = pkt_host_copy(h_base, walk_off.data(), walk_len.data(), 0, 0, m, h_flags ? fl.data() : nullptr, nullptr,
+                          0u, udp_mode, true, 1u);
         if (e != NET_UTIL_ERR_NONE) return e;
         if (h_flags) {
-            for (uint32_t k = 0; k < m; ++k) h_flags[walk_off[k] / stride] = fl[k];
+            for (uint32_t k = 0; k < m; ++k) h_flags[walk_idx[k]] = fl[k];
         }
     }
     return NET_UTIL_ERR_NONE;
@@ -1496,7 +1521,7 @@ static NET_ERR pkt_host(void* h_base, const uint64_t* h_off, const uint16_t* h_l
         NET_ERR e = host_ctx(&cp);
         if (e != NET_UTIL_ERR_NONE) return e;
         bool taken = false;
-        e = tx ? tx_burst_zero_copy(*cp, h_base, h_off, stride, pkt_len, n_pkt, h_flags, udp_mode, &taken)
+        e = tx ? tx_burst_zero_copy(*cp, h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, udp_mode, &taken)
                : rx_burst_zero_copy(*cp, h_base, h_off, h_len, stride, pkt_len, n_pkt, h_flags, h_action, rx_cfg, &taken);
         if (taken) return e;
     }

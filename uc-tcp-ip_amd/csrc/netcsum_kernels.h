@@ -159,7 +159,7 @@ uint32_t varlen_run_bytes();
 constexpr uint32_t kVarlenSpwMin = 3u;
 void set_hdr_burst(int v);     // NETCSUM_TUNE_HDR_BURST: header stream results written per run (1) or per piece (0)
 bool hdr_burst();
-bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver);    // run-stream packet kernel's domain
+bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound);   // run-stream packet kernel's domain
 // Tx finalize write-back of the dirty field lines (NETCSUM_TUNE_TX_FLUSH): -1 / 0 none, 1 scatter
 // stores at system scope, 2 release at the end of every scatter wave, 3 / 4 a write-back launch of
 // 8 / 256 workgroups after the Tx launch(es).

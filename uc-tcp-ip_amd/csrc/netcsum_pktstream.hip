@@ -410,24 +410,16 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 // the piece clamp to 0: a datagram with nothing to sum (malformed: end 0) may start in a skipped
 // piece, and its event then falls in a later one with an empty range.
 constexpr uint32_t kNoPiece = 0x3FFFFu;                 // past every run (qb < 2^28)
-template <int D, bool NT, bool TX, bool REC, int VER, int BND>
-__global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
-    if (sb64 >= A.n) {
-        return;
-    }
-    const uint32_t s_begin = (uint32_t)sb64;
-    const uint32_t nres = min(A.n - s_begin, spw);
+// One wave run: packets s_begin .. s_begin + nres - 1, lane k's packet at run-relative offset prel
+// (from O, 128-B aligned) with `avail` bytes present; the run's bytes [O, O + span). VL: per-packet
+// starts (offset/length descriptors) instead of a stride.
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
+__device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec, uint32_t w, uint32_t lane,
+                                        uint32_t s_begin, uint32_t nres, uintptr_t O, uint32_t prel, uint32_t avail,
+                                        uint32_t span) {
     const uint32_t s_end = s_begin + nres;
-    const uint32_t L = A.len_u;
     const uint32_t st = (uint32_t)A.stride;
-    const uintptr_t a_first = (uintptr_t)A.base + (uint64_t)s_begin * A.stride;
-    const uintptr_t O = a_first & ~(uintptr_t)127;
-    const uint32_t lead0 = (uint32_t)(a_first - O);
-    const uint32_t span = lead0 + (nres - 1u) * st + L;
+    const uint32_t lead0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)prel);
     const uint32_t npieces = (span + 1023u) >> 10;
     const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
     const uint32_t lane16 = 16u * lane;
@@ -442,7 +434,6 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
 
     // ... while lane k parses packet k from its own 96-B window.
     const bool mine = lane < nres;
-    const uint32_t prel = lead0 + lane * st;                   // run-relative start of packet `lane`
     const uint32_t plead = prel & 15u;
     const uint32_t pq = prel - plead;
     u32x4 h[6];
@@ -459,13 +450,13 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         wd[4 * c + 3] = h[c].w;
     }
     const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
-    const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, L, odd, A.udp_tx_csum);
+    const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, avail, odd, A.udp_tx_csum);
     // Row touch (off by default here: the header loads above already touch every datagram) issued
     // after the parse, when the window's registers are free (issued before it, its two VGPRs raised
     // the prologue's peak to 73 = 6 waves/SIMD).
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
-    const RunBound rb{lead0, st, nres, 1.0f / (float)st};
+    const RunBound rb{lead0, st, nres, 1.0f / (float)max(st, 1u)};
     uint64_t lm0 = 0u, lm1 = 0u;                               // BND 3: live pieces 0-63 / 64-127
     uint32_t pm0 = 0u, pm1 = 0u;                               // BND 3: sector masks of pieces l, l + 64
     uint32_t nlive = npieces;
@@ -546,7 +537,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                 t = (lane == u - s_begin) ? T : t;
                 a = 0u;
                 ++u;
-                c += st;
+                if constexpr (VL) {
+                    c = (uint32_t)__builtin_amdgcn_readlane((int)prel, (int)min(u - s_begin, 63u));
+                } else {
+                    c += st;
+                }
                 const bool adj = c == e;                       // dense: the next packet starts at this end
                 if (u < s_end) {
                     e = c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin));
@@ -647,7 +642,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         A.action_out[idx] = (uint8_t)rx_action(f, pk.proto, pk.v6, A.rx_cfg);
     }
     if constexpr (TX) {
-        uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)idx * A.stride;
+        uint8_t* p = reinterpret_cast<uint8_t*>(O + prel);
         if (cip != ~0u) {
             store_field(p + 10, cip);
         }
@@ -663,6 +658,59 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
     if constexpr (kWalkHere) {
         if (walk_here) {
             v6walk::walk_wave<TX>(A, s_begin, need, lane);
+        }
+    }
+}
+
+// Offset/length runs (VL) are streamed when their datagrams lie in increasing address order, each
+// slot's present bytes ending before the next one starts, within 128 KiB from the run's first
+// 128-B line (the live-piece bitmap's reach); any other run is done one datagram at a time, each as
+// a run of its own (correct for any order or overlap, at one prologue per datagram).
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
+__global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
+    static_assert(!VL || BND == 3, "offset/length runs take the live-piece form");
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
+    if (sb64 >= A.n) {
+        return;
+    }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(A.n - s_begin, spw);
+    if constexpr (!VL) {
+        const uintptr_t a_first = (uintptr_t)A.base + (uint64_t)s_begin * A.stride;
+        const uintptr_t O = a_first & ~(uintptr_t)127;
+        const uint32_t lead0 = (uint32_t)(a_first - O);
+        const uint32_t st = (uint32_t)A.stride;
+        pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, lead0 + lane * st, A.len_u,
+                                             lead0 + (nres - 1u) * st + A.len_u);
+    } else {
+        const bool mine = lane < nres;
+        const uint64_t off = A.off[mine ? s_begin + lane : s_begin];
+        const uint32_t len = mine ? (uint32_t)A.len[s_begin + lane] : 0u;
+        const uint64_t off0 = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(off >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off);
+        const uintptr_t O = ((uintptr_t)A.base + off0) & ~(uintptr_t)127;
+        const uint64_t rel = (uintptr_t)A.base + off - O;                 // >= 0 when ordered
+        const uint64_t end = rel + len;
+        // ordered: lane k starts at or after lane k - 1's present bytes end (DPP shift by one lane)
+        const uint32_t prev_end_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
+        const bool ok = !mine || (rel < (128u << 10) && end <= (128u << 10) - 128u &&
+                                  (lane == 0u || (uint64_t)prev_end_lo <= rel));
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0u) {
+            const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u));
+            pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, mine ? (uint32_t)rel : 0u,
+                                                 len, span);
+        } else {
+            for (uint32_t k = 0; k < nres; ++k) {                // one datagram per run
+                const uint64_t ok_ = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(off >> 32), (int)k) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, (int)k);
+                const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)k);
+                const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
+                const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
+                pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+            }
         }
     }
 }
@@ -689,7 +737,7 @@ __global__ void __launch_bounds__(256) pkt_scatter_kernel(PktBatchArgs A, const 
         if (A.fieldpos_out && !need) {
             A.fieldpos_out[i] = ((store & 1u) ? kFieldIP : 0u) | ((store & 2u) ? kFieldL4 | l4_off : 0u);
         }
-        uint8_t* p = const_cast<uint8_t*>(A.base) + (uint64_t)i * A.stride;
+        uint8_t* p = const_cast<uint8_t*>(A.base) + (A.off ? A.off[i] : (uint64_t)i * A.stride);
         if constexpr (WT) {
             if (store & 1u) {
                 __hip_atomic_store(p + 10, (uint8_t)(vals & 0xFFu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -795,7 +843,7 @@ hipError_t launch_tx_flush(hipStream_t s) {
     return hipSuccess;
 }
 
-template <int D, bool NT, bool TX, int VER, int BND>
+template <int D, bool NT, bool TX, int VER, int BND, bool VL>
 hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec, bool scatter) {
     PktBatchArgs a = a0;
     // no piece touch by default: the header prologue already loads each packet's first bytes with
@@ -805,13 +853,13 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     if (TX && rec != nullptr) {
-        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND, VL>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || !scatter) return e;
         e = launch_scatter<VER != 4>(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND, VL>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
     hipError_t e = hipGetLastError();
     return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }
@@ -835,27 +883,36 @@ void set_tx_flush(int mode) {
     g_tx_flush.store(mode);
 }
 
-// Strided batches of >= 64-B packets (IPv4, IPv6 or mixed), dense (gap <= 64 B), whose runs span
-// < 2^31 bytes.
-bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver) {
-    return (ip_ver == 4 || ip_ver == 6 || ip_ver == 0) && a.off == nullptr && a.len_u >= 64u && a.stride >= a.len_u &&
-           a.stride <= a.len_u + 64u && (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
+// Strided batches of >= 64-B packets (IPv4, IPv6 or mixed) whose runs span < 2^31 bytes: any gap
+// between slots in the live-piece form (bound 3), at most 64 B in the others; offset/length batches
+// in the live-piece form.
+bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
+    if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
+    if (a.off != nullptr) return bound == 3 && a.len != nullptr;
+    return a.len_u >= 64u && a.stride >= a.len_u && (bound == 3 || a.stride <= a.len_u + 64u) &&
+           (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
 
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec, bool scatter) {
-    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3) return hipErrorInvalidValue;
-    // live pieces: a run spans at most 128 pieces (the host sizes runs for it)
-    if (bound == 3 && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) return hipErrorInvalidValue;
-    // every bound with 4 pieces in flight; 8 pieces only in the default bound (3)
-#define NETCSUM_P(V_, D_, NT_, TX_, B_)                                                                   \
-    if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_ && bound == B_)                              \
-        return launch_pkt_stream_t<D_, NT_, TX_, V_, B_>(a, spw, s, rec, scatter);
-#define NETCSUM_PB(V_, D_, B_)                                                                            \
-    NETCSUM_P(V_, D_, true, false, B_) NETCSUM_P(V_, D_, false, false, B_) NETCSUM_P(V_, D_, true, true, B_) \
-    NETCSUM_P(V_, D_, false, true, B_)
-#define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0) NETCSUM_PB(V_, 4, 1) NETCSUM_PB(V_, 4, 2) NETCSUM_PB(V_, 4, 3) \
-    NETCSUM_PB(V_, 8, 3)
+    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3 || !pkt_stream_supported(a, ip_ver, bound)) {
+        return hipErrorInvalidValue;
+    }
+    // live pieces: a strided run spans at most 128 pieces (the host sizes runs for it; offset/length
+    // runs check their span on the device)
+    if (bound == 3 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
+        return hipErrorInvalidValue;
+    }
+    const bool vl = a.off != nullptr;
+    // every bound with 4 pieces in flight; 8 pieces and offset/length runs only in the live-piece form
+#define NETCSUM_P(V_, D_, NT_, TX_, B_, VL_)                                                              \
+    if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_ && bound == B_ && vl == VL_)                 \
+        return launch_pkt_stream_t<D_, NT_, TX_, V_, B_, VL_>(a, spw, s, rec, scatter);
+#define NETCSUM_PB(V_, D_, B_, VL_)                                                                       \
+    NETCSUM_P(V_, D_, true, false, B_, VL_) NETCSUM_P(V_, D_, false, false, B_, VL_)                      \
+    NETCSUM_P(V_, D_, true, true, B_, VL_) NETCSUM_P(V_, D_, false, true, B_, VL_)
+#define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0, false) NETCSUM_PB(V_, 4, 1, false) NETCSUM_PB(V_, 4, 2, false)     \
+    NETCSUM_PB(V_, 4, 3, false) NETCSUM_PB(V_, 8, 3, false) NETCSUM_PB(V_, 4, 3, true) NETCSUM_PB(V_, 8, 3, true)
     NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
 #undef NETCSUM_PV
 #undef NETCSUM_PB
