@@ -657,9 +657,11 @@ typedef enum netcsum_tune_key {
                                          are read. 0 = the whole slot (pkt_len bytes), 1 = the first
                                          pieces whole, then only each datagram's parsed extent, 2 = the
                                          parse first, then only the parsed extents; -1 = the default (2) */
-    NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory Rx batches with n_chunks 0 of <= 4096 frames whose
-                                         ring is pinned host memory: 1 (default) the kernel reads the ring
-                                         in place and the host polls a completion word; 0 = the copy
+    NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
+                                         ring is pinned host memory: the kernel reads the ring in place;
+                                         1 (default) a completion kernel copies the results out and stores
+                                         a completion word the host polls, 2 = the results go straight to
+                                         coherent pinned memory and the host polls them; 0 = the copy
                                          pipeline (H2D, kernel, D2H, stream synchronisation)           */
 } NETCSUM_TUNE_KEY;
 

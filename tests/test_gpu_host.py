@@ -187,7 +187,8 @@ def test_tx_host_records_every_kernel_form(kernel, passes, chunks):
 @pytest.mark.parametrize("form", ["strided", "offlen"])
 def test_rx_burst_host_zero_copy(n, form):
     """NIC-burst sizes with n_chunks 0 from a pinned ring: the kernel reads the ring in place and the
-    host polls a completion word (rx_burst_zero_copy, up to 4096 frames; 4097 takes the copy path);
+    host polls a completion word (rx_burst_zero_copy, up to 4096 frames; 4097 takes the copy path) or
+    the results themselves (TUNE_BURST_ZERO_COPY 2);
     the same results as the copy pipeline (TUNE_BURST_ZERO_COPY 0), a pageable ring (copy path) and
     the oracle, for RxBurstHost and RxValidateIPHost; the ring is never written."""
     rng = random.Random(900 + n + (form == "offlen"))
@@ -209,7 +210,7 @@ def test_rx_burst_host_zero_copy(n, form):
     want_f = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
     want_a = np.array([netcsum.rx_action(int(x), oo.transport_proto(f), len(f) and f[0] >> 4 == 6)
                        for x, f in zip(want_f, frames)], np.uint8)
-    for zc, ring in ((1, _pinned(buf)), (0, _pinned(buf)), (1, buf.copy())):
+    for zc, ring in ((1, _pinned(buf)), (2, _pinned(buf)), (0, _pinned(buf)), (1, buf.copy())):
         netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
         try:
             act = np.full(n, 0xEE, np.uint8)
@@ -293,7 +294,7 @@ def test_tx_burst_host_zero_copy(n, form):
     for i in range(n):                                     # the flags the oracle gives the stack's frame
         o = i * stride + lead
         want_f[i] = op.tx_finalize_ip(bytes(buf[o:(i + 1) * stride]), True)[1]
-    for zc in (1, 0):
+    for zc in (1, 2, 0):
         netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
         try:
             hb = _pinned(buf)

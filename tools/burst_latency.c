@@ -145,7 +145,54 @@ static double time_us(kind_t k, uint32_t n)
     return median(t, REPS);
 }
 
-int main(void)
+/* "zc": only the zero-copy bursts of 1 / 64 frames, 2000 calls each, plus the host-side pieces of
+ * their cost (pointer-attribute queries, an empty-stream synchronise) — the program rocprofv3 traces
+ * for the per-call breakdown. */
+static int zc_only(void)
+{
+    static const uint32_t sizes[] = {1u, 64u};
+    hipPointerAttribute_t at;
+    double t0, t[2000];
+    uint32_t s;
+    int r, b;
+    for (r = 0; r < 2000; ++r) {
+        t0 = now_us();
+        HIP_OK(hipPointerGetAttributes(&at, g_hring));
+        t[r] = now_us() - t0;
+    }
+    printf("{\"pointer_attributes_us\": %.3f", median(t, 2000));
+    for (r = 0; r < 2000; ++r) {
+        t0 = now_us();
+        HIP_OK(hipStreamSynchronize(g_st));
+        t[r] = now_us() - t0;
+    }
+    printf(", \"empty_stream_sync_us\": %.3f", median(t, 2000));
+    for (b = 0; b <= 5; b += 1) {
+        if (b == 1 || b == 2 || b == 4) continue;           /* bound 0, 3; 5 = bound 3 + polled results */
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, b == 5 ? 3 : b));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b == 5 ? 2 : 1));
+        for (s = 0; s < 2; ++s) {
+            for (r = 0; r < 2000; ++r) {
+                t0 = now_us();
+                NET_OK(NetUtil_MI355X_RxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], 0u, g_hact, NULL, 0u));
+                t[r] = now_us() - t0;
+            }
+            printf(", \"rx_host_zc_b%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
+            for (r = 0; r < 2000; ++r) {
+                t0 = now_us();
+                NET_OK(NetUtil_MI355X_TxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], NULL, 0u));
+                t[r] = now_us() - t0;
+            }
+            printf(", \"tx_host_zc_b%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
+        }
+    }
+    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, -1));
+    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 1));
+    printf("}\n");
+    return 0;
+}
+
+int main(int argc, char **argv)
 {
     static const uint32_t sizes[] = {1u, 10u, 16u, 32u, 64u, 128u, 256u, 1024u, 4096u, 16384u, 65536u, 262144u};
     const size_t bytes = (size_t)NMAX * SLOT;
@@ -159,6 +206,7 @@ int main(void)
     for (i = 0; i < NMAX; ++i) build(g_hring + (size_t)i * SLOT);
     NET_OK(NetUtil_MI355X_TxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, NMAX, NULL, 8u));   /* valid sums */
     HIP_OK(hipMemcpy(g_dring, g_hring, bytes, hipMemcpyHostToDevice));
+    if (argc > 1 && strcmp(argv[1], "zc") == 0) return zc_only();
     for (s = 0; s < sizeof sizes / sizeof sizes[0]; ++s) {
         const uint32_t n = sizes[s];
         double rx_dev, tx_dev, rx_host, tx_host;

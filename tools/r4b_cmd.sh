@@ -13,6 +13,8 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method threa
 tail -3 "$O/tests.log"
 timeout -k 10 300 tools/build/burst_latency > "$O/burst_latency.jsonl" 2> "$O/burst_latency.err" || { tail -20 "$O/burst_latency.err"; exit 1; }
 cat "$O/burst_latency.jsonl" | cut -c1-400
+timeout -k 10 120 tools/build/burst_latency zc > "$O/burst_zc.jsonl" 2> "$O/burst_zc.err" || { tail -20 "$O/burst_zc.err"; exit 1; }
+cat "$O/burst_zc.jsonl"
 timeout -k 10 500 python -u tools/ring_probe.py > "$O/ring_probe.jsonl" 2> "$O/ring_probe.err" || { tail -20 "$O/ring_probe.err"; exit 1; }
 python3 - "$O/ring_probe.jsonl" <<'PY'
 import json,sys

@@ -1272,6 +1272,30 @@ static NET_ERR burst_wait(HostCtx& c, uint32_t tag) {
     return NET_UTIL_ERR_NONE;
 }
 
+// Polls until ready(i) holds for every i < n (each result is written once by the kernel, into
+// coherent memory initialised to a sentinel), scanning forward; after 2 s a stream synchronisation
+// reports a failed launch.
+extern "C++" {
+template <class Ready>
+static NET_ERR burst_poll(HostCtx& c, Ready ready, uint32_t n) {
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t i = 0, spin = 0;
+    while (i < n) {
+        if (ready(i)) {
+            ++i;
+            continue;
+        }
+        if ((++spin & 1023u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            NC_HIP(hipStreamSynchronize(c.stream));
+            for (; i < n; ++i) {
+                if (!ready(i)) return dev_fail("burst results", hipErrorUnknown);
+            }
+        }
+    }
+    return NET_UTIL_ERR_NONE;
+}
+}  // extern "C++"
+
 // Rx over a pinned ring in place. *taken = false: the burst does not qualify (the caller takes the
 // copy path); else the call's result.
 static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t* h_off, const uint16_t* h_len,
@@ -1298,6 +1322,21 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
         std::memcpy(c.h_burst + kBurstLen, h_len, (size_t)n_pkt * 2u);
         d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
         d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
+    }
+    if (g_tune_burst_zc.load() == 2) {                  // results straight into coherent memory, polled
+        uint8_t* hf = c.h_burst + kBurstFlags;
+        uint8_t* ha = c.h_burst + kBurstAct;
+        std::memset(hf, 0xFF, n_pkt);                   // sentinels: no flag byte or action is 0xFF
+        std::memset(ha, 0xFF, n_pkt);
+        e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, c.h_burst_dev + kBurstFlags, 1u, false, 0, c.stream,
+                      c.h_burst_dev + kBurstAct, rx_cfg);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hf + i) != 0xFFu &&
+                                                   *(volatile uint8_t*)(ha + i) != 0xFFu; }, n_pkt);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        if (h_flags) std::memcpy(h_flags, hf, n_pkt);
+        if (h_action) std::memcpy(h_action, ha, n_pkt);
+        return NET_UTIL_ERR_NONE;
     }
     uint8_t* d_fl = c.d_burst;
     uint8_t* d_act = h_action ? c.d_burst + kBurstZC : nullptr;
@@ -1359,18 +1398,29 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
         d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
     }
-    netcsum::PktTxRecord* d_rec = reinterpret_cast<netcsum::PktTxRecord*>(c.d_burst + kBurstDevRec);
-    e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
-                  nullptr, d_rec);
-    if (e != NET_UTIL_ERR_NONE) return e;
-    if (++c.seq == 0u) c.seq = 1u;
-    const uint32_t tag = c.seq;
-    *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
-    NC_HIP(netcsum::launch_burst_done(reinterpret_cast<const uint8_t*>(d_rec), nullptr, n_pkt * 8u,
-                                      c.h_burst_dev + kBurstRec, nullptr,
-                                      reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstWord), tag, c.stream));
-    e = burst_wait(c, tag);
-    if (e != NET_UTIL_ERR_NONE) return e;
+    if (g_tune_burst_zc.load() == 2) {                  // records straight into coherent memory, polled
+        uint8_t* hr = c.h_burst + kBurstRec;
+        std::memset(hr, 0xFF, (size_t)n_pkt * 8u);     // sentinel: a record's store byte is 0..3
+        e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
+                      nullptr, reinterpret_cast<netcsum::PktTxRecord*>(c.h_burst_dev + kBurstRec));
+        if (e != NET_UTIL_ERR_NONE) return e;
+        e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hr + 8u * i + 7u) != 0xFFu; }, n_pkt);
+        if (e != NET_UTIL_ERR_NONE) return e;
+    } else {
+        netcsum::PktTxRecord* d_rec = reinterpret_cast<netcsum::PktTxRecord*>(c.d_burst + kBurstDevRec);
+        e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
+                      nullptr, d_rec);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        if (++c.seq == 0u) c.seq = 1u;
+        const uint32_t tag = c.seq;
+        *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
+        NC_HIP(netcsum::launch_burst_done(reinterpret_cast<const uint8_t*>(d_rec), nullptr, n_pkt * 8u,
+                                          c.h_burst_dev + kBurstRec, nullptr,
+                                          reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstWord), tag,
+                                          c.stream));
+        e = burst_wait(c, tag);
+        if (e != NET_UTIL_ERR_NONE) return e;
+    }
     uint8_t* hb = static_cast<uint8_t*>(h_base);
     const uint64_t* rec = reinterpret_cast<const uint64_t*>(c.h_burst + kBurstRec);
     std::vector<uint64_t> walk_off;
@@ -1674,7 +1724,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         netcsum::set_crc_nt(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BURST_ZERO_COPY:
-        if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_burst_zc.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
