@@ -245,8 +245,7 @@ def test_pkt_stream_v6_and_mixed_vs_oracle(ver, stride, pkt_len, lead, passes):
     tag = "v6" if ver == 6 else "mixed"
     assert d_rx.startswith("pkt_stream_kernel") and f",rx,{tag}>" in d_rx and f",tx,{tag}>" in d_tx, (d_rx, d_tx)
     assert d_rx.endswith(" +inline_v6_walk"), d_rx
-    assert d_tx.endswith(" +pkt_scatter_kernel +inline_v6_walk" if passes == 2 else "> block=256 pkts_per_wave="
-                         + d_tx.split("pkts_per_wave=")[1].split(" ")[0] + " +inline_v6_walk"), d_tx
+    assert d_tx.endswith(" +inline_v6_walk") and (" +pkt_scatter_kernel" in d_tx) == (passes == 2), d_tx
     bad = np.nonzero(rx != rx_w)[0]
     assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
     bad = np.nonzero(tx != tx_w)[0]

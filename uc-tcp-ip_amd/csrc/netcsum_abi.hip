@@ -992,9 +992,9 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
             spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
         }
         char desc[144];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s,bound=%d%s> block=256 pkts_per_wave=%u%s%s", d,
-                 snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", bound,
-                 d_off ? ",offlen" : "", spw,
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s", d,
+                 snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, bound,
+                 d_off ? " offlen" : "",
                  two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "");
         netcsum::set_last_launch(desc);
         if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
