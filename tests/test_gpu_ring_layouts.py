@@ -97,7 +97,7 @@ def _check(got, want, what):
     assert bad.size == 0, (what, [(int(i), int(got[i]), int(want[i])) for i in bad[:6]])
 
 
-@pytest.mark.parametrize("bound", [0, 1, 2, 3])
+@pytest.mark.parametrize("bound", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64), (1536, 1), (9216, 2)])
 @pytest.mark.parametrize("passes", [1, 2])
 def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
@@ -120,7 +120,7 @@ def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
     _check(ft.cpu().numpy(), txf_w, "tx flags")
 
 
-@pytest.mark.parametrize("bound", [0, 1, 2, 3])
+@pytest.mark.parametrize("bound", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("spw", [1, 8, 64])
 def test_mixed_version_ring_every_bound_vs_oracle(bound, spw):
     """IPv4 and IPv6 frames in one 1520-B-slot ring (RxValidateIP / TxFinalizeIP), runs of 1..64."""
@@ -181,14 +181,14 @@ def test_bounded_stream_full_size_ring_properties():
     b[: n * slot].view(n, slot)[:, lead:lead + 40] = torch.from_numpy(h).to(DEV)
     base = b[lead:]
     outs = []
-    for bound in (0, 1, 2, 3):
+    for bound in (0, 1, 2, 3, 4):
         netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
         c = b.clone()
         netcsum.tx_finalize_ipv4(c[lead:], n, None, stride=slot, pkt_len=slot - lead)
         outs.append(c)
     torch.cuda.synchronize()
     assert all(torch.equal(outs[0], o) for o in outs[1:])
-    b.copy_(outs[3])
+    b.copy_(outs[4])
     del outs
     f = torch.zeros(n, dtype=torch.uint8, device=DEV)
     netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
@@ -209,12 +209,14 @@ def test_bounded_stream_full_size_ring_properties():
 
 @pytest.mark.parametrize("order", ["sorted", "reversed", "shuffled", "duplicates", "far", "packed"])
 @pytest.mark.parametrize("spw", [-1, 1, 7, 64])
-def test_offset_length_runs_every_order_vs_oracle(order, spw):
+@pytest.mark.parametrize("bound", [3, 4])
+def test_offset_length_runs_every_order_vs_oracle(order, spw, bound):
     """Offset/length batches in the live-piece stream (netcsum_pktstream.hip, VL): a run of
     descriptors in increasing address order within 128 KiB streams; any other run (reversed or
     shuffled rings, the same datagram listed twice, slots > 128 KiB apart) is done datagram by
     datagram. Mixed IPv4 / IPv6 (RxValidateIP, TxFinalizeIP, RxBurst), results equal the oracle's."""
     netcsum.tune(netcsum.TUNE_TILE, spw)
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
     rng = random.Random(zlib.crc32(f"{order}/{spw}".encode()))
     n, slot, lead = 700, 1520, 14
     buf, lens = _ring(rng, n, slot, lead, v6mix=True)

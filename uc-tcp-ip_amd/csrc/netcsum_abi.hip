@@ -987,7 +987,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const bool two = tx && (rec_only != nullptr || tp == 2 || (tp == 0 && n_pkt >= 65536u));
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
-        if (bound == 3 && d_off == nullptr) {
+        if (bound >= 3 && d_off == nullptr) {
             const uint64_t cap = (128u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
         }
@@ -1728,7 +1728,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_burst_zc.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
-        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_pkt_bound.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:

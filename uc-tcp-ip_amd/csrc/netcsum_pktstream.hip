@@ -398,7 +398,8 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 // BND 0: every piece of the run streamed whole (the round-3 form); 1: the first D pieces whole, the
 // refills bounded by the parsed ends; 2: the parse first, then every piece bounded; 3: live pieces
 // (below): the parse first, then only the pieces holding summed bytes, each masked to its live
-// 64-B sectors (runs of <= 128 pieces).
+// 64-B sectors (runs of <= 128 pieces); 4: the same with the run's piece 0 (which holds the first
+// datagram's start) loaded whole while the parse runs.
 //
 // Live pieces (BND 3). After the parse each lane marks its datagram's summed bytes [a, a + end) as
 // 64-B sectors (the HBM access unit) in a per-wave bitmap in LDS (2048 bits: a run spans <= 128 KiB),
@@ -431,6 +432,9 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
         }
     }
+    if constexpr (BND == 4) {                                  // piece 0 (the first datagram's start)
+        dv[0] = buf_load16<NT>(rd, lane16);                    // whole, while the parse runs
+    }
 
     // ... while lane k parses packet k from its own 96-B window.
     const bool mine = lane < nres;
@@ -460,7 +464,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     uint64_t lm0 = 0u, lm1 = 0u;                               // BND 3: live pieces 0-63 / 64-127
     uint32_t pm0 = 0u, pm1 = 0u;                               // BND 3: sector masks of pieces l, l + 64
     uint32_t nlive = npieces;
-    if constexpr (BND == 3) {
+    if constexpr (BND >= 3) {
         __shared__ uint32_t sect_all[4][64];
         uint32_t* sect = sect_all[w];
         sect[lane] = 0u;
@@ -498,9 +502,14 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         return ((sm >> lsect) & 1u) ? (q << 10) + lane16 : kOOB;
     };
     uint32_t qd[D];                                            // BND 3: the piece in flight in slot j
-    if constexpr (BND == 3) {
+    if constexpr (BND >= 3) {
+        if constexpr (BND == 4) {                              // piece 0 is in flight already
+            nlive += (uint32_t)(lm0 & 1u) ^ 1u;
+            lm0 |= 1u;
+            qd[0] = pop();
+        }
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
+        for (int j = BND == 4 ? 1 : 0; j < D; ++j) {
             qd[j] = pop();
             dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
         }
@@ -563,7 +572,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     for (uint32_t r = 0; r < rounds; ++r) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            if constexpr (BND == 3) {
+            if constexpr (BND >= 3) {
                 consume(qd[j], opaque_tuple(dv[j]));
                 qd[j] = pop();                                                // none left: OOB, zeros
                 dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
@@ -668,7 +677,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 // a run of its own (correct for any order or overlap, at one prologue per datagram).
 template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
-    static_assert(!VL || BND == 3, "offset/length runs take the live-piece form");
+    static_assert(!VL || BND >= 3, "offset/length runs take the live-piece form");
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -888,19 +897,19 @@ void set_tx_flush(int mode) {
 // in the live-piece form.
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
-    if (a.off != nullptr) return bound == 3 && a.len != nullptr;
-    return a.len_u >= 64u && a.stride >= a.len_u && (bound == 3 || a.stride <= a.len_u + 64u) &&
+    if (a.off != nullptr) return bound >= 3 && a.len != nullptr;
+    return a.len_u >= 64u && a.stride >= a.len_u && (bound >= 3 || a.stride <= a.len_u + 64u) &&
            (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
 
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec, bool scatter) {
-    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3 || !pkt_stream_supported(a, ip_ver, bound)) {
+    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 4 || !pkt_stream_supported(a, ip_ver, bound)) {
         return hipErrorInvalidValue;
     }
     // live pieces: a strided run spans at most 128 pieces (the host sizes runs for it; offset/length
     // runs check their span on the device)
-    if (bound == 3 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
+    if (bound >= 3 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
         return hipErrorInvalidValue;
     }
     const bool vl = a.off != nullptr;
@@ -912,7 +921,8 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
     NETCSUM_P(V_, D_, true, false, B_, VL_) NETCSUM_P(V_, D_, false, false, B_, VL_)                      \
     NETCSUM_P(V_, D_, true, true, B_, VL_) NETCSUM_P(V_, D_, false, true, B_, VL_)
 #define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0, false) NETCSUM_PB(V_, 4, 1, false) NETCSUM_PB(V_, 4, 2, false)     \
-    NETCSUM_PB(V_, 4, 3, false) NETCSUM_PB(V_, 8, 3, false) NETCSUM_PB(V_, 4, 3, true) NETCSUM_PB(V_, 8, 3, true)
+    NETCSUM_PB(V_, 4, 3, false) NETCSUM_PB(V_, 8, 3, false) NETCSUM_PB(V_, 4, 3, true) NETCSUM_PB(V_, 8, 3, true) \
+    NETCSUM_PB(V_, 4, 4, false) NETCSUM_PB(V_, 4, 4, true)
     NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
 #undef NETCSUM_PV
 #undef NETCSUM_PB
