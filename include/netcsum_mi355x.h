@@ -653,10 +653,14 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_VARLEN_RUN_BYTES = 20,/* varlen stream kernel (C4): B > 0 = runs of about B bytes, the
                                          run length chosen on the device from sampled lengths; 0 =
                                          runs of 8 segments; -1 = the default (16 KiB)                 */
-    NETCSUM_TUNE_PKT_BOUND     = 21,  /* strided packet batches (run-stream form): which bytes of a slot
-                                         are read. 0 = the whole slot (pkt_len bytes), 1 = the first
-                                         pieces whole, then only each datagram's parsed extent, 2 = the
-                                         parse first, then only the parsed extents; -1 = the default (2) */
+    NETCSUM_TUNE_PKT_BOUND     = 21,  /* packet batches (run-stream form): which bytes are read. 0 = every
+                                         byte of each wave's span (dense strided layouts: gaps <= 64 B),
+                                         1 = only the 64-B sectors holding summed bytes (live pieces), the
+                                         parse first; 2 = live pieces with the run's first piece loaded
+                                         during the parse; 3 = live pieces with the run's first 4 (8)
+                                         pieces loaded during the parse (dense strided layouts);
+                                         -1 = the default: 3 for dense strided, 2 for sparse strided and
+                                         offset/length batches                                       */
     NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
                                          1 (default) a completion kernel copies the results out and stores

@@ -34,7 +34,7 @@ thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read 
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 thread_local netcsum::TuneKnob g_tune_burst_zc{1};              // host bursts read pinned rings in place
-thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto (3), 0..3
+thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
@@ -900,7 +900,8 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
                          CPU_INT16U pkt_len, uint32_t n_pkt, uint8_t* d_flags, uint32_t udp_mode, bool tx,
                          int ip_ver, void* hip_stream, uint8_t* d_action = nullptr, uint32_t rx_cfg = 0u,
-                         uint32_t* d_fieldpos = nullptr, netcsum::PktTxRecord* rec_only = nullptr) {
+                         uint32_t* d_fieldpos = nullptr, netcsum::PktTxRecord* rec_only = nullptr,
+                         int bound_pref = -1) {
     if (n_pkt == 0) return NET_UTIL_ERR_NONE;
     if (n_pkt > 0x7FFFFFFFu) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     if (d_base == nullptr || (d_off != nullptr) != (d_len != nullptr) || (!tx && d_flags == nullptr && d_action == nullptr)) {
@@ -962,16 +963,27 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     const bool walk = ip_ver != 4;
     const bool own_flags = walk && d_flags == nullptr;
     hipStream_t hs = static_cast<hipStream_t>(hip_stream);
-    // which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND; 3 = live pieces, whose runs span at
-    // most 128 KiB); offset/length batches stream in the live-piece form only
+    // Which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND, netcsum_pktstream.hip): by default the
+    // live pieces — dense strided layouts (gaps <= 64 B) with their first pieces loaded during the
+    // parse (3), sparse strided and offset/length layouts with piece 0 (2); a burst read in place from
+    // host memory may prefer the whole-span form 0 (bound_pref: one PCIe round trip). Live-piece runs
+    // span at most 128 KiB.
     const int d = g_tune_chunks.load() == 8 ? 8 : 4;
-    const int bound = d == 8 ? 3 : (g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load());
+    const bool dense = d_off == nullptr && stride <= (uint64_t)pkt_len + 64u;
+    int bound = g_tune_pkt_bound.load() >= 0 ? g_tune_pkt_bound.load() : (dense ? 3 : 2);
+    if (bound_pref >= 0 && g_tune_pkt_bound.load() < 0) {   // the caller's preference, where it applies
+        if (netcsum::pkt_stream_supported(a, ip_ver, bound_pref)) bound = bound_pref;
+    }
+    if (d == 8 && bound == 1) bound = 2;                    // (8 pieces in flight: forms 0, 2, 3)
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver, bound)) {
         // offset/length runs: 16 datagrams (their lengths are on the device; the device checks each
         // run's order and reach, and takes a run datagram by datagram otherwise)
-        const uint64_t per = d_off ? 1280u : std::max<uint64_t>(a.stride, 1u);
+        // the live-piece forms parse first, so their runs are longer: about 32 KB of span (r4e ring
+        // probe, profiles/r4e_ring_probe.jsonl: 1520-B slots 8 -> 16 datagrams 0.2575 -> 0.2281 ms)
+        const uint64_t per = d_off ? 2048u : std::max<uint64_t>(a.stride, 1u);
+        const uint64_t budget = bound == 0 ? 20480u : 32768u;
         const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
-                                         : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
+                                         : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (budget / per) & ~7ull));
         // small batches (NIC bursts) are latency-bound: a run costs ~run x len / 4 KiB memory round
         // trips, so runs halve until the batch spreads over >= 2048 waves (burst of 256 mixed frames:
         // Rx 19.9 -> 13.3 us, Tx 22.8 -> 15.7 us; 16 Ki frames: runs of 8, 19.2 -> 17.2 us;
@@ -987,7 +999,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const bool two = tx && (rec_only != nullptr || tp == 2 || (tp == 0 && n_pkt >= 65536u));
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
-        if (bound >= 3 && d_off == nullptr) {
+        if (bound >= 1 && d_off == nullptr) {
             const uint64_t cap = (128u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
         }
@@ -1226,6 +1238,11 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
 // the wave's own stores); the host polls that word, as the drop-in's single-block sums do, instead of
 // synchronising the stream, and copies the results out. A pageable ring takes the copy path.
 constexpr uint32_t kBurstZC = 4096u;                    // frames
+// Over PCIe a burst is latency-bound: the whole-slot stream (bound 0) issues the pieces with the
+// parse's loads (one round trip) where the live-piece forms parse first (two); it applies to
+// strided rings with gaps <= 64 B, the others keep the default (tools/burst_latency.c zc,
+// profiles/r4d_burst_zc.jsonl: 64 frames 17.4 -> 15.6 us)
+constexpr int kBurstBound = 0;
 constexpr uint64_t kBurstZCSpan = 64ull << 20;          // ring bytes the kernel may read in place
 constexpr size_t kBurstWord = 0, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
                  kBurstOff = kBurstAct + kBurstZC, kBurstLen = kBurstOff + 8u * kBurstZC,
@@ -1329,7 +1346,7 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
         std::memset(hf, 0xFF, n_pkt);                   // sentinels: no flag byte or action is 0xFF
         std::memset(ha, 0xFF, n_pkt);
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, c.h_burst_dev + kBurstFlags, 1u, false, 0, c.stream,
-                      c.h_burst_dev + kBurstAct, rx_cfg);
+                      c.h_burst_dev + kBurstAct, rx_cfg, nullptr, nullptr, kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
         e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hf + i) != 0xFFu &&
                                                    *(volatile uint8_t*)(ha + i) != 0xFFu; }, n_pkt);
@@ -1340,7 +1357,8 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
     }
     uint8_t* d_fl = c.d_burst;
     uint8_t* d_act = h_action ? c.d_burst + kBurstZC : nullptr;
-    e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, d_fl, 1u, false, 0, c.stream, d_act, rx_cfg);
+    e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, d_fl, 1u, false, 0, c.stream, d_act, rx_cfg, nullptr,
+                  nullptr, kBurstBound);
     if (e != NET_UTIL_ERR_NONE) return e;
     if (++c.seq == 0u) c.seq = 1u;
     const uint32_t tag = c.seq;
@@ -1402,14 +1420,14 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         uint8_t* hr = c.h_burst + kBurstRec;
         std::memset(hr, 0xFF, (size_t)n_pkt * 8u);     // sentinel: a record's store byte is 0..3
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
-                      nullptr, reinterpret_cast<netcsum::PktTxRecord*>(c.h_burst_dev + kBurstRec));
+                      nullptr, reinterpret_cast<netcsum::PktTxRecord*>(c.h_burst_dev + kBurstRec), kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
         e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hr + 8u * i + 7u) != 0xFFu; }, n_pkt);
         if (e != NET_UTIL_ERR_NONE) return e;
     } else {
         netcsum::PktTxRecord* d_rec = reinterpret_cast<netcsum::PktTxRecord*>(c.d_burst + kBurstDevRec);
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
-                      nullptr, d_rec);
+                      nullptr, d_rec, kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
         if (++c.seq == 0u) c.seq = 1u;
         const uint32_t tag = c.seq;
@@ -1728,7 +1746,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_burst_zc.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
-        if (value < -1 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_pkt_bound.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:

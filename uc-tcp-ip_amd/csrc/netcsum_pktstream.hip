@@ -31,7 +31,9 @@
 // datagram (lead = its address mod 16); a chain beyond it gets EXT_HDR, as the lane-group kernel's
 // beyond its 16 G - lead bytes, and the walk pass (netcsum_v6walk.hip) finishes it.
 //
-// Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64, gap <= 64 B).
+// Domain (pkt_stream_supported): strided batches (stride >= pkt_len >= 64; gaps <= 64 B for the
+// whole-span bounds 0 and 3, any gap for the live-piece bounds 1 and 2) and offset/length batches
+// (bounds 1 and 2).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -346,37 +348,6 @@ __device__ __forceinline__ void store_field(uint8_t* p, uint32_t v) {    // memc
     q[1] = (uint8_t)(v >> 8);
 }
 
-// Bounded stream (BND >= 1). A NIC ring's slots are larger than most of its frames: 1518 / 1520-B
-// pool buffers holding 40-B ACKs (Cfg/Template/net_dev_cfg.c:146-149, one NET_BUF per frame,
-// Source/net_buf.h:595-598, the frame length per frame from the driver, IF/net_if.c:6593), or 2-KiB
-// buffers whose present bytes the caller passes as pkt_len. Streaming the whole run fetches every
-// slot whole. Here a lane's 16-B chunk at run offset x is loaded only when it holds a byte that some
-// packet of the run sums — [lead0 + p*st, lead0 + p*st + end_p), end_p parsed in the prologue —
-// and otherwise gets the out-of-range offset (zeros, no memory request). The stream's sums only ever
-// take differences of prefixes inside [start, end) ranges, so zero-filled bytes outside them change
-// nothing. The chunk overlaps the slot of packet p0 = floor((x - lead0) / st) and perhaps the start of
-// p0 + 1 (st >= 64 > 16); their ends come from lanes p0 and p0 + 1 by ds_bpermute.
-struct RunBound {
-    uint32_t lead0, st, nres;
-    float inv_st;
-};
-
-__device__ __forceinline__ uint32_t bounded_voff(uint32_t x, const RunBound& b, uint32_t end_v) {
-    const bool before = x < b.lead0;                               // only in the run's first line
-    const uint32_t rel = x - b.lead0;
-    uint32_t p = (uint32_t)((float)(before ? 0u : rel) * b.inv_st);   // rel < 2^23: off by <= 1
-    p = (p * b.st > rel) ? p - 1u : p;
-    p = ((p + 1u) * b.st <= rel) ? p + 1u : p;
-    const uint32_t p0 = before ? 0u : p, p1 = before ? 0u : p + 1u;
-    const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p0 & 63u) << 2), (int)end_v);
-    const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p1 & 63u) << 2), (int)end_v);
-    const uint32_t s0 = b.lead0 + p0 * b.st;
-    const uint32_t s1 = b.lead0 + p1 * b.st;
-    const bool live0 = !before && p0 < b.nres && x < s0 + e0;
-    const bool live1 = p1 < b.nres && s1 < x + 16u && e1 != 0u;
-    return (live0 || live1) ? x : kOOB;
-}
-
 // REC (Tx only): instead of writing the checksum fields, write one PktTxRecord per packet (dense,
 // coalesced); pkt_scatter_kernel then writes the fields in a pass of its own.
 template <int VER, bool TX>
@@ -395,21 +366,29 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 }
 
 // VER 4 / 6: one IP version per batch; VER 0: per datagram by the version nibble (a mixed ring).
-// BND 0: every piece of the run streamed whole (the round-3 form); 1: the first D pieces whole, the
-// refills bounded by the parsed ends; 2: the parse first, then every piece bounded; 3: live pieces
-// (below): the parse first, then only the pieces holding summed bytes, each masked to its live
-// 64-B sectors (runs of <= 128 pieces); 4: the same with the run's piece 0 (which holds the first
-// datagram's start) loaded whole while the parse runs.
 //
-// Live pieces (BND 3). After the parse each lane marks its datagram's summed bytes [a, a + end) as
-// 64-B sectors (the HBM access unit) in a per-wave bitmap in LDS (2048 bits: a run spans <= 128 KiB),
-// by ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfwords l and
+// Which bytes are read (BND, NETCSUM_TUNE_PKT_BOUND). A NIC ring's slots are larger than most of its
+// frames: 1518 / 1520-B pool buffers holding 40-B ACKs (Cfg/Template/net_dev_cfg.c:146-149, one NET_BUF
+// per frame, Source/net_buf.h:595-598, the frame length per frame from the driver, IF/net_if.c:6593),
+// or 2-KiB buffers whose present bytes the caller passes as pkt_len.
+//   0  the round-3 form: every 1-KiB piece of the run's span, the first D issued with the parse's
+//      loads (dense strided layouts only: gaps <= 64 B);
+//   1  live pieces, the parse first: only the pieces holding summed bytes are loaded, each masked to
+//      its live 64-B sectors (below);
+//   2  live pieces, with the run's piece 0 (which holds the first datagram's start) loaded whole
+//      while the parse runs;
+//   3  live pieces, with the run's first D pieces loaded whole while the parse runs (dense strided
+//      layouts: at most D KiB per run read past the summed bytes; the rest as 1).
+// Live pieces. After the parse each lane marks its datagram's summed bytes [a, a + end) as 64-B
+// sectors (the HBM access unit) in a per-wave bitmap in LDS (2048 bits: a run spans <= 128 KiB), by
+// ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfwords l and
 // l + 64, and a ballot of their non-zero values gives the run's live pieces as two uniform 64-bit
 // masks. The stream then pops live pieces in address order (scalar find-first-set), skipping dead
 // ones entirely (no load, no consume), and lane l of piece q loads its 16 B only if sector l / 4 of
-// the piece's mask (one readlane) is set. The consume walk is unchanged except that offsets below
-// the piece clamp to 0: a datagram with nothing to sum (malformed: end 0) may start in a skipped
-// piece, and its event then falls in a later one with an empty range.
+// the piece's mask (one readlane) is set. The stream's sums only take differences of prefixes inside
+// [start, end) ranges, so zero-filled (unloaded) bytes outside them change nothing. The consume walk
+// clamps offsets below the piece to 0: a datagram with nothing to sum (malformed: end 0) may start in
+// a skipped piece, and its event then falls in a later one with an empty range.
 constexpr uint32_t kNoPiece = 0x3FFFFu;                 // past every run (qb < 2^28)
 // One wave run: packets s_begin .. s_begin + nres - 1, lane k's packet at run-relative offset prel
 // (from O, 128-B aligned) with `avail` bytes present; the run's bytes [O, O + span). VL: per-packet
@@ -426,14 +405,10 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     const uint32_t lane16 = 16u * lane;
 
     u32x4 dv[D];
-    if constexpr (BND < 2) {
+    constexpr int kSpec = BND == 0 || BND == 3 ? D : BND == 2 ? 1 : 0;   // pieces loaded before the parse
 #pragma unroll
-        for (int j = 0; j < D; ++j) {                          // first D pieces in flight ...
-            dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
-        }
-    }
-    if constexpr (BND == 4) {                                  // piece 0 (the first datagram's start)
-        dv[0] = buf_load16<NT>(rd, lane16);                    // whole, while the parse runs
+    for (int j = 0; j < kSpec; ++j) {                          // the first pieces in flight ...
+        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
 
     // ... while lane k parses packet k from its own 96-B window.
@@ -460,11 +435,10 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     // the prologue's peak to 73 = 6 waves/SIMD).
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
-    const RunBound rb{lead0, st, nres, 1.0f / (float)max(st, 1u)};
-    uint64_t lm0 = 0u, lm1 = 0u;                               // BND 3: live pieces 0-63 / 64-127
-    uint32_t pm0 = 0u, pm1 = 0u;                               // BND 3: sector masks of pieces l, l + 64
+    uint64_t lm0 = 0u, lm1 = 0u;                               // live pieces 0-63 / 64-127
+    uint32_t pm0 = 0u, pm1 = 0u;                               // sector masks of pieces l, l + 64
     uint32_t nlive = npieces;
-    if constexpr (BND >= 3) {
+    if constexpr (BND >= 1) {
         __shared__ uint32_t sect_all[4][64];
         uint32_t* sect = sect_all[w];
         sect[lane] = 0u;
@@ -485,7 +459,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         nlive = (uint32_t)__builtin_popcountll(lm0) + (uint32_t)__builtin_popcountll(lm1);
     }
     const uint32_t lsect = lane >> 2;                          // the lane's 64-B sector in a piece
-    auto pop = [&]() -> uint32_t {                             // BND 3: next live piece (uniform)
+    auto pop = [&]() -> uint32_t {                             // next live piece (uniform)
         // selects only (a branch choosing which mask to clear made the compiler address the two
         // masks through a pointer, i.e. scratch memory)
         const bool z0 = lm0 == 0u;
@@ -495,29 +469,26 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         lm0 &= lm0 - 1u;
         return q;
     };
-    auto live_voff = [&](uint32_t q) -> uint32_t {             // BND 3: lane's offset in piece q, or OOB
+    auto live_voff = [&](uint32_t q) -> uint32_t {             // lane's offset in piece q, or OOB
         const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)(q & 63u));
         const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)pm1, (int)(q & 63u));
         const uint32_t sm = q < 64u ? r0 : (q < 128u ? r1 : 0u);
         return ((sm >> lsect) & 1u) ? (q << 10) + lane16 : kOOB;
     };
-    uint32_t qd[D];                                            // BND 3: the piece in flight in slot j
-    if constexpr (BND >= 3) {
-        if constexpr (BND == 4) {                              // piece 0 is in flight already
-            nlive += (uint32_t)(lm0 & 1u) ^ 1u;
-            lm0 |= 1u;
-            qd[0] = pop();
+    uint32_t qd[D];                                            // the piece in flight in slot j
+    if constexpr (BND >= 1) {
+        // pieces 0 .. kSpec - 1 are in flight already: consumed first, whether live or not
+        constexpr uint64_t spec = kSpec ? (1ull << kSpec) - 1u : 0u;
+        nlive = (uint32_t)__builtin_popcountll(lm0 | spec) + (uint32_t)__builtin_popcountll(lm1);
+        lm0 &= ~spec;
+#pragma unroll
+        for (int j = 0; j < kSpec; ++j) {
+            qd[j] = (uint32_t)j;
         }
 #pragma unroll
-        for (int j = BND == 4 ? 1 : 0; j < D; ++j) {
+        for (int j = kSpec; j < D; ++j) {
             qd[j] = pop();
             dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
-        }
-    }
-    if constexpr (BND == 2) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            dv[j] = buf_load16<NT>(rd, bounded_voff(((uint32_t)j << 10) + lane16, rb, end_v));
         }
     }
 
@@ -572,15 +543,14 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     for (uint32_t r = 0; r < rounds; ++r) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            if constexpr (BND >= 3) {
+            if constexpr (BND >= 1) {
                 consume(qd[j], opaque_tuple(dv[j]));
                 qd[j] = pop();                                                // none left: OOB, zeros
                 dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
             } else {
                 const uint32_t q = r * (uint32_t)D + (uint32_t)j;
                 consume(q, opaque_tuple(dv[j]));
-                const uint32_t x = ((q + (uint32_t)D) << 10) + lane16;        // past the run: zeros
-                dv[j] = buf_load16<NT>(rd, BND ? bounded_voff(x, rb, end_v) : x);
+                dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
             }
             asm volatile("" ::: "memory");
         }
@@ -677,7 +647,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 // a run of its own (correct for any order or overlap, at one prologue per datagram).
 template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
-    static_assert(!VL || BND >= 3, "offset/length runs take the live-piece form");
+    static_assert(!VL || BND == 1 || BND == 2, "offset/length runs take the live-piece forms 1 / 2");
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -897,23 +867,24 @@ void set_tx_flush(int mode) {
 // in the live-piece form.
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
-    if (a.off != nullptr) return bound >= 3 && a.len != nullptr;
-    return a.len_u >= 64u && a.stride >= a.len_u && (bound >= 3 || a.stride <= a.len_u + 64u) &&
+    if (a.off != nullptr) return (bound == 1 || bound == 2) && a.len != nullptr;
+    return a.len_u >= 64u && a.stride >= a.len_u && ((bound == 1 || bound == 2) || a.stride <= a.len_u + 64u) &&
            (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
 
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec, bool scatter) {
-    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 4 || !pkt_stream_supported(a, ip_ver, bound)) {
+    if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3 || !pkt_stream_supported(a, ip_ver, bound)) {
         return hipErrorInvalidValue;
     }
     // live pieces: a strided run spans at most 128 pieces (the host sizes runs for it; offset/length
     // runs check their span on the device)
-    if (bound >= 3 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
+    if (bound >= 1 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
         return hipErrorInvalidValue;
     }
     const bool vl = a.off != nullptr;
-    // every bound with 4 pieces in flight; 8 pieces and offset/length runs only in the live-piece form
+    // every bound with 4 pieces in flight, 8 with bounds 0, 2 and 3; offset/length runs in the
+    // live-piece forms 1 and 2
 #define NETCSUM_P(V_, D_, NT_, TX_, B_, VL_)                                                              \
     if (ip_ver == V_ && depth == D_ && nt == NT_ && tx == TX_ && bound == B_ && vl == VL_)                 \
         return launch_pkt_stream_t<D_, NT_, TX_, V_, B_, VL_>(a, spw, s, rec, scatter);
@@ -921,8 +892,8 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
     NETCSUM_P(V_, D_, true, false, B_, VL_) NETCSUM_P(V_, D_, false, false, B_, VL_)                      \
     NETCSUM_P(V_, D_, true, true, B_, VL_) NETCSUM_P(V_, D_, false, true, B_, VL_)
 #define NETCSUM_PV(V_) NETCSUM_PB(V_, 4, 0, false) NETCSUM_PB(V_, 4, 1, false) NETCSUM_PB(V_, 4, 2, false)     \
-    NETCSUM_PB(V_, 4, 3, false) NETCSUM_PB(V_, 8, 3, false) NETCSUM_PB(V_, 4, 3, true) NETCSUM_PB(V_, 8, 3, true) \
-    NETCSUM_PB(V_, 4, 4, false) NETCSUM_PB(V_, 4, 4, true)
+    NETCSUM_PB(V_, 4, 3, false) NETCSUM_PB(V_, 8, 0, false) NETCSUM_PB(V_, 8, 2, false) NETCSUM_PB(V_, 8, 3, false) \
+    NETCSUM_PB(V_, 4, 1, true) NETCSUM_PB(V_, 4, 2, true) NETCSUM_PB(V_, 8, 2, true)
     NETCSUM_PV(4) NETCSUM_PV(6) NETCSUM_PV(0)
 #undef NETCSUM_PV
 #undef NETCSUM_PB
