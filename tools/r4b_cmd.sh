@@ -9,10 +9,10 @@ O=gpurun_out/${1:-r4b}
 mkdir -p "$O"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_ring_layouts.py \
     tests/test_gpu_host.py tests/test_gpu_pktstream.py tests/test_gpu_packets.py tests/test_gpu_packets_v6.py \
-    tests/test_gpu_offload.py > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
+    tests/test_gpu_offload.py tests/test_gpu_threads.py > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
 tail -3 "$O/tests.log"
-timeout -k 10 300 tools/build/burst_latency > "$O/burst_latency.jsonl" 2> "$O/burst_latency.err" || { tail -20 "$O/burst_latency.err"; exit 1; }
-cat "$O/burst_latency.jsonl" | cut -c1-400
+# (full burst-size table: tools/build/burst_latency without "zc")
+
 timeout -k 10 120 tools/build/burst_latency zc > "$O/burst_zc.jsonl" 2> "$O/burst_zc.err" || { tail -20 "$O/burst_zc.err"; exit 1; }
 cat "$O/burst_zc.jsonl"
 timeout -k 10 500 python -u tools/ring_probe.py > "$O/ring_probe.jsonl" 2> "$O/ring_probe.err" || { tail -20 "$O/ring_probe.err"; exit 1; }
