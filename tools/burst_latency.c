@@ -167,23 +167,24 @@ static int zc_only(void)
         t[r] = now_us() - t0;
     }
     printf(", \"empty_stream_sync_us\": %.3f", median(t, 2000));
-    for (b = 0; b <= 5; b += 1) {
-        if (b == 1 || b == 2 || b == 4) continue;           /* bound 0, 3; 5 = bound 3 + polled results */
-        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, b == 5 ? 3 : b));
-        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b == 5 ? 2 : 1));
+    /* b = 0: the library's defaults; 1: results polled (TUNE_BURST_ZERO_COPY 2); 2: polled, live-piece
+     * stream with piece 0 during the parse (TUNE_PKT_BOUND 2) instead of the whole-span form */
+    for (b = 0; b <= 2; b += 1) {
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, b == 2 ? 2 : -1));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b >= 1 ? 2 : 1));
         for (s = 0; s < 2; ++s) {
             for (r = 0; r < 2000; ++r) {
                 t0 = now_us();
                 NET_OK(NetUtil_MI355X_RxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], 0u, g_hact, NULL, 0u));
                 t[r] = now_us() - t0;
             }
-            printf(", \"rx_host_zc_b%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
+            printf(", \"rx_host_zc_v%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
             for (r = 0; r < 2000; ++r) {
                 t0 = now_us();
                 NET_OK(NetUtil_MI355X_TxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], NULL, 0u));
                 t[r] = now_us() - t0;
             }
-            printf(", \"tx_host_zc_b%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
+            printf(", \"tx_host_zc_v%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
         }
     }
     NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, -1));
