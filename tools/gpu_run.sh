@@ -31,11 +31,11 @@ for s in $STEPS; do
   prof)
     ( cd /tmp && export TMPDIR=/tmp &&
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${T}_trace -o trace --output-format csv \
-        -- python3 $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline --pmc off > $O/${T}_prof_bench.json 2> $O/${T}_prof_trace.err &&
+        -- python3 $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-c5-point --pmc off > $O/${T}_prof_bench.json 2> $O/${T}_prof_trace.err &&
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/${T}_fetch -o fetch --output-format csv \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --pmc off > /dev/null 2> $O/${T}_pmc_fetch.err &&
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --no-c5-point --pmc off > /dev/null 2> $O/${T}_pmc_fetch.err &&
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/${T}_write -o write --output-format csv \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --pmc off > /dev/null 2> $O/${T}_pmc_write.err
+        -- python3 $R/bench.py --steps 3 --warmup 1 --ramp-seconds 0 --no-cpu-baseline --no-c5-point --pmc off > /dev/null 2> $O/${T}_pmc_write.err
     ) || { tail -20 $O/${T}_prof_trace.err $O/${T}_pmc_*.err; exit 1; }
     cat $O/${T}_prof_bench.json
     d() { dirname "$(find $O/${T}_$1 -name "$1_$2" -print -quit)"; }
