@@ -65,13 +65,22 @@ def main():
         netcsum.tx_finalize_ipv4(r["base"], n, None, stream=st, **strided)
         torch.cuda.synchronize()
         ref = r["buf"].clone()
-        variants = [("strided.b0", 0, -1, strided), ("strided.b1", 1, -1, strided), ("strided.b2", 2, -1, strided),
-                    ("strided.b3", 3, -1, strided), ("strided.b2.s8", 2, 8, strided),
-                    ("strided.b3.s8", 3, 8, strided), ("strided.b2.s32", 2, 32, strided),
-                    ("offlen", -1, -1, desc), ("offlen.b2.s32", 2, 32, desc), ("offlen.lanegroup", -1, -2, desc)]
+        # (tag, bound, datagrams per run, form, pieces in flight); RING_VARIANTS=dN selects the D=8 set
+        if os.environ.get("RING_VARIANTS") == "d8":
+            variants = [("strided.b0", 0, -1, strided, 4), ("strided.b2", 2, -1, strided, 4),
+                        ("strided.b2.d8", 2, -1, strided, 8), ("strided.b3.d8", 3, -1, strided, 8),
+                        ("strided.b2.s32.d8", 2, 32, strided, 8), ("offlen", -1, -1, desc, 4),
+                        ("offlen.d8", -1, -1, desc, 8)]
+        else:
+            variants = [("strided.b0", 0, -1, strided, 4), ("strided.b1", 1, -1, strided, 4),
+                        ("strided.b2", 2, -1, strided, 4), ("strided.b3", 3, -1, strided, 4),
+                        ("strided.b2.s8", 2, 8, strided, 4), ("strided.b3.s8", 3, 8, strided, 4),
+                        ("strided.b2.s32", 2, 32, strided, 4), ("offlen", -1, -1, desc, 4),
+                        ("offlen.b2.s32", 2, 32, desc, 4), ("offlen.lanegroup", -1, -2, desc, 4)]
         res = {}
         for p in range(2):
-            for tag, bound, spw, kw in variants:
+            for tag, bound, spw, kw, dd in variants:
+                netcsum.tune(netcsum.TUNE_CHUNKS, 8 if dd == 8 else 0)
                 netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
                 netcsum.tune(netcsum.TUNE_TILE, max(spw, -1))
                 netcsum.tune(netcsum.TUNE_KERNEL, 2 if spw == -2 else 0)   # the lane-group packet kernel
@@ -92,6 +101,7 @@ def main():
         netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
         netcsum.tune(netcsum.TUNE_TILE, -1)
         netcsum.tune(netcsum.TUNE_KERNEL, 0)
+        netcsum.tune(netcsum.TUNE_CHUNKS, 0)
         for (tag, op), d in res.items():
             algo = r["datagram_bytes"] + n * (1 if op == "rx" else 4)
             ms = min(d["ms"])
