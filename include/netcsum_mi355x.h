@@ -663,9 +663,9 @@ typedef enum netcsum_tune_key {
                                          offset/length batches                                       */
     NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
-                                         1 (default) a completion kernel copies the results out and stores
-                                         a completion word the host polls, 2 = the results go straight to
-                                         coherent pinned memory and the host polls them; 0 = the copy
+                                         2 (default) the results go straight to coherent pinned memory and
+                                         the host polls them, 1 = a completion kernel copies the results
+                                         out and stores a completion word the host polls; 0 = the copy
                                          pipeline (H2D, kernel, D2H, stream synchronisation)           */
 } NETCSUM_TUNE_KEY;
 

@@ -224,7 +224,7 @@ def test_rx_burst_host_zero_copy(n, form):
             netcsum.rx_burst_host(base(ring), n, act2, **kw)           # actions only
             assert np.array_equal(act2, want_a)
         finally:
-            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 1)
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
         r = ring.numpy() if hasattr(ring, "numpy") else ring
         assert np.array_equal(r, buf)
 
@@ -306,7 +306,7 @@ def test_tx_burst_host_zero_copy(n, form):
                 lens = np.full(n, stride - lead, np.uint16)
                 netcsum.tx_burst_host(hb, n, fl, off=offs, lens=lens)
         finally:
-            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 1)
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
         got = hb.numpy()
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (zc, [(int(j) // stride, int(j) % stride) for j in bad[:8]])

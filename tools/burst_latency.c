@@ -10,7 +10,7 @@
  *   rx_host / tx_host  RxBurstHost / TxBurstHost on a pinned host ring in one chunk, which return
  *                      with the results in host memory (_auto: n_chunks 0, the library's choice —
  *                      up to 4096 frames the kernel reads the pinned ring in place and the host
- *                      polls a completion word; _auto_copy: the same with NETCSUM_TUNE_BURST_ZERO_COPY
+ *                      polls the results; _auto_copy: the same with NETCSUM_TUNE_BURST_ZERO_COPY
  *                      0; from 1024 frames also in 2-16 chunks: _cK)
  * and a check that every Rx action is DELIVER. One JSON line per n on stdout.
  *
@@ -167,8 +167,9 @@ static int zc_only(void)
         t[r] = now_us() - t0;
     }
     printf(", \"empty_stream_sync_us\": %.3f", median(t, 2000));
-    /* b = 0: the library's defaults; 1: results polled (TUNE_BURST_ZERO_COPY 2); 2: polled, live-piece
-     * stream with piece 0 during the parse (TUNE_PKT_BOUND 2) instead of the whole-span form */
+    /* b = 0: a completion kernel and word (TUNE_BURST_ZERO_COPY 1); 1: results polled (2, the default);
+     * 2: polled, live-piece stream with piece 0 during the parse (TUNE_PKT_BOUND 2) instead of the
+     * whole-span form */
     for (b = 0; b <= 2; b += 1) {
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, b == 2 ? 2 : -1));
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b >= 1 ? 2 : 1));
@@ -188,7 +189,7 @@ static int zc_only(void)
         }
     }
     NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, -1));
-    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 1));
+    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
     printf("}\n");
     return 0;
 }
@@ -233,7 +234,7 @@ int main(int argc, char **argv)
         /* n_chunks 0 without the zero-copy burst path (the copy pipeline in one chunk) */
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 0));
         printf(", \"rx_host_us_auto_copy\": %.2f", time_us(RX_HOST, n));
-        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 1));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
         for (g_chunks = 2u; g_chunks <= 16u && n >= 1024u; g_chunks *= 2u) {
             printf(", \"rx_host_us_c%u\": %.2f", g_chunks, time_us(RX_HOST, n));
             printf(", \"tx_host_us_c%u\": %.2f", g_chunks, time_us(TX_HOST, n));

@@ -33,7 +33,7 @@ thread_local netcsum::TuneKnob g_tune_chunks{0};
 thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read probe by default
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
-thread_local netcsum::TuneKnob g_tune_burst_zc{1};              // host bursts read pinned rings in place
+thread_local netcsum::TuneKnob g_tune_burst_zc{2};              // host bursts read pinned rings in place, results polled
 thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
@@ -1233,10 +1233,14 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
 // Cfg/Template/net_dev_cfg.c:147), so its cost is fixed, not bandwidth: an H2D copy, a launch, a D2H
 // copy and a stream synchronisation took 19.3 us for one frame (profiles/r3x_burst_latency.jsonl).
 // When the caller's ring is pinned (device-accessible host memory) the kernel reads it in place over
-// PCIe; its flags and actions go to device memory, and a one-wave completion kernel copies them into
-// coherent pinned memory and then stores a tagged completion word there (system-scope release, after
-// the wave's own stores); the host polls that word, as the drop-in's single-block sums do, instead of
-// synchronising the stream, and copies the results out. A pageable ring takes the copy path.
+// PCIe. By default (TUNE_BURST_ZERO_COPY 2) its flags and actions (Tx: 8-B field records) go straight
+// into coherent pinned memory that the host set to a sentinel no result can take (0xFF), and the host
+// polls them until every one has arrived — each is written once, so no completion protocol is needed —
+// instead of synchronising the stream. TUNE_BURST_ZERO_COPY 1: the results go to device memory and a
+// one-wave completion kernel copies them into coherent memory, then stores a tagged completion word
+// (system-scope release after the wave's own stores) that the host polls. tools/burst_latency.c zc,
+// profiles/r4f_burst_zc.jsonl: 64 frames 16.3 us (1) against 14.1 us (2); 1 frame 14.1 / 12.4 us. A
+// pageable ring takes the copy path.
 constexpr uint32_t kBurstZC = 4096u;                    // frames
 // Over PCIe a burst is latency-bound: the whole-slot stream (bound 0) issues the pieces with the
 // parse's loads (one round trip) where the live-piece forms parse first (two); it applies to
