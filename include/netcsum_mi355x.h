@@ -659,8 +659,9 @@ typedef enum netcsum_tune_key {
                                          parse first; 2 = live pieces with the run's first piece loaded
                                          during the parse; 3 = live pieces with the run's first 4 (8)
                                          pieces loaded during the parse (dense strided layouts);
-                                         -1 = the default: 3 for dense strided, 2 for sparse strided and
-                                         offset/length batches                                       */
+                                         -1 = the default: 0 for packed batches (stride == pkt_len), 3 for
+                                         other dense strided ones, 2 for sparse strided and offset/length
+                                         batches                                                     */
     NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
                                          2 (default) the results go straight to coherent pinned memory and
