@@ -269,3 +269,46 @@ def test_offset_length_runs_every_order_vs_oracle(order, spw, bound):
         torch.cuda.synchronize()
         _check(bt.cpu().numpy(), tx_w, f"tx bytes ({passes} passes)")
         _check(ft.cpu().numpy(), txf_w, f"tx flags ({passes} passes)")
+
+
+@pytest.mark.parametrize("form", ["strided", "offlen"])
+@pytest.mark.parametrize("bound", [-1, 1, 2])
+def test_datagrams_past_the_bitmap_reach(form, bound):
+    """Datagrams of 65 000-65 535 B (a run of one spans more than the live-piece bitmap's 64 KiB):
+    strided batches take the whole-span form (or the lane-group kernel when a live-piece form is
+    forced), offset/length runs the whole-span form for those datagrams; every result the oracle's."""
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
+    rng = random.Random(4242 + bound)
+    n, slot = 24, 65536 + 128
+    pkts = []
+    for i in range(n):
+        p = make_packet(rng, rng.choice(["tcp", "udp", "icmp", "corrupt_l4"]), payload=rng.randint(64000, 65400))
+        pkts.append(p[: 65535])
+    buf = np.frombuffer(rng.randbytes(n * slot + 64), np.uint8).copy()
+    lead = 5
+    for i, p in enumerate(pkts):
+        buf[i * slot + lead:i * slot + lead + len(p)] = np.frombuffer(p, np.uint8)
+    lens = np.array([len(p) for p in pkts], np.uint16)
+    present = 65535
+    if form == "strided":
+        want = _want(buf, n, slot, lead, present, True)
+    else:
+        want = _want(buf, n, slot, lead, None, True, lens=lens)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    if form == "strided":
+        netcsum.rx_validate_ipv4(b[lead:], n, f, stride=slot, pkt_len=present)
+        torch.cuda.synchronize()
+        _check(f.cpu().numpy(), want[0], "rx")
+        netcsum.tx_finalize_ipv4(b[lead:], n, ft, stride=slot, pkt_len=present)
+    else:
+        off = torch.from_numpy(np.arange(n, dtype=np.int64) * slot + lead).to(DEV)
+        ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
+        netcsum.rx_validate_ipv4(b, n, f, off=off, lens=ln)
+        torch.cuda.synchronize()
+        _check(f.cpu().numpy(), want[0], "rx")
+        netcsum.tx_finalize_ipv4(b, n, ft, off=off, lens=ln)
+    torch.cuda.synchronize()
+    _check(b.cpu().numpy(), want[1], "tx bytes")
+    _check(ft.cpu().numpy(), want[2], "tx flags")

@@ -968,7 +968,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // with their first pieces loaded during the parse (3), sparse strided and offset/length layouts
     // with piece 0 (2); a burst read in place from
     // host memory may prefer the whole-span form 0 (bound_pref: one PCIe round trip). Live-piece runs
-    // span at most 128 KiB.
+    // span at most 64 KiB.
     const int d = g_tune_chunks.load() == 8 ? 8 : 4;
     // (a packed batch, stride == pkt_len, says every byte is datagram: nothing to skip, form 0;
     // r4f ring probe: 1 M x 1500 B Rx 0.2145 ms against 0.2188 in form 3)
@@ -979,6 +979,9 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         if (netcsum::pkt_stream_supported(a, ip_ver, bound_pref)) bound = bound_pref;
     }
     if (d == 8 && bound == 1) bound = 2;                    // (8 pieces in flight: forms 0, 2, 3)
+    if (!netcsum::pkt_stream_supported(a, ip_ver, bound) && bound >= 1 && dense && g_tune_pkt_bound.load() < 0) {
+        bound = 0;                                          // datagrams > 65408 B: past the bitmap's reach
+    }
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver, bound)) {
         // offset/length runs: 16 datagrams (their lengths are on the device; the device checks each
         // run's order and reach, and takes a run datagram by datagram otherwise)
@@ -1004,7 +1007,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
         if (bound >= 1 && d_off == nullptr) {
-            const uint64_t cap = (128u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+            const uint64_t cap = (64u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
         }
         char desc[144];

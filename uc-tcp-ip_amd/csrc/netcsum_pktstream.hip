@@ -380,10 +380,11 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 //   3  live pieces, with the run's first D pieces loaded whole while the parse runs (dense strided
 //      layouts: at most D KiB per run read past the summed bytes; the rest as 1).
 // Live pieces. After the parse each lane marks its datagram's summed bytes [a, a + end) as 64-B
-// sectors (the HBM access unit) in a per-wave bitmap in LDS (2048 bits: a run spans <= 128 KiB), by
-// ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfwords l and
-// l + 64, and a ballot of their non-zero values gives the run's live pieces as two uniform 64-bit
-// masks. The stream then pops live pieces in address order (scalar find-first-set), skipping dead
+// sectors (the HBM access unit) in a per-wave bitmap in LDS (1024 bits: a run spans <= 64 KiB), by
+// ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfword l, and a
+// ballot of their non-zero values gives the run's live pieces as one uniform 64-bit mask (one
+// SALU find-first-set and clear per piece: the kernels are scalar-issue bound on sparse layouts,
+// profiles/r4h_instmix.txt). The stream then pops live pieces in address order, skipping dead
 // ones entirely (no load, no consume), and lane l of piece q loads its 16 B only if sector l / 4 of
 // the piece's mask (one readlane) is set. The stream's sums only take differences of prefixes inside
 // [start, end) ranges, so zero-filled (unloaded) bytes outside them change nothing. The consume walk
@@ -435,13 +436,15 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     // the prologue's peak to 73 = 6 waves/SIMD).
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
     const uint32_t end_v = mine ? pk.end : 0u;
-    uint64_t lm0 = 0u, lm1 = 0u;                               // live pieces 0-63 / 64-127
-    uint32_t pm0 = 0u, pm1 = 0u;                               // sector masks of pieces l, l + 64
+    uint64_t lm0 = 0u;                                         // live pieces of the run (<= 64)
+    uint32_t pm0 = 0u;                                         // sector mask of piece `lane`
     uint32_t nlive = npieces;
     if constexpr (BND >= 1) {
-        __shared__ uint32_t sect_all[4][64];
+        __shared__ uint32_t sect_all[4][32];
         uint32_t* sect = sect_all[w];
-        sect[lane] = 0u;
+        if (lane < 32u) {
+            sect[lane] = 0u;
+        }
         __builtin_amdgcn_wave_barrier();
         if (end_v != 0u) {
             const uint32_t s0 = prel >> 6, s1 = (prel + end_v - 1u) >> 6;
@@ -451,35 +454,25 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             }
         }
         __builtin_amdgcn_wave_barrier();
-        const uint16_t* s16 = reinterpret_cast<const uint16_t*>(sect);
-        pm0 = s16[lane];
-        pm1 = s16[lane + 64u];
+        pm0 = reinterpret_cast<const uint16_t*>(sect)[lane];
         lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
-        lm1 = __builtin_amdgcn_ballot_w64(pm1 != 0u);
-        nlive = (uint32_t)__builtin_popcountll(lm0) + (uint32_t)__builtin_popcountll(lm1);
+        nlive = (uint32_t)__builtin_popcountll(lm0);
     }
-    const uint32_t lsect = lane >> 2;                          // the lane's 64-B sector in a piece
-    auto pop = [&]() -> uint32_t {                             // next live piece (uniform)
-        // selects only (a branch choosing which mask to clear made the compiler address the two
-        // masks through a pointer, i.e. scratch memory)
-        const bool z0 = lm0 == 0u;
-        const uint32_t q = !z0 ? (uint32_t)__builtin_ctzll(lm0) : (lm1 != 0u ? 64u + (uint32_t)__builtin_ctzll(lm1) : kNoPiece);
-        const uint64_t n1 = lm1 & (lm1 - 1u);
-        lm1 = z0 ? n1 : lm1;
+    const uint32_t lbit = 1u << (lane >> 2);                   // the lane's 64-B sector in a piece
+    auto pop = [&]() -> uint32_t {                             // next live piece (uniform; none: kNoPiece)
+        const uint32_t q = lm0 != 0u ? (uint32_t)__builtin_ctzll(lm0) : kNoPiece;       // s_ff1 + select
         lm0 &= lm0 - 1u;
         return q;
     };
     auto live_voff = [&](uint32_t q) -> uint32_t {             // lane's offset in piece q, or OOB
-        const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)(q & 63u));
-        const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)pm1, (int)(q & 63u));
-        const uint32_t sm = q < 64u ? r0 : (q < 128u ? r1 : 0u);
-        return ((sm >> lsect) & 1u) ? (q << 10) + lane16 : kOOB;
+        const uint32_t sm = q < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q) : 0u;
+        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
     };
     uint32_t qd[D];                                            // the piece in flight in slot j
     if constexpr (BND >= 1) {
         // pieces 0 .. kSpec - 1 are in flight already: consumed first, whether live or not
         constexpr uint64_t spec = kSpec ? (1ull << kSpec) - 1u : 0u;
-        nlive = (uint32_t)__builtin_popcountll(lm0 | spec) + (uint32_t)__builtin_popcountll(lm1);
+        nlive = (uint32_t)__builtin_popcountll(lm0 | spec);
         lm0 &= ~spec;
 #pragma unroll
         for (int j = 0; j < kSpec; ++j) {
@@ -642,12 +635,13 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 }
 
 // Offset/length runs (VL) are streamed when their datagrams lie in increasing address order, each
-// slot's present bytes ending before the next one starts, within 128 KiB from the run's first
+// slot's present bytes ending before the next one starts, within 64 KiB from the run's first
 // 128-B line (the live-piece bitmap's reach); any other run is done one datagram at a time, each as
 // a run of its own (correct for any order or overlap, at one prologue per datagram).
 template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
-    static_assert(!VL || BND == 1 || BND == 2, "offset/length runs take the live-piece forms 1 / 2");
+    // (offset/length runs: the live-piece forms 1 / 2, and 0 for a datagram past the bitmap's reach)
+    static_assert(!VL || BND == 1 || BND == 2, "offset/length runs take the live-piece forms");
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -675,7 +669,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         const uint64_t end = rel + len;
         // ordered: lane k starts at or after lane k - 1's present bytes end (DPP shift by one lane)
         const uint32_t prev_end_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
-        const bool ok = !mine || (rel < (128u << 10) && end <= (128u << 10) - 128u &&
+        const bool ok = !mine || (rel < (64u << 10) && end <= (64u << 10) - 128u &&
                                   (lane == 0u || (uint64_t)prev_end_lo <= rel));
         if (__builtin_amdgcn_ballot_w64(!ok) == 0u) {
             const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u));
@@ -688,7 +682,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                 const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)k);
                 const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
                 const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
-                pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                if (pk + lk <= (64u << 10)) {
+                    pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                } else {                                         // past the bitmap's reach: the whole span
+                    pkt_run<D, NT, TX, REC, VER, 0, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                }
             }
         }
     }
@@ -868,6 +866,7 @@ void set_tx_flush(int mode) {
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
     if (a.off != nullptr) return (bound == 1 || bound == 2) && a.len != nullptr;
+    if (bound >= 1 && a.len_u + 128u > 64u * 1024u) return false;       // a run of one spans <= 64 KiB
     return a.len_u >= 64u && a.stride >= a.len_u && ((bound == 1 || bound == 2) || a.stride <= a.len_u + 64u) &&
            (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
@@ -877,9 +876,9 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
     if (spw == 0u || spw > kMaxRunPkts || bound < 0 || bound > 3 || !pkt_stream_supported(a, ip_ver, bound)) {
         return hipErrorInvalidValue;
     }
-    // live pieces: a strided run spans at most 128 pieces (the host sizes runs for it; offset/length
+    // live pieces: a strided run spans at most 64 pieces (the host sizes runs for it; offset/length
     // runs check their span on the device)
-    if (bound >= 1 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 128u * 1024u) {
+    if (bound >= 1 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 64u * 1024u) {
         return hipErrorInvalidValue;
     }
     const bool vl = a.off != nullptr;
