@@ -1008,7 +1008,11 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
         if (bound >= 1 && d_off == nullptr) {
             const uint64_t cap = (64u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
-            spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
+            if (spw > cap && tile > 0 && g_tune_pkt_bound.load() < 0 && dense) {
+                bound = 0;                                // a run length asked for: the whole-span form
+            } else {
+                spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
+            }
         }
         char desc[144];
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s", d,
