@@ -13,7 +13,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for sub in ("uc-tcp-ip_amd", "oracle", ""):
+for sub in ("uc-tcp-ip_amd", "oracle", "", "tools"):
     sys.path.insert(0, os.path.join(REPO, sub))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -82,6 +82,26 @@ def packet_cpu_lines(threads):
                                                       ns * L, seconds=2.0 if t > 1 else 1.0)
         res[f"{tag}_all_valid"] = ok
     del buf, v
+    # the NIC ring of tools/ring_layouts.py: 40 / 576 / 1500-B datagrams (7:4:1) in 1520-B slots, the
+    # IPv4 header at +14, 1506 B present per slot; frames per second and GiB/s of datagram bytes
+    import ring_layouts as rl
+    nr, slot, lead = 1 << 18, 1520, 14
+    rbuf = oracle.fill_parallel(0, nr * slot, SEED, 0, n_threads=threads, unit=slot)
+    sizes = rl.ring_sizes(nr)
+    rbuf.reshape(nr, slot)[:, lead:lead + 40] = rl.headers(sizes)
+    rb = rbuf[lead:]
+    oracle.pkt_batch(rb, slot, slot - lead, nr, True, n_threads=threads)      # valid checksums
+    ok = bool((oracle.pkt_batch(rb, slot, slot - lead, nr, False, n_threads=threads) & 7 == 7).all())
+    dgram = int(sizes.sum())
+    for t in (threads, 1):
+        sfx = "" if t > 1 else "_1thread"
+        g = cpu_rate(lambda: oracle.pkt_batch(rb, slot, slot - lead, nr, False, n_threads=t), dgram,
+                     seconds=2.0 if t > 1 else 1.0)
+        res["ring_rx_GiB_per_s" + sfx] = g
+        res["ring_rx_Mframes_per_s" + sfx] = round(g * 2 ** 30 / (dgram / nr) / 1e6, 1)
+    res["ring_all_valid"] = ok
+    res["ring_sample"] = f"{nr} frames of the 40/576/1500-B ring in 1520-B slots ({dgram / 1e6:.0f} MB of datagrams)"
+    del rbuf, rb
     nc, per, B = 1 << 11, 45, 2048
     plen = np.full(per, 1480, np.uint16)
     plen[-1] = 65515 - 1480 * (per - 1) - 8
