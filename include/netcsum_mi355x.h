@@ -662,12 +662,18 @@ typedef enum netcsum_tune_key {
                                          -1 = the default: 0 for packed batches (stride == pkt_len), 3 for
                                          other dense strided ones, 2 for sparse strided and offset/length
                                          batches                                                     */
-    NETCSUM_TUNE_BURST_ZERO_COPY = 22 /* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
+    NETCSUM_TUNE_BURST_ZERO_COPY = 22,/* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
-                                         2 (default) the results go straight to coherent pinned memory and
-                                         the host polls them, 1 = a completion kernel copies the results
-                                         out and stores a completion word the host polls; 0 = the copy
-                                         pipeline (H2D, kernel, D2H, stream synchronisation)           */
+                                         3 = a resident server kernel (one per calling thread, on a stream
+                                         of its own) takes each burst from a 64-B post in coherent host
+                                         memory, no launch per burst; 2 (default) a launch per burst, the
+                                         results go straight to coherent pinned memory and the host polls
+                                         them; 1 = a completion kernel copies the results out and stores
+                                         a completion word the host polls; 0 = the copy pipeline (H2D,
+                                         kernel, D2H, stream synchronisation)                           */
+    NETCSUM_TUNE_BURST_SERVER_IDLE_US = 23 /* mode 3: microseconds without a burst after which the server
+                                         stops (the next burst relaunches it); a device-wide
+                                         synchronisation waits up to this long. 1..1000000, default 500 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

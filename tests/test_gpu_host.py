@@ -184,23 +184,25 @@ def test_tx_host_records_every_kernel_form(kernel, passes, chunks):
 
 
 @pytest.mark.parametrize("n", [1, 2, 17, 64, 256, 4096, 4097])
-@pytest.mark.parametrize("form", ["strided", "offlen"])
+@pytest.mark.parametrize("form", ["strided", "offlen", "sparse"])
 def test_rx_burst_host_zero_copy(n, form):
     """NIC-burst sizes with n_chunks 0 from a pinned ring: the kernel reads the ring in place and the
     host polls a completion word (rx_burst_zero_copy, up to 4096 frames; 4097 takes the copy path) or
-    the results themselves (TUNE_BURST_ZERO_COPY 2);
-    the same results as the copy pipeline (TUNE_BURST_ZERO_COPY 0), a pageable ring (copy path) and
-    the oracle, for RxBurstHost and RxValidateIPHost; the ring is never written."""
-    rng = random.Random(900 + n + (form == "offlen"))
-    stride = 1520
-    pkts = [p[:stride - 14] for p in _mixed(rng, n, 1400)]
+    the results themselves (TUNE_BURST_ZERO_COPY 2), or the resident burst server takes the burst
+    from a posted line (3); the same results as the copy pipeline (TUNE_BURST_ZERO_COPY 0), a pageable
+    ring (copy path) and the oracle, for RxBurstHost and RxValidateIPHost; the ring is never written.
+    Forms: 1520-B slots at +14 (strided: the whole-span stream; offlen: per-frame descriptors) and
+    2048-B slots at +64 with 1984 B present (sparse: the live-piece stream)."""
+    rng = random.Random(900 + n + (form == "offlen") + 2 * (form == "sparse"))
+    stride, lead = (2048, 64) if form == "sparse" else (1520, 14)
+    pkts = [p[:stride - lead] for p in _mixed(rng, n, 1400)]
     buf = np.frombuffer(rng.randbytes(n * stride + 64), np.uint8).copy()
     for i, p in enumerate(pkts):
-        buf[i * stride + 14:i * stride + 14 + len(p)] = np.frombuffer(p, np.uint8)
-    if form == "strided":
-        frames = [bytes(buf[i * stride + 14:(i + 1) * stride]) for i in range(n)]
-        kw = {"stride": stride, "pkt_len": stride - 14}
-        base = lambda b: b[14:]                                     # noqa: E731
+        buf[i * stride + lead:i * stride + lead + len(p)] = np.frombuffer(p, np.uint8)
+    if form != "offlen":
+        frames = [bytes(buf[i * stride + lead:(i + 1) * stride]) for i in range(n)]
+        kw = {"stride": stride, "pkt_len": stride - lead}
+        base = lambda b: b[lead:]                                   # noqa: E731
     else:
         offs = np.arange(n, dtype=np.uint64) * stride + 14
         lens = np.array([max(len(p), 46) for p in pkts], np.uint16)
@@ -210,7 +212,7 @@ def test_rx_burst_host_zero_copy(n, form):
     want_f = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
     want_a = np.array([netcsum.rx_action(int(x), oo.transport_proto(f), len(f) and f[0] >> 4 == 6)
                        for x, f in zip(want_f, frames)], np.uint8)
-    for zc, ring in ((1, _pinned(buf)), (2, _pinned(buf)), (0, _pinned(buf)), (1, buf.copy())):
+    for zc, ring in ((1, _pinned(buf)), (2, _pinned(buf)), (3, _pinned(buf)), (0, _pinned(buf)), (3, buf.copy())):
         netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
         try:
             act = np.full(n, 0xEE, np.uint8)
@@ -229,14 +231,16 @@ def test_rx_burst_host_zero_copy(n, form):
         assert np.array_equal(r, buf)
 
 
-def test_rx_burst_host_zero_copy_many_calls_and_threads():
+@pytest.mark.parametrize("zc", [1, 2, 3])
+def test_rx_burst_host_zero_copy_many_calls_and_threads(zc):
     """Back-to-back zero-copy bursts reuse one completion word per thread (tags never repeat a stale
-    value), from two threads at once, each with its own ring."""
+    value), from two threads at once, each with its own ring (and, in mode 3, its own burst server)."""
     import threading
     errs = []
 
     def worker(seed):
         try:
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)              # (per thread)
             rng = random.Random(seed)
             n, stride = 48, 1520
             for it in range(60):
@@ -294,7 +298,7 @@ def test_tx_burst_host_zero_copy(n, form):
     for i in range(n):                                     # the flags the oracle gives the stack's frame
         o = i * stride + lead
         want_f[i] = op.tx_finalize_ip(bytes(buf[o:(i + 1) * stride]), True)[1]
-    for zc in (1, 2, 0):
+    for zc in (1, 2, 3, 0):
         netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
         try:
             hb = _pinned(buf)
@@ -312,3 +316,92 @@ def test_tx_burst_host_zero_copy(n, form):
         assert bad.size == 0, (zc, [(int(j) // stride, int(j) % stride) for j in bad[:8]])
         # flags: the verdict bits of the finalize (UDP placeholder rules aside) on every datagram
         assert ((fl & op.MALFORMED) == (want_f & op.MALFORMED)).all()
+
+
+def test_burst_server_idle_stop_and_relaunch():
+    """The resident burst server (TUNE_BURST_ZERO_COPY 3) with a 20-us idle limit, bursts posted after
+    pauses of 0..300 us: the server stops between many of them and bursts arrive while its blocks are
+    closing (the post / closed-mark handshake, relaunch when a burst went unserved); every burst's
+    results match the oracle; alternating Rx and Tx, strided and offset/length; a device-wide
+    synchronisation returns once the server is idle."""
+    import time
+    rng = random.Random(77)
+    stride, lead, n = 1520, 14, 40
+    pkts = [p[:stride - lead] for p in _mixed(rng, n, 1400)]
+    buf = np.frombuffer(rng.randbytes(n * stride), np.uint8).copy()
+    for i, p in enumerate(pkts):
+        buf[i * stride + lead:i * stride + lead + len(p)] = np.frombuffer(p, np.uint8)
+    hb = _pinned(buf)
+    want = np.array([op.rx_validate_ip(bytes(buf[i * stride + lead:(i + 1) * stride])) for i in range(n)], np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * stride + lead
+    lens = np.full(n, stride - lead, np.uint16)
+    tx_ref = _pinned(buf)                                           # Tx through the copy pipeline
+    netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 0)
+    netcsum.tx_burst_host(tx_ref[lead:], n, None, stride=stride, pkt_len=stride - lead)
+    tx_ref = tx_ref.numpy().copy()
+    tb = _pinned(buf)
+    netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
+    netcsum.tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 20)
+    try:
+        for it in range(400):
+            k = rng.randint(1, n)
+            fl = np.zeros(k, np.uint8)
+            if it % 2:
+                netcsum.rx_validate_ip_host(hb[lead:], k, fl, stride=stride, pkt_len=stride - lead)
+            else:
+                netcsum.rx_validate_ip_host(hb, k, fl, off=offs[:k], lens=lens[:k])
+            assert np.array_equal(fl, want[:k]), it
+            if it % 25 == 7:                                        # Tx of the first k slots of a copy
+                tb.copy_(torch.from_numpy(buf))
+                netcsum.tx_burst_host(tb[lead:], k, None, stride=stride, pkt_len=stride - lead)
+                exp = buf.copy()
+                exp[:k * stride] = tx_ref[:k * stride]
+                assert np.array_equal(tb.numpy(), exp), it
+            pause = rng.choice([0, 0, 5e-6, 2e-5, 5e-5, 3e-4])
+            if pause:
+                t = time.perf_counter() + pause
+                while time.perf_counter() < t:
+                    pass
+        torch.cuda.synchronize()
+    finally:
+        netcsum.tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500)
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
+
+
+@pytest.mark.parametrize("zc", [2, 3])
+def test_zero_copy_ring_rewritten_between_bursts(zc):
+    """The host rewrites its pinned ring in place between bursts (new frames in the same slots, as a
+    NIC does): every burst sees the new bytes — a launch per burst through the launch's cache
+    invalidation, the resident server (3) through its system-scope loads. Two ring contents
+    alternate in one buffer, bursts of 1-8 frames back to back, Rx flags and Tx bytes checked each
+    time against the oracle's for the content just written."""
+    rng = random.Random(31 + zc)
+    stride, lead, n = 1520, 14, 8
+    rings, wants, txs = [], [], []
+    for _ in range(2):
+        pkts = [p[:stride - lead] for p in _mixed(rng, n, 1400)]
+        b = np.frombuffer(rng.randbytes(n * stride), np.uint8).copy()
+        for i, p in enumerate(pkts):
+            b[i * stride + lead:i * stride + lead + len(p)] = np.frombuffer(p, np.uint8)
+        rings.append(b)
+        wants.append(np.array([op.rx_validate_ip(bytes(b[i * stride + lead:(i + 1) * stride])) for i in range(n)], np.uint8))
+        t = _pinned(b)
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 0)
+        netcsum.tx_burst_host(t[lead:], n, None, stride=stride, pkt_len=stride - lead)
+        txs.append(t.numpy().copy())
+    hb = _pinned(rings[0])
+    hv = hb.numpy()
+    netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, zc)
+    try:
+        for it in range(300):
+            j = it & 1
+            k = rng.randint(1, n)
+            hv[:] = rings[j]                                        # the host writes the ring in place
+            fl = np.zeros(k, np.uint8)
+            netcsum.rx_validate_ip_host(hb[lead:], k, fl, stride=stride, pkt_len=stride - lead)
+            assert np.array_equal(fl, wants[j][:k]), (it, j, k)
+            if it % 3 == 0:
+                netcsum.tx_burst_host(hb[lead:], n, None, stride=stride, pkt_len=stride - lead)
+                assert np.array_equal(hv, txs[j]), (it, j)
+    finally:
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)

@@ -326,11 +326,11 @@ def test_pkt_stream_v6_c2_shape_round_trip_1M():
 
 
 @pytest.mark.parametrize("stride,pkt_len,run", [(1500, 1500, 8), (1000, 1000, 16), (577, 577, 32), (256, 200, 64),
-                                                (128, 128, 64), (9000, 9000, 8), (1520, 1506, 16), (2048, 1984, 16)])
+                                                (128, 128, 64), (9000, 9000, 8), (1520, 1506, 16), (2048, 1984, 8)])
 @pytest.mark.parametrize("copies", [1, 1000])
 def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run, copies):
     """Default run: about 20 KB of datagrams per wave for packed batches (the whole-span form 0, r2zq sweep) and
-    32 KB for the live-piece form 3 of other dense layouts (r4e ring probe), in multiples of 8, 8..64, halved while
+    24 KB of slots for the live-piece form 2 of other layouts (r4m ring probe), in multiples of 8, 8..64, halved while
     the batch has fewer than 2048 runs (small bursts are latency-bound); results equal the lane-group kernel's.
     copies: the 300-datagram batch repeated (300 000 datagrams keep the full run)."""
     rng = random.Random(stride)

@@ -11,7 +11,8 @@
  *                      with the results in host memory (_auto: n_chunks 0, the library's choice —
  *                      up to 4096 frames the kernel reads the pinned ring in place and the host
  *                      polls the results; _auto_copy: the same with NETCSUM_TUNE_BURST_ZERO_COPY
- *                      0; from 1024 frames also in 2-16 chunks: _cK)
+ *                      0; _server: 3, the resident burst server; from 1024 frames also in 2-16
+ *                      chunks: _cK)
  * and a check that every Rx action is DELIVER. One JSON line per n on stdout.
  *
  * Built here (the binary travels with the tree; tools/build/ is git-ignored), run on the GPU box:
@@ -167,19 +168,27 @@ static int zc_only(void)
         t[r] = now_us() - t0;
     }
     printf(", \"empty_stream_sync_us\": %.3f", median(t, 2000));
-    /* b = 0: a completion kernel and word (TUNE_BURST_ZERO_COPY 1); 1: results polled (2, the default);
-     * 2: polled, live-piece stream with piece 0 during the parse (TUNE_PKT_BOUND 2) instead of the
-     * whole-span form */
-    for (b = 0; b <= 2; b += 1) {
+    /* b = 0: a completion kernel and word (TUNE_BURST_ZERO_COPY 1); 1: results polled (2); 2: polled,
+     * live-piece stream with piece 0 during the parse (TUNE_PKT_BOUND 2) instead of the whole-span
+     * form; 3: the resident burst server (TUNE_BURST_ZERO_COPY 3) */
+    for (b = 0; b <= 3; b += 1) {
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, b == 2 ? 2 : -1));
-        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b >= 1 ? 2 : 1));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, b == 3 ? 3 : b >= 1 ? 2 : 1));
         for (s = 0; s < 2; ++s) {
+            int ok = 1;
+            uint32_t i;
             for (r = 0; r < 2000; ++r) {
+                memset(g_hact, 0xEE, sizes[s]);
                 t0 = now_us();
                 NET_OK(NetUtil_MI355X_RxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], 0u, g_hact, NULL, 0u));
                 t[r] = now_us() - t0;
+                for (i = 0; i < sizes[s]; ++i) ok &= g_hact[i] == NETCSUM_RX_DELIVER;
             }
             printf(", \"rx_host_zc_v%d_%u_us\": %.2f", b, sizes[s], median(t, 2000));
+            if (!ok) {
+                printf(", \"rx_host_zc_v%d_%u_delivered\": false}\n", b, sizes[s]);
+                return 1;
+            }
             for (r = 0; r < 2000; ++r) {
                 t0 = now_us();
                 NET_OK(NetUtil_MI355X_TxBurstHost(g_hring + IP_AT, NULL, NULL, SLOT, DGRAM, sizes[s], NULL, 0u));
@@ -234,6 +243,13 @@ int main(int argc, char **argv)
         /* n_chunks 0 without the zero-copy burst path (the copy pipeline in one chunk) */
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 0));
         printf(", \"rx_host_us_auto_copy\": %.2f", time_us(RX_HOST, n));
+        /* ... and with the resident burst server (TUNE_BURST_ZERO_COPY 3) */
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 3));
+        if (n <= 4096u) {
+            memset(g_hact, 0xEE, NMAX);
+            printf(", \"rx_host_us_server\": %.2f, \"tx_host_us_server\": %.2f", time_us(RX_HOST, n), time_us(TX_HOST, n));
+            for (i = 0; i < n; ++i) ok &= g_hact[i] == NETCSUM_RX_DELIVER;
+        }
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
         for (g_chunks = 2u; g_chunks <= 16u && n >= 1024u; g_chunks *= 2u) {
             printf(", \"rx_host_us_c%u\": %.2f", g_chunks, time_us(RX_HOST, n));

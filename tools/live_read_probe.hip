@@ -1,0 +1,227 @@
+// Live-sector read probe (not product code): how fast can the run-stream access pattern read only the
+// 64-B sectors that hold datagram bytes of a strided NIC ring, with nothing computed? The floor of
+// the packet run-stream kernel's live-piece forms (DESIGN §9 "NIC-ring layouts").
+//
+// Ring: n slots of `stride` bytes, each holding `len` datagram bytes at +lead. A wave owns a run of R
+// slots and reads it as 1-KiB pieces from the 128-B line below the run (lane l: 16 B at 16 l), D = 4
+// pieces in flight, nt loads — as pkt_stream_kernel does — in one of two forms:
+//   whole  every piece of the run's span (the kernel's bound 0)
+//   live   only pieces holding a live sector, each lane loading its 16 B only if its sector is live
+//          (the kernel's bounds 1-3; the sector bitmap is precomputed here, one bit per 64-B sector
+//          of the ring, 1/512 of the ring's bytes, read once per run)
+// with D = 4 or 8 pieces in flight, and optionally ".touch": before the stream, lane k loads the 16 B
+// at datagram k's start with the plain policy (what the kernel's header parse does, and what the
+// row touch of DESIGN §5.2 does for the segment kernels)
+// and only adds the loaded words up. Median of 20 HIP-event timed launches after a warm-up, per
+// (layout, form, R); one JSON line each: ms, datagram GB/s, fraction of 8 TB/s, sector bytes.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/build/live_read_probe tools/live_read_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                             \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                 \
+        }                                                                                 \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 2);
+}
+
+__device__ __forceinline__ u32x4 opaque(u32x4 v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t add4(u32x4 v, uint32_t a) {
+    return __builtin_amdgcn_sad_u16(v.x, 0u, __builtin_amdgcn_sad_u16(v.y, 0u, __builtin_amdgcn_sad_u16(v.z, 0u, __builtin_amdgcn_sad_u16(v.w, 0u, a))));
+}
+
+__global__ void fill_kernel(u32x4* p, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t x = (uint32_t)i * 2654435761u;
+        p[i] = u32x4{x, x ^ 0x9E3779B9u, x + 7u, ~x};
+    }
+}
+
+// bit s of bits: sector s (bytes [64 s, 64 s + 64) of the ring) holds datagram bytes
+__global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, uint32_t lead, uint32_t len) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w * 32u >= nsect) return;
+    uint32_t m = 0;
+    for (uint32_t b = 0; b < 32u; ++b) {
+        const uint64_t s0 = (w * 32u + b) * 64u, s1 = s0 + 64u;
+        const uint64_t a = s0 / stride;
+        bool live = false;
+        for (uint64_t i = a; i <= (s1 - 1u) / stride; ++i) {
+            const uint64_t d0 = i * stride + lead, d1 = d0 + len;
+            live = live || (s0 < d1 && d0 < s1);
+        }
+        m |= live ? (1u << b) : 0u;
+    }
+    bits[w] = m;
+}
+
+template <bool LIVE, int D, bool TOUCH>
+__global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_t ring_bytes, uint32_t n, uint64_t stride,
+                                                    uint32_t lead, uint32_t len, uint32_t R, const uint32_t* bits,
+                                                    uint32_t* sink) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t s_begin = ((uint64_t)blockIdx.x * 4u + w) * R;
+    if (s_begin >= n) return;
+    const uint32_t nres = (uint32_t)std::min<uint64_t>(R, n - s_begin);
+    const uint64_t a0 = s_begin * stride + lead;                       // the run's first datagram byte
+    const uint64_t O = a0 & ~127ull;
+    const uint32_t span = (uint32_t)(a0 - O) + (uint32_t)((nres - 1u) * stride) + len;
+    const uint32_t npieces = (span + 1023u) >> 10;
+    const __amdgpu_buffer_rsrc_t rd = rsrc(ring + O, (span + 15u) & ~15u);
+    const uint32_t lane16 = 16u * lane;
+    uint64_t lm = 0;                                                     // live pieces (bit 63: sentinel)
+    uint32_t pm = 0;                                                     // sector mask of piece `lane`
+    if constexpr (LIVE) {
+        // piece `lane`: its 16 sectors start at sector O / 64 + 16 lane (O is 128-B aligned)
+        const uint64_t s = O / 64u + 16u * lane;
+        if (lane < npieces) {                                            // (words inside the bitmap)
+            const uint32_t lo = bits[s >> 5], hi = bits[(s >> 5) + 1u];
+            pm = (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31u)) & 0xFFFFu;
+        }
+        lm = __builtin_amdgcn_ballot_w64(pm != 0u) | (1ull << 63);
+    }
+    const uint32_t lbit = 1u << (lane >> 2);
+    auto pop = [&]() -> uint32_t {
+        const uint32_t q = (uint32_t)__builtin_ctzll(lm);
+        lm = (lm & (lm - 1u)) | (1ull << 63);
+        return q;
+    };
+    auto voff = [&](uint32_t q) -> uint32_t {
+        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm, (int)q);
+        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+    };
+    const uint32_t nlive = LIVE ? (uint32_t)__builtin_popcountll(lm) - 1u : npieces;
+    // touch: lane k loads the 16 B at datagram k's start (plain policy), as the kernel's parse does
+    u32x4 tv = {0u, 0u, 0u, 0u};
+    if constexpr (TOUCH) {
+        tv = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(lane < nres ? ((uint32_t)(a0 - O) + lane * (uint32_t)stride) & ~15u : kOOB), 0, 0);
+    }
+    u32x4 dv[D];
+    uint32_t qd[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        qd[j] = LIVE ? pop() : (uint32_t)j;
+        dv[j] = ld16(rd, LIVE ? voff(qd[j]) : ((uint32_t)j << 10) + lane16);
+    }
+    uint32_t acc = 0;
+    const uint32_t rounds = (nlive + D - 1u) / D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            acc = add4(opaque(dv[j]), acc);
+            if constexpr (LIVE) {
+                qd[j] = pop();
+                dv[j] = ld16(rd, voff(qd[j]));
+            } else {
+                dv[j] = ld16(rd, ((r * D + (uint32_t)j + D) << 10) + lane16);
+            }
+            asm volatile("" ::: "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    acc = add4(tv, acc);
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+int main() {
+    struct Layout {
+        const char* name;
+        uint64_t stride;
+        uint32_t lead, len;
+    } layouts[] = {{"packed", 1500, 0, 1500}, {"template", 1520, 14, 1500}, {"nb2k", 2048, 64, 1500}};
+    const uint32_t n = 1u << 20;
+    const uint64_t ring_bytes = (uint64_t)n * 2048u + 4096u;
+    uint8_t* ring = nullptr;
+    uint32_t *bits = nullptr, *sink = nullptr;
+    CK(hipMalloc(&ring, ring_bytes));
+    CK(hipMalloc(&bits, ring_bytes / 64u / 8u + 1024u));
+    CK(hipMemset(bits, 0, ring_bytes / 64u / 8u + 1024u));
+    CK(hipMalloc(&sink, 64));
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, reinterpret_cast<u32x4*>(ring), ring_bytes / 16u);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (const Layout& L : layouts) {
+        const uint64_t bytes = (uint64_t)n * L.stride + 4096u;
+        const uint64_t nsect = bytes / 64u;
+        hipLaunchKernelGGL(sectors_kernel, dim3((unsigned)((nsect / 32u + 256u) / 256u)), dim3(256), 0, 0, bits, nsect,
+                           L.stride, L.lead, L.len);
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> hb(nsect / 32u);
+        CK(hipMemcpy(hb.data(), bits, hb.size() * 4u, hipMemcpyDeviceToHost));
+        uint64_t live = 0;
+        for (uint32_t x : hb) live += (uint64_t)__builtin_popcount(x);
+        // (form, D, touch): whole / live with 4 pieces in flight, live with the datagram-start touch,
+        // live with 8 in flight, with and without the touch
+        struct V {
+            const char* tag;
+            int live, d, touch;
+        } vs[] = {{"whole", 0, 4, 0}, {"live", 1, 4, 0}, {"live.touch", 1, 4, 1}, {"live.d8", 1, 8, 0},
+                  {"live.d8.touch", 1, 8, 1}, {"whole.touch", 0, 4, 1}};
+        for (int pass = 0; pass < 2; ++pass) {
+            for (const V& v : vs) {
+                for (uint32_t R : {8u, 16u}) {
+                    const uint64_t waves = (n + R - 1u) / R;
+                    const dim3 g((unsigned)((waves + 3u) / 4u)), b(256);
+                    auto launch = [&]() {
+#define LRP_L(LV, DD, TT) hipLaunchKernelGGL((probe_kernel<LV, DD, TT>), g, b, 0, 0, ring, bytes, n, L.stride, L.lead, L.len, R, bits, sink)
+                        if (v.live && v.d == 4 && !v.touch) LRP_L(true, 4, false);
+                        else if (v.live && v.d == 4) LRP_L(true, 4, true);
+                        else if (v.live && !v.touch) LRP_L(true, 8, false);
+                        else if (v.live) LRP_L(true, 8, true);
+                        else if (!v.touch) LRP_L(false, 4, false);
+                        else LRP_L(false, 4, true);
+#undef LRP_L
+                    };
+                    for (int i = 0; i < 200; ++i) launch();
+                    std::vector<float> t(20);
+                    for (float& x : t) {
+                        CK(hipEventRecord(e0, 0));
+                        launch();
+                        CK(hipEventRecord(e1, 0));
+                        CK(hipEventSynchronize(e1));
+                        CK(hipEventElapsedTime(&x, e0, e1));
+                    }
+                    CK(hipGetLastError());
+                    std::sort(t.begin(), t.end());
+                    const double ms = t[10], dgram = (double)n * L.len;
+                    std::printf("{\"layout\": \"%s\", \"stride\": %llu, \"lead\": %u, \"len\": %u, \"form\": \"%s\", \"run\": %u, "
+                                "\"pass\": %d, \"ms\": %.4f, \"datagram_GBps\": %.1f, \"frac_of_8TBps\": %.4f, "
+                                "\"sector_bytes\": %llu, \"sector_GBps\": %.1f}\n",
+                                L.name, (unsigned long long)L.stride, L.lead, L.len, v.tag, R, pass, ms,
+                                dgram / ms / 1e6, dgram / ms / 1e6 / 8000.0, (unsigned long long)(live * 64u),
+                                (v.live ? (double)live * 64.0 : (double)n * L.stride) / ms / 1e6);
+                    std::fflush(stdout);
+                }
+            }
+        }
+    }
+    CK(hipFree(ring));
+    CK(hipFree(bits));
+    CK(hipFree(sink));
+    return 0;
+}

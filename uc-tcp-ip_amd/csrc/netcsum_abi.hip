@@ -34,6 +34,7 @@ thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read 
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 thread_local netcsum::TuneKnob g_tune_burst_zc{2};              // host bursts read pinned rings in place, results polled
+thread_local netcsum::TuneKnob g_tune_burst_idle{500};           // resident burst server: idle microseconds before it stops
 thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
@@ -490,9 +491,14 @@ struct HostCtx {
     uint8_t*             d_burst = nullptr;
     uint8_t*             h_burst = nullptr;
     uint8_t*             h_burst_dev = nullptr;
+    // resident burst server (TUNE_BURST_ZERO_COPY 3): its stream, whether it may be serving, the last
+    // burst number posted
+    hipStream_t          sstream = nullptr;
+    bool                 server_live = false;
+    uint64_t             post_seq = 0;
 
     bool empty() const {
-        if (stream || h_stage || d_stage || d_sum || h_sum || d_burst || h_burst) return false;
+        if (stream || h_stage || d_stage || d_sum || h_sum || d_burst || h_burst || sstream) return false;
         for (int j = 0; j < 3; ++j) {
             if (pstream[j] || d_pipe[j] || h_pipe[j]) return false;
         }
@@ -511,6 +517,8 @@ struct HostCtx {
         for (int j = 0; j < 3; ++j) {
             if (pstream[j]) (void)hipStreamSynchronize(pstream[j]);
         }
+        stop_server();
+        if (sstream) (void)hipStreamDestroy(sstream);
         if (stream) (void)hipStreamDestroy(stream);
         if (h_stage) (void)hipHostFree(h_stage);
         if (d_stage) (void)hipFree(d_stage);
@@ -527,6 +535,7 @@ struct HostCtx {
         *this = HostCtx{};
     }
     ~HostCtx() { release(); }
+    void stop_server();
 };
 
 thread_local HostCtx tls_ctx[kMaxDev];
@@ -964,31 +973,34 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     const bool own_flags = walk && d_flags == nullptr;
     hipStream_t hs = static_cast<hipStream_t>(hip_stream);
     // Which bytes of each slot are read (NETCSUM_TUNE_PKT_BOUND, netcsum_pktstream.hip): by default the
-    // whole span for packed batches (0), else the live pieces — dense strided layouts (gaps <= 64 B)
-    // with their first pieces loaded during the parse (3), sparse strided and offset/length layouts
-    // with piece 0 (2); a burst read in place from
-    // host memory may prefer the whole-span form 0 (bound_pref: one PCIe round trip). Live-piece runs
-    // span at most 64 KiB.
+    // whole span for packed batches (0), else the live pieces with piece 0 loaded during the parse (2;
+    // since the one-mask sentinel pop it beats form 3 on every ring layout, profiles/r4m_ring_probe.jsonl:
+    // 1520-B slots at +14, 1500-B datagrams 0.2177 against 0.2197 ms, the mixed ring 0.1532 against
+    // 0.1583, 2-KiB slots at +64 0.2522 against 0.2677); a burst read in place from host memory may
+    // prefer the whole-span form 0 (bound_pref: one PCIe round trip). Live-piece runs span at most
+    // 63 KiB (kLiveReach).
     const int d = g_tune_chunks.load() == 8 ? 8 : 4;
     // (a packed batch, stride == pkt_len, says every byte is datagram: nothing to skip, form 0;
     // r4f ring probe: 1 M x 1500 B Rx 0.2145 ms against 0.2188 in form 3)
     const bool dense = d_off == nullptr && stride <= (uint64_t)pkt_len + 64u;
     const bool packed = d_off == nullptr && stride == (uint64_t)pkt_len;
-    int bound = g_tune_pkt_bound.load() >= 0 ? g_tune_pkt_bound.load() : (packed ? 0 : dense ? 3 : 2);
+    int bound = g_tune_pkt_bound.load() >= 0 ? g_tune_pkt_bound.load() : (packed ? 0 : 2);
     if (bound_pref >= 0 && g_tune_pkt_bound.load() < 0) {   // the caller's preference, where it applies
         if (netcsum::pkt_stream_supported(a, ip_ver, bound_pref)) bound = bound_pref;
     }
     if (d == 8 && bound == 1) bound = 2;                    // (8 pieces in flight: forms 0, 2, 3)
     if (!netcsum::pkt_stream_supported(a, ip_ver, bound) && bound >= 1 && dense && g_tune_pkt_bound.load() < 0) {
-        bound = 0;                                          // datagrams > 65408 B: past the bitmap's reach
+        bound = 0;                                          // datagrams > 64384 B: past the bitmap's reach
     }
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver, bound)) {
         // offset/length runs: 16 datagrams (their lengths are on the device; the device checks each
         // run's order and reach, and takes a run datagram by datagram otherwise)
-        // the live-piece forms parse first, so their runs are longer: about 32 KB of span (r4e ring
-        // probe, profiles/r4e_ring_probe.jsonl: 1520-B slots 8 -> 16 datagrams 0.2575 -> 0.2281 ms)
+        // the live-piece forms parse first, so their runs are longer: about 24 KB of strided span, which
+        // gives 1520-B slots runs of 16 (the mixed 40/576/1500-B ring: 0.1532 ms against 0.1921 for 8)
+        // and 2-KiB slots runs of 8 (0.2522 against 0.2627 for 16; profiles/r4m_ring_probe.jsonl);
+        // offset/length runs 16 (32: 64 KiB of 2-KiB slots, past the reach)
         const uint64_t per = d_off ? 2048u : std::max<uint64_t>(a.stride, 1u);
-        const uint64_t budget = bound == 0 ? 20480u : 32768u;
+        const uint64_t budget = bound == 0 ? 20480u : d_off ? 32768u : 24576u;
         const uint32_t run = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
                                          : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (budget / per) & ~7ull));
         // small batches (NIC bursts) are latency-bound: a run costs ~run x len / 4 KiB memory round
@@ -1007,7 +1019,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
         if (bound >= 1 && d_off == nullptr) {
-            const uint64_t cap = (64u * 1024u - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+            const uint64_t cap = (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             if (spw > cap && tile > 0 && g_tune_pkt_bound.load() < 0 && dense) {
                 bound = 0;                                // a run length asked for: the whole-span form
             } else {
@@ -1259,7 +1271,7 @@ constexpr uint32_t kBurstZC = 4096u;                    // frames
 // profiles/r4d_burst_zc.jsonl: 64 frames 17.4 -> 15.6 us)
 constexpr int kBurstBound = 0;
 constexpr uint64_t kBurstZCSpan = 64ull << 20;          // ring bytes the kernel may read in place
-constexpr size_t kBurstWord = 0, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
+constexpr size_t kBurstWord = 0, kBurstPost = 64, kBurstClosed = 128, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
                  kBurstOff = kBurstAct + kBurstZC, kBurstLen = kBurstOff + 8u * kBurstZC,
                  kBurstRec = kBurstLen + 2u * kBurstZC, kBurstHostBytes = kBurstRec + 8u * kBurstZC;
 // device side: [flags | actions | Tx records]
@@ -1326,6 +1338,141 @@ static NET_ERR burst_poll(HostCtx& c, Ready ready, uint32_t n) {
     }
     return NET_UTIL_ERR_NONE;
 }
+
+// ---- resident burst server (TUNE_BURST_ZERO_COPY 3; netcsum_pktstream.hip burst_server_kernel)
+// A launch per burst is most of a small burst's cost (launch, dispatch, then the kernel's PCIe round
+// trips). This context's server is launched once, on a stream of its own, and serves every burst
+// posted to it until it has been idle for TUNE_BURST_SERVER_IDLE_US (default 500 us: a device-wide
+// synchronisation waits at most that long for it after the last burst). Posting: the line's fields,
+// then its burst number (a read that sees the new number with stale fields fails the check), a
+// full fence, then the blocks' closed marks — a block that closed may have missed the post
+// (Dekker's handshake, see the kernel), so the host waits the server out and relaunches it if the
+// burst is not served. A server that stopped unnoticed is found by a stream query after 200 us
+// without results.
+// 16 blocks x 4 waves: a block's leader polls the post line (16 64-B reads per poll round); 4 blocks
+// of 16 waves were slower from 10 frames up (tools/burst_latency.c, 64 frames 14.8 us against 13.1 us
+// for a launch per burst: 16 waves on one CU queue their PCIe reads)
+constexpr int kServerBlocks = 16;
+static_assert(kServerBlocks <= netcsum::kBurstServerMaxBlocks && kBurstClosed + 8u * kServerBlocks <= kBurstFlags,
+              "closed marks");
+
+static void write_post(HostCtx& c, const netcsum::BurstPost& p) {
+    volatile uint32_t* l = reinterpret_cast<volatile uint32_t*>(c.h_burst + kBurstPost);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&p);
+    for (int i = 2; i < 16; ++i) l[i] = q[i];            // fields, check
+    std::atomic_thread_fence(std::memory_order_release);
+    *reinterpret_cast<volatile uint64_t*>(c.h_burst + kBurstPost) = p.seq;
+    std::atomic_thread_fence(std::memory_order_seq_cst); // the post before the closed marks are read
+}
+
+static NET_ERR launch_server(HostCtx& c, uint64_t seq0) {
+    volatile unsigned long long* closed = reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstClosed);
+    for (int b = 0; b < kServerBlocks; ++b) closed[b] = 0ull;
+    int khz = 0;
+    NC_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c.dev));
+    netcsum::BurstServerArgs a{};
+    a.post = reinterpret_cast<const netcsum::BurstPost*>(c.h_burst_dev + kBurstPost);
+    a.closed = reinterpret_cast<unsigned long long*>(c.h_burst_dev + kBurstClosed);
+    a.flags = c.h_burst_dev + kBurstFlags;
+    a.act = c.h_burst_dev + kBurstAct;
+    a.rec = reinterpret_cast<netcsum::PktTxRecord*>(c.h_burst_dev + kBurstRec);
+    a.off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
+    a.len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
+    a.seq0 = seq0;
+    a.idle_ticks = (uint64_t)std::max(1, g_tune_burst_idle.load()) * (uint64_t)std::max(khz, 1) / 1000u;
+    NC_HIP(netcsum::launch_burst_server(a, kServerBlocks, c.sstream));
+    c.server_live = true;
+    return NET_UTIL_ERR_NONE;
+}
+
+void HostCtx::stop_server() {
+    if (server_live && sstream && h_burst) {
+        netcsum::BurstPost p{};
+        p.seq = netcsum::kBurstStop;
+        p.check = netcsum::burst_post_check(p);
+        write_post(*this, p);
+        (void)hipStreamSynchronize(sstream);
+    }
+    server_live = false;
+}
+
+template <class Ready>
+static NET_ERR burst_server_run(HostCtx& c, netcsum::BurstPost p, Ready ready, uint32_t n) {
+    if (c.sstream == nullptr) NC_HIP(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
+    auto all_ready = [&](uint32_t from) {
+        for (uint32_t i = from; i < n; ++i) {
+            if (!ready(i)) return false;
+        }
+        return true;
+    };
+    auto wait_out = [&](uint32_t from) -> NET_ERR {     // the server has stopped, or is stopping
+        NC_HIP(hipStreamSynchronize(c.sstream));
+        c.server_live = false;
+        return all_ready(from) ? NET_UTIL_ERR_NONE : launch_server(c, p.seq - 1u);
+    };
+    p.seq = ++c.post_seq;
+    p.check = netcsum::burst_post_check(p);
+    write_post(c, p);
+    NET_ERR e = NET_UTIL_ERR_NONE;
+    if (!c.server_live) {
+        e = launch_server(c, p.seq - 1u);
+    } else {
+        const volatile unsigned long long* closed =
+            reinterpret_cast<const volatile unsigned long long*>(c.h_burst + kBurstClosed);
+        bool any = false;
+        for (int b = 0; b < kServerBlocks; ++b) any = any || closed[b] != 0ull;
+        if (any) e = wait_out(0u);
+    }
+    if (e != NET_UTIL_ERR_NONE) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto t_check = t0 + std::chrono::microseconds(200);
+    uint32_t i = 0, spin = 0;
+    while (i < n) {
+        if (ready(i)) {
+            ++i;
+            continue;
+        }
+        if ((++spin & 255u) != 0u) continue;
+        const auto t = std::chrono::steady_clock::now();
+        if (t < t_check) continue;
+        t_check = t + std::chrono::microseconds(200);
+        if (c.server_live && hipStreamQuery(c.sstream) == hipSuccess) {   // stopped without serving it
+            e = wait_out(i);
+            if (e != NET_UTIL_ERR_NONE) return e;
+        } else if (t - t0 > std::chrono::seconds(2)) {
+            c.stop_server();
+            if (!all_ready(i)) return dev_fail("burst server results", hipErrorUnknown);
+        }
+    }
+    return NET_UTIL_ERR_NONE;
+}
+
+// The server's form for a burst (BurstPost::form >> 1 and its run length), or false when the burst is
+// outside the run-stream kernel's domain (the launch path takes it).
+static bool server_form(const uint64_t* h_off, uint64_t stride, CPU_INT16U pkt_len, uint32_t n_pkt, uint32_t* form,
+                        uint32_t* spw) {
+    netcsum::PktBatchArgs a{};
+    a.off = h_off;
+    a.len = reinterpret_cast<const uint16_t*>(h_off);     // (only tested against nullptr)
+    a.stride = stride;
+    a.len_u = pkt_len;
+    a.n = n_pkt;
+    uint32_t run = std::max<uint32_t>(1u, std::min<uint32_t>(16u, (n_pkt + 4u * kServerBlocks - 1u) / (4u * kServerBlocks)));
+    if (h_off != nullptr) {
+        *form = netcsum::kBurstOffLen;
+        if (!netcsum::pkt_stream_supported(a, 0, 2)) return false;
+    } else if (stride <= (uint64_t)pkt_len + 64u && netcsum::pkt_stream_supported(a, 0, 0)) {
+        *form = netcsum::kBurstWhole;                   // (kBurstBound: one PCIe round trip)
+    } else if (netcsum::pkt_stream_supported(a, 0, 2)) {
+        *form = netcsum::kBurstLive;
+        const uint64_t cap = (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+        run = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(run, cap));
+    } else {
+        return false;
+    }
+    *spw = run;
+    return true;
+}
 }  // extern "C++"
 
 // Rx over a pinned ring in place. *taken = false: the burst does not qualify (the caller takes the
@@ -1355,7 +1502,29 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
         d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
         d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
     }
-    if (g_tune_burst_zc.load() == 2) {                  // results straight into coherent memory, polled
+    uint32_t form = 0, spw = 0;
+    const int zc = g_tune_burst_zc.load();
+    if (zc == 3 && server_form(h_off, stride, pkt_len, n_pkt, &form, &spw)) {   // the resident server
+        uint8_t* hf = c.h_burst + kBurstFlags;
+        uint8_t* ha = c.h_burst + kBurstAct;
+        std::memset(hf, 0xFF, n_pkt);
+        std::memset(ha, 0xFF, n_pkt);
+        netcsum::BurstPost p{};
+        p.ring = reinterpret_cast<uint64_t>(d_ring);
+        p.stride = (uint32_t)stride;
+        p.n = n_pkt;
+        p.pkt_len = pkt_len;
+        p.spw = spw;
+        p.form = form << 1;
+        p.rx_cfg = rx_cfg;
+        e = burst_server_run(c, p, [&](uint32_t i) { return *(volatile uint8_t*)(hf + i) != 0xFFu &&
+                                                            *(volatile uint8_t*)(ha + i) != 0xFFu; }, n_pkt);
+        if (e != NET_UTIL_ERR_NONE) return e;
+        if (h_flags) std::memcpy(h_flags, hf, n_pkt);
+        if (h_action) std::memcpy(h_action, ha, n_pkt);
+        return NET_UTIL_ERR_NONE;
+    }
+    if (zc >= 2) {                                      // results straight into coherent memory, polled
         uint8_t* hf = c.h_burst + kBurstFlags;
         uint8_t* ha = c.h_burst + kBurstAct;
         std::memset(hf, 0xFF, n_pkt);                   // sentinels: no flag byte or action is 0xFF
@@ -1431,7 +1600,22 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         d_off = reinterpret_cast<const uint64_t*>(c.h_burst_dev + kBurstOff);
         d_len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
     }
-    if (g_tune_burst_zc.load() == 2) {                  // records straight into coherent memory, polled
+    uint32_t form = 0, spw = 0;
+    const int zc = g_tune_burst_zc.load();
+    if (zc == 3 && server_form(h_off, stride, pkt_len, n_pkt, &form, &spw)) {   // the resident server
+        uint8_t* hr = c.h_burst + kBurstRec;
+        std::memset(hr, 0xFF, (size_t)n_pkt * 8u);
+        netcsum::BurstPost p{};
+        p.ring = reinterpret_cast<uint64_t>(d_ring);
+        p.stride = (uint32_t)stride;
+        p.n = n_pkt;
+        p.pkt_len = pkt_len;
+        p.spw = spw;
+        p.form = (form << 1) | 1u;
+        p.udp_mode = udp_mode;
+        e = burst_server_run(c, p, [&](uint32_t i) { return *(volatile uint8_t*)(hr + 8u * i + 7u) != 0xFFu; }, n_pkt);
+        if (e != NET_UTIL_ERR_NONE) return e;
+    } else if (zc >= 2) {                               // records straight into coherent memory, polled
         uint8_t* hr = c.h_burst + kBurstRec;
         std::memset(hr, 0xFF, (size_t)n_pkt * 8u);     // sentinel: a record's store byte is 0..3
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
@@ -1757,8 +1941,12 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         netcsum::set_crc_nt(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BURST_ZERO_COPY:
-        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_burst_zc.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_BURST_SERVER_IDLE_US:
+        if (value < 1 || value > 1000000) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_burst_idle.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
         if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

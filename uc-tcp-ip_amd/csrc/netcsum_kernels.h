@@ -164,8 +164,8 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound);   // ru
 // stores at system scope, 2 release at the end of every scatter wave, 3 / 4 a write-back launch of
 // 8 / 256 workgroups after the Tx launch(es).
 void set_tx_flush(int mode);
-// bound (NETCSUM_TUNE_PKT_BOUND): 0 slots streamed whole, 1 refills bounded by the parsed ends, 2 parse
-// first and every piece bounded (depth 8 only with bound 2)
+// bound (NETCSUM_TUNE_PKT_BOUND): 0 every piece of the run's span, 1 / 2 / 3 the live pieces, with 0 / 1
+// / depth pieces loaded during the parse (netcsum_pktstream.hip; depth 8: bounds 0, 2 and 3)
 // rec: two-pass Tx (records + scatter); scatter = false: the records only (zero-copy host bursts, whose
 // host applies them)
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
@@ -174,6 +174,51 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
 // device memory into coherent pinned host memory, then stores `tag` into *word (system scope).
 hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, uint8_t* h_fl, uint8_t* h_act,
                              unsigned long long* word, uint32_t tag, hipStream_t s);
+
+// Resident burst server (NETCSUM_TUNE_BURST_ZERO_COPY 3; netcsum_pktstream.hip burst_server_kernel):
+// the host posts a zero-copy burst as ONE 64-B line of coherent host memory, which the server's
+// leader waves poll, instead of launching a kernel per burst.
+// Live-piece runs (run-stream packet kernels, bounds 1-3) span at most 63 KiB from their first 128-B
+// line: piece 63 is never live, and its bit is the pop's sentinel.
+constexpr uint32_t kLiveReach = 63u << 10;
+
+struct alignas(64) BurstPost {
+    uint64_t seq;          // burst number, increasing; kBurstStop: exit
+    uint64_t ring;         // device address of the ring (its pinned alias)
+    uint32_t stride;       // strided forms
+    uint32_t n;            // frames (<= 4096)
+    uint32_t pkt_len;      // strided forms: bytes present per slot
+    uint32_t spw;          // frames per wave run
+    uint32_t form;         // bit 0 Tx; form >> 1: kBurstWhole / kBurstLive / kBurstOffLen
+    uint32_t udp_mode;     // Tx: PktBatchArgs::udp_tx_csum
+    uint32_t rx_cfg;       // Rx: NETCSUM_RXCFG_* for the actions
+    uint32_t check;        // burst_post_check of the fields above: a read that tore the line fails it
+    uint32_t pad[4];
+};
+static_assert(sizeof(BurstPost) == 64, "one line");
+constexpr uint64_t kBurstStop = ~0ull;
+constexpr uint32_t kBurstWhole = 0u, kBurstLive = 1u, kBurstOffLen = 2u;
+constexpr int kBurstServerMaxBlocks = 16;
+__host__ __device__ __forceinline__ uint32_t burst_post_check(const BurstPost& p) {
+    const uint32_t d[11] = {(uint32_t)p.seq, (uint32_t)(p.seq >> 32), (uint32_t)p.ring, (uint32_t)(p.ring >> 32),
+                            p.stride, p.n, p.pkt_len, p.spw, p.form, p.udp_mode, p.rx_cfg};
+    uint32_t h = 0x811C9DC5u;                               // FNV-1a over the dwords
+    for (int i = 0; i < 11; ++i) h = (h ^ d[i]) * 0x01000193u;
+    return h;
+}
+struct BurstServerArgs {
+    const BurstPost*    post;      // device alias of the post line
+    unsigned long long* closed;    // [blocks]: set by a block that stops serving (device-written)
+    uint8_t*            flags;     // Rx results (device aliases of coherent host memory)
+    uint8_t*            act;
+    PktTxRecord*        rec;       // Tx records
+    const uint64_t*     off;       // offset/length descriptors (staged in coherent host memory)
+    const uint16_t*     len;
+    uint64_t            seq0;      // the last burst number already served
+    uint64_t            idle_ticks;   // wall-clock ticks without a post after which a block stops
+};
+// blocks x 256 threads on stream s (a stream of its own: the kernel runs until it is idle)
+hipError_t launch_burst_server(const BurstServerArgs& a, int blocks, hipStream_t s);
 // IPv6 extension-header chains past the batch kernels' window (flags EXT_HDR): walked to the end and
 // finished in place (netcsum_v6walk.hip); a.flags_out holds the batch kernel's flags.
 hipError_t launch_pkt_v6_walk(const PktBatchArgs& a, bool tx, int cus, hipStream_t s);

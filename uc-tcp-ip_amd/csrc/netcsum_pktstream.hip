@@ -380,7 +380,7 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 //   3  live pieces, with the run's first D pieces loaded whole while the parse runs (dense strided
 //      layouts: at most D KiB per run read past the summed bytes; the rest as 1).
 // Live pieces. After the parse each lane marks its datagram's summed bytes [a, a + end) as 64-B
-// sectors (the HBM access unit) in a per-wave bitmap in LDS (1024 bits: a run spans <= 64 KiB), by
+// sectors (the HBM access unit) in a per-wave bitmap in LDS (1024 bits: a run spans <= 63 KiB), by
 // ds_or of whole-dword ranges. Piece q's 16 sectors are halfword q; lane l holds halfword l, and a
 // ballot of their non-zero values gives the run's live pieces as one uniform 64-bit mask (one
 // SALU find-first-set and clear per piece: the kernels are scalar-issue bound on sparse layouts,
@@ -390,11 +390,47 @@ __device__ __forceinline__ LanePkt lane_parse_ver(const uint32_t (&wd)[24], cons
 // [start, end) ranges, so zero-filled (unloaded) bytes outside them change nothing. The consume walk
 // clamps offsets below the piece to 0: a datagram with nothing to sum (malformed: end 0) may start in
 // a skipped piece, and its event then falls in a later one with an empty range.
-constexpr uint32_t kNoPiece = 0x3FFFFu;                 // past every run (qb < 2^28)
+// The pop: s_ff1 of the run's live-piece mask, which always holds bit 63 (piece 63 is never live:
+// kLiveReach), so the empty mask needs no test: the sentinel piece 63 has no live sector (nothing
+// loaded) and lies past every datagram end (its consume takes any pending events). Piece offsets x
+// inside a consume take their two partial-lane byte masks from a table (one scalar load instead of
+// ~12 SALU building them).
+constexpr uint64_t kSentinel = 1ull << 63;
+constexpr uint32_t kDone = ~0u;                         // end of "the next packet" once the run is done
+struct PrefixMasks {
+    uint64_t m0, m1;
+};
+constexpr uint64_t prefix_lo(uint32_t k) { return k >= 8u ? ~0ull : (1ull << (8u * k)) - 1ull; }
+constexpr uint64_t prefix_hi(uint32_t k) { return k <= 8u ? 0ull : (1ull << (8u * (k - 8u))) - 1ull; }
+__constant__ PrefixMasks kPrefixMask[16] = {
+    {prefix_lo(0), prefix_hi(0)},   {prefix_lo(1), prefix_hi(1)},   {prefix_lo(2), prefix_hi(2)},
+    {prefix_lo(3), prefix_hi(3)},   {prefix_lo(4), prefix_hi(4)},   {prefix_lo(5), prefix_hi(5)},
+    {prefix_lo(6), prefix_hi(6)},   {prefix_lo(7), prefix_hi(7)},   {prefix_lo(8), prefix_hi(8)},
+    {prefix_lo(9), prefix_hi(9)},   {prefix_lo(10), prefix_hi(10)}, {prefix_lo(11), prefix_hi(11)},
+    {prefix_lo(12), prefix_hi(12)}, {prefix_lo(13), prefix_hi(13)}, {prefix_lo(14), prefix_hi(14)},
+    {prefix_lo(15), prefix_hi(15)}};
+
+// piece_prefix (netcsum_stream.h) with the table's masks.
+__device__ __forceinline__ uint32_t piece_prefix_t(u32x4 v, uint32_t s4, uint32_t lane16, uint32_t x) {
+    const PrefixMasks m = kPrefixMask[x & 15u];
+    uint32_t pv = __builtin_amdgcn_sad_u16(v.x & (uint32_t)m.m0, 0u, 0u);
+    pv = __builtin_amdgcn_sad_u16(v.y & (uint32_t)(m.m0 >> 32), 0u, pv);
+    pv = __builtin_amdgcn_sad_u16(v.z & (uint32_t)m.m1, 0u, pv);
+    pv = __builtin_amdgcn_sad_u16(v.w & (uint32_t)(m.m1 >> 32), 0u, pv);
+    return (lane16 + 16u <= x) ? s4 : ((lane16 < x) ? pv : 0u);
+}
+// SYS (the resident burst server): the run's loads at system scope (sc0 sc1), so that no line of
+// the host ring an L2 holds from an earlier burst is used (the host rewrites its ring between
+// bursts; a kernel launch per burst gets that from the launch's cache invalidation).
+template <bool NT, bool SYS>
+__device__ __forceinline__ u32x4 ring_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, (NT ? 2 : 0) | (SYS ? 17 : 0));
+}
+
 // One wave run: packets s_begin .. s_begin + nres - 1, lane k's packet at run-relative offset prel
 // (from O, 128-B aligned) with `avail` bytes present; the run's bytes [O, O + span). VL: per-packet
 // starts (offset/length descriptors) instead of a stride.
-template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL, bool SYS = false>
 __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec, uint32_t w, uint32_t lane,
                                         uint32_t s_begin, uint32_t nres, uintptr_t O, uint32_t prel, uint32_t avail,
                                         uint32_t span) {
@@ -409,7 +445,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     constexpr int kSpec = BND == 0 || BND == 3 ? D : BND == 2 ? 1 : 0;   // pieces loaded before the parse
 #pragma unroll
     for (int j = 0; j < kSpec; ++j) {                          // the first pieces in flight ...
-        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
+        dv[j] = ring_load16<NT, SYS>(rd, ((uint32_t)j << 10) + lane16);
     }
 
     // ... while lane k parses packet k from its own 96-B window.
@@ -419,7 +455,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     u32x4 h[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-        h[c] = buf_load16<false>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
+        h[c] = ring_load16<false, SYS>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
     }
     uint32_t wd[24];
 #pragma unroll
@@ -440,7 +476,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     uint32_t pm0 = 0u;                                         // sector mask of piece `lane`
     uint32_t nlive = npieces;
     if constexpr (BND >= 1) {
-        __shared__ uint32_t sect_all[4][32];
+        __shared__ uint32_t sect_all[16][32];                   // (blocks of up to 16 waves)
         uint32_t* sect = sect_all[w];
         if (lane < 32u) {
             sect[lane] = 0u;
@@ -459,13 +495,13 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         nlive = (uint32_t)__builtin_popcountll(lm0);
     }
     const uint32_t lbit = 1u << (lane >> 2);                   // the lane's 64-B sector in a piece
-    auto pop = [&]() -> uint32_t {                             // next live piece (uniform; none: kNoPiece)
-        const uint32_t q = lm0 != 0u ? (uint32_t)__builtin_ctzll(lm0) : kNoPiece;       // s_ff1 + select
-        lm0 &= lm0 - 1u;
+    auto pop = [&]() -> uint32_t {                             // next live piece (uniform; none: 63)
+        const uint32_t q = (uint32_t)__builtin_ctzll(lm0);     // (lm0 holds the sentinel)
+        lm0 = (lm0 & (lm0 - 1u)) | kSentinel;
         return q;
     };
     auto live_voff = [&](uint32_t q) -> uint32_t {             // lane's offset in piece q, or OOB
-        const uint32_t sm = q < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q) : 0u;
+        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
         return (sm & lbit) ? (q << 10) + lane16 : kOOB;
     };
     uint32_t qd[D];                                            // the piece in flight in slot j
@@ -473,7 +509,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         // pieces 0 .. kSpec - 1 are in flight already: consumed first, whether live or not
         constexpr uint64_t spec = kSpec ? (1ull << kSpec) - 1u : 0u;
         nlive = (uint32_t)__builtin_popcountll(lm0 | spec);
-        lm0 &= ~spec;
+        lm0 = (lm0 & ~spec) | kSentinel;
 #pragma unroll
         for (int j = 0; j < kSpec; ++j) {
             qd[j] = (uint32_t)j;
@@ -481,7 +517,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 #pragma unroll
         for (int j = kSpec; j < D; ++j) {
             qd[j] = pop();
-            dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+            dv[j] = ring_load16<NT, SYS>(rd, live_voff(qd[j]));
         }
     }
 
@@ -492,20 +528,20 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     uint32_t acc = 0u;
 
     // General walk of seg_stream_kernel with per-packet ends (state written back unconditionally).
+    // Once the run's last packet has ended, e = kDone: no later piece has an event, and what the
+    // walk accumulates is never used.
     auto consume = [&](uint32_t q, u32x4 v) {
         const uint32_t qb = q << 10;
         const uint32_t pend = qb + 1024u;
         const uint32_t full = sum4(v, 0u);
         uint32_t u = cur, c = cs, e = ce, a = acc, t = tot_v;
-        if (!(u < s_end && e <= pend)) {                       // no packet ends in this piece
-            if (u < s_end) {
-                a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
-            }
+        if (e > pend) {                                        // no packet ends in this piece
+            a += (c <= qb) ? full : full - piece_prefix_t(v, full, lane16, min(c - qb, 1024u));
         } else {
-            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix_t(v, full, lane16, c - qb);
 #pragma clang loop vectorize(disable) unroll(disable)
             do {
-                const uint32_t Pe = piece_prefix(v, full, lane16, e <= qb ? 0u : e - qb);
+                const uint32_t Pe = piece_prefix_t(v, full, lane16, e <= qb ? 0u : e - qb);
                 const uint32_t T = wave_total(a + (Pe - Ps));
                 t = (lane == u - s_begin) ? T : t;
                 a = 0u;
@@ -516,14 +552,10 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
                     c += st;
                 }
                 const bool adj = c == e;                       // dense: the next packet starts at this end
-                if (u < s_end) {
-                    e = c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin));
-                }
-                Ps = adj ? Pe : piece_prefix(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
-            } while (u < s_end && e <= pend);
-            if (u < s_end) {
-                a = full - Ps;
-            }
+                e = u < s_end ? c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin)) : kDone;
+                Ps = adj ? Pe : piece_prefix_t(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
+            } while (e <= pend);
+            a = full - Ps;
         }
         cur = u;
         cs = c;
@@ -539,11 +571,11 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             if constexpr (BND >= 1) {
                 consume(qd[j], opaque_tuple(dv[j]));
                 qd[j] = pop();                                                // none left: OOB, zeros
-                dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+                dv[j] = ring_load16<NT, SYS>(rd, live_voff(qd[j]));
             } else {
                 const uint32_t q = r * (uint32_t)D + (uint32_t)j;
                 consume(q, opaque_tuple(dv[j]));
-                dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
+                dv[j] = ring_load16<NT, SYS>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
             }
             asm volatile("" ::: "memory");
         }
@@ -605,13 +637,24 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         const uint64_t r = (uint64_t)((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16)) |
                            ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) | ((uint64_t)(f & 0xFFu) << 48) |
                            ((uint64_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u)) << 56);
-        reinterpret_cast<uint64_t*>(rec)[idx] = r;
+        if constexpr (SYS) {                                   // (written through to host memory)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(rec) + idx, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            reinterpret_cast<uint64_t*>(rec)[idx] = r;
+        }
     } else {
+    auto put8 = [](uint8_t* p, uint32_t v) {
+        if constexpr (SYS) {
+            __hip_atomic_store(p, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            *p = (uint8_t)v;
+        }
+    };
     if (A.flags_out && !need) {
-        A.flags_out[idx] = (uint8_t)f;
+        put8(A.flags_out + idx, f);
     }
     if (!TX && A.action_out && !need) {
-        A.action_out[idx] = (uint8_t)rx_action(f, pk.proto, pk.v6, A.rx_cfg);
+        put8(A.action_out + idx, rx_action(f, pk.proto, pk.v6, A.rx_cfg));
     }
     if constexpr (TX) {
         uint8_t* p = reinterpret_cast<uint8_t*>(O + prel);
@@ -629,7 +672,14 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     }
     if constexpr (kWalkHere) {
         if (walk_here) {
+            const bool any = SYS && __builtin_amdgcn_ballot_w64(need) != 0u;
+            if (any) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the walk's plain loads: fresh host lines
+            }
             v6walk::walk_wave<TX>(A, s_begin, need, lane);
+            if (any) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // and its plain result stores out
+            }
         }
     }
 }
@@ -638,14 +688,13 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 // slot's present bytes ending before the next one starts, within 64 KiB from the run's first
 // 128-B line (the live-piece bitmap's reach); any other run is done one datagram at a time, each as
 // a run of its own (correct for any order or overlap, at one prologue per datagram).
-template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
-__global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
+// Run `run` (packets run * spw ...) by wave w of its block.
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL, bool SYS = false>
+__device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t spw, PktTxRecord* rec, uint64_t run,
+                                               uint32_t w, uint32_t lane) {
     // (offset/length runs: the live-piece forms 1 / 2, and 0 for a datagram past the bitmap's reach)
     static_assert(!VL || BND == 1 || BND == 2, "offset/length runs take the live-piece forms");
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
+    const uint64_t sb64 = run * spw;
     if (sb64 >= A.n) {
         return;
     }
@@ -656,7 +705,7 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         const uintptr_t O = a_first & ~(uintptr_t)127;
         const uint32_t lead0 = (uint32_t)(a_first - O);
         const uint32_t st = (uint32_t)A.stride;
-        pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, lead0 + lane * st, A.len_u,
+        pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin, nres, O, lead0 + lane * st, A.len_u,
                                              lead0 + (nres - 1u) * st + A.len_u);
     } else {
         const bool mine = lane < nres;
@@ -669,11 +718,11 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
         const uint64_t end = rel + len;
         // ordered: lane k starts at or after lane k - 1's present bytes end (DPP shift by one lane)
         const uint32_t prev_end_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
-        const bool ok = !mine || (rel < (64u << 10) && end <= (64u << 10) - 128u &&
+        const bool ok = !mine || (rel < kLiveReach && end <= kLiveReach - 128u &&
                                   (lane == 0u || (uint64_t)prev_end_lo <= rel));
         if (__builtin_amdgcn_ballot_w64(!ok) == 0u) {
             const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u));
-            pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, mine ? (uint32_t)rel : 0u,
+            pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin, nres, O, mine ? (uint32_t)rel : 0u,
                                                  len, span);
         } else {
             for (uint32_t k = 0; k < nres; ++k) {                // one datagram per run
@@ -682,14 +731,21 @@ __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_
                 const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)k);
                 const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
                 const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
-                if (pk + lk <= (64u << 10)) {
-                    pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                if (pk + lk <= kLiveReach) {
+                    pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
                 } else {                                         // past the bitmap's reach: the whole span
-                    pkt_run<D, NT, TX, REC, VER, 0, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                    pkt_run<D, NT, TX, REC, VER, 0, VL, SYS>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
                 }
             }
         }
     }
+}
+
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
+__global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    pkt_stream_run<D, NT, TX, REC, VER, BND, VL>(A, spw, rec, (uint64_t)blk * 4u + w, w, threadIdx.x & 63u);
 }
 
 // Second pass of the two-pass Tx: one thread per packet writes its fields (and flags) from its record.
@@ -790,6 +846,139 @@ __global__ void __launch_bounds__(64) burst_done_kernel(const uint8_t* fl, const
     }
 }
 
+// ---- resident burst server (NETCSUM_TUNE_BURST_ZERO_COPY 3; netcsum_abi.hip burst_server_post)
+// A small burst's work is a few PCIe round trips; a kernel launch per burst costs more than that. The
+// server is launched once and stays: wave 0 of each block (the leader) polls the post line, a 64-B
+// line of coherent host memory read as a whole (one request: its check catches a read that tore it),
+// and hands a burst it has not served to its block through LDS; the block's 4 waves then take runs
+// blockIdx * 4 + w, + 4 * blocks, ... of the burst with the run-stream code above (mixed IPv4 / IPv6,
+// 4 pieces in flight), write the results into coherent host memory and release them. A block idle for
+// idle_ticks stops (Dekker's handshake with the host: it marks itself closed, fences, and reads the
+// line once more; the host posts, fences and reads the marks, so a burst posted meanwhile is taken
+// here or found by the host, which waits the server out and relaunches it when the burst is unserved).
+constexpr uint32_t kServeRun = 1u, kServeExit = 2u;
+
+__device__ uint32_t burst_leader_wait(const BurstServerArgs& S, uint64_t seen, uint32_t lane, uint32_t* s_line) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool closing = false;
+    for (;;) {
+        uint64_t v = 0u;
+        if (lane < 8u) {                                        // lanes 0..7: the line's 8 quadwords
+            v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(S.post) + lane, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        uint32_t d[12];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            d[2 * i] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, i);
+            d[2 * i + 1] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), i);
+        }
+        BurstPost p{};
+        p.seq = ((uint64_t)d[1] << 32) | d[0];
+        p.ring = ((uint64_t)d[3] << 32) | d[2];
+        p.stride = d[4];
+        p.n = d[5];
+        p.pkt_len = d[6];
+        p.spw = d[7];
+        p.form = d[8];
+        p.udp_mode = d[9];
+        p.rx_cfg = d[10];
+        p.check = d[11];
+        if (p.seq != seen && p.check == burst_post_check(p)) {
+            if (lane < 6u) {
+                s_line[2u * lane] = (uint32_t)v;
+                s_line[2u * lane + 1u] = (uint32_t)(v >> 32);
+            }
+            return p.seq == kBurstStop ? kServeExit : closing ? (kServeRun | kServeExit) : kServeRun;
+        }
+        if (closing) {
+            return kServeExit;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > S.idle_ticks) {
+            closing = true;
+            if (lane == 0u) {
+                __hip_atomic_store(S.closed + blockIdx.x, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");       // the mark before the line's last read
+            continue;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <bool TX, int BND, bool VL>
+__device__ __forceinline__ void burst_serve(const PktBatchArgs& A, uint32_t spw, PktTxRecord* rec, uint32_t w,
+                                            uint32_t lane) {
+    const uint32_t runs = (A.n + spw - 1u) / spw;
+    for (uint32_t r = blockIdx.x * 4u + w; r < runs; r += gridDim.x * 4u) {
+        pkt_stream_run<4, true, TX, TX, 0, BND, VL, true>(A, spw, rec, r, w, lane);
+    }
+}
+
+__global__ void __launch_bounds__(256) burst_server_kernel(BurstServerArgs S) {
+    __shared__ uint32_t s_line[12];
+    __shared__ uint32_t s_cmd;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t seen = S.seq0;
+    for (;;) {
+        if (w == 0u) {
+            const uint32_t cmd = burst_leader_wait(S, seen, lane, s_line);
+            if (lane == 0u) {
+                s_cmd = cmd;
+            }
+        }
+        __syncthreads();
+        const uint32_t cmd = __builtin_amdgcn_readfirstlane(s_cmd);
+        if (cmd & kServeRun) {
+            uint32_t d[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                d[i] = __builtin_amdgcn_readfirstlane(s_line[i]);
+            }
+            PktBatchArgs A{};
+            A.base = reinterpret_cast<const uint8_t*>(((uint64_t)d[3] << 32) | d[2]);
+            A.stride = d[4];
+            A.n = d[5];
+            A.len_u = d[6];
+            const uint32_t spw = d[7], form = d[8];
+            A.udp_tx_csum = d[9];
+            A.rx_cfg = d[10];
+            if ((form >> 1) == kBurstOffLen) {
+                A.off = S.off;
+                A.len = S.len;
+            }
+            // No fence: the ring is read and the results are written at system scope (pkt_run<SYS>),
+            // the descriptors lie in coherent host memory (an L2 invalidate and write-back per wave and
+            // burst were measured slower, tools/burst_latency.c zc)
+            if (form & 1u) {
+                if ((form >> 1) == kBurstWhole) {
+                    burst_serve<true, 0, false>(A, spw, S.rec, w, lane);
+                } else if ((form >> 1) == kBurstLive) {
+                    burst_serve<true, 2, false>(A, spw, S.rec, w, lane);
+                } else {
+                    burst_serve<true, 2, true>(A, spw, S.rec, w, lane);
+                }
+            } else {
+                A.flags_out = S.flags;
+                A.action_out = S.act;
+                if ((form >> 1) == kBurstWhole) {
+                    burst_serve<false, 0, false>(A, spw, nullptr, w, lane);
+                } else if ((form >> 1) == kBurstLive) {
+                    burst_serve<false, 2, false>(A, spw, nullptr, w, lane);
+                } else {
+                    burst_serve<false, 2, true>(A, spw, nullptr, w, lane);
+                }
+            }
+            seen = ((uint64_t)d[1] << 32) | d[0];
+        }
+        if (cmd & kServeExit) {
+            break;
+        }
+        __syncthreads();                                        // s_line / s_cmd free for the next post
+    }
+}
+
 thread_local TuneKnob g_tx_flush{-1};
 
 int tx_flush_mode() {
@@ -856,6 +1045,14 @@ hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, 
     return hipGetLastError();
 }
 
+hipError_t launch_burst_server(const BurstServerArgs& a, int blocks, hipStream_t s) {
+    if (blocks < 1 || blocks > kBurstServerMaxBlocks || a.post == nullptr || a.closed == nullptr) {
+        return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(burst_server_kernel, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 void set_tx_flush(int mode) {
     g_tx_flush.store(mode);
 }
@@ -866,7 +1063,7 @@ void set_tx_flush(int mode) {
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
     if (a.off != nullptr) return (bound == 1 || bound == 2) && a.len != nullptr;
-    if (bound >= 1 && a.len_u + 128u > 64u * 1024u) return false;       // a run of one spans <= 64 KiB
+    if (bound >= 1 && a.len_u + 128u > kLiveReach) return false;        // a run of one spans <= 63 KiB
     return a.len_u >= 64u && a.stride >= a.len_u && ((bound == 1 || bound == 2) || a.stride <= a.len_u + 64u) &&
            (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
 }
@@ -878,7 +1075,7 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
     }
     // live pieces: a strided run spans at most 64 pieces (the host sizes runs for it; offset/length
     // runs check their span on the device)
-    if (bound >= 1 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > 64u * 1024u) {
+    if (bound >= 1 && a.off == nullptr && 128u + (uint64_t)(spw - 1u) * a.stride + a.len_u > kLiveReach) {
         return hipErrorInvalidValue;
     }
     const bool vl = a.off != nullptr;

@@ -70,6 +70,7 @@ TUNE_HDR_BURST = 19
 TUNE_VARLEN_RUN_BYTES = 20
 TUNE_PKT_BOUND = 21
 TUNE_BURST_ZERO_COPY = 22
+TUNE_BURST_SERVER_IDLE_US = 23
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
