@@ -391,6 +391,12 @@ NET_ERR  NetUtil_MI355X_RxBurstTally       (const uint8_t   *h_action,
  * (tools/burst_latency.c). Host buffers should be pinned (hipHostMalloc / hipHostRegister) for the
  * copies to run at PCIe rate. Returns when every result is in
  * host memory. IP = mixed IPv4 / IPv6 (per datagram by the version nibble).
+ * Packet bursts (RxValidateIPHost, TxFinalizeIPHost, RxBurstHost, TxBurstHost) of <= 4096 frames with
+ * n_chunks 0 whose frames lie in ONE pinned allocation (<= 64 MiB span) are not copied: the calling
+ * thread's resident burst server kernel reads them in place over PCIe and writes the results into
+ * coherent pinned memory the call polls (NETCSUM_TUNE_BURST_ZERO_COPY; 1 frame ~7 us, 64 frames
+ * ~11 us). The server stays resident until idle for NETCSUM_TUNE_BURST_SERVER_IDLE_US (500 us), so a
+ * device-wide synchronisation right after a burst may wait up to that long.
  * ============================================================================================ */
 NET_ERR  NetUtil_MI355X_ChkSumBatchVarLenHost(const void      *h_base,
                                               const uint64_t  *h_seg_off,
@@ -664,13 +670,13 @@ typedef enum netcsum_tune_key {
                                          batches                                                     */
     NETCSUM_TUNE_BURST_ZERO_COPY = 22,/* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
-                                         3 = a resident server kernel (one per calling thread, on a stream
-                                         of its own) takes each burst from a 64-B post in coherent host
-                                         memory, no launch per burst; 2 (default) a launch per burst, the
-                                         results go straight to coherent pinned memory and the host polls
-                                         them; 1 = a completion kernel copies the results out and stores
-                                         a completion word the host polls; 0 = the copy pipeline (H2D,
-                                         kernel, D2H, stream synchronisation)                           */
+                                         3 (default) = a resident server kernel (one per calling thread,
+                                         on a stream of its own) takes each burst from a 64-B post in
+                                         coherent host memory, no launch per burst; 2 = a launch per
+                                         burst, the results go straight to coherent pinned memory and the
+                                         host polls them; 1 = a completion kernel copies the results out
+                                         and stores a completion word the host polls; 0 = the copy
+                                         pipeline (H2D, kernel, D2H, stream synchronisation)            */
     NETCSUM_TUNE_BURST_SERVER_IDLE_US = 23 /* mode 3: microseconds without a burst after which the server
                                          stops (the next burst relaunches it); a device-wide
                                          synchronisation waits up to this long. 1..1000000, default 500 */

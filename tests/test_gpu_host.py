@@ -226,7 +226,7 @@ def test_rx_burst_host_zero_copy(n, form):
             netcsum.rx_burst_host(base(ring), n, act2, **kw)           # actions only
             assert np.array_equal(act2, want_a)
         finally:
-            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
         r = ring.numpy() if hasattr(ring, "numpy") else ring
         assert np.array_equal(r, buf)
 
@@ -310,7 +310,7 @@ def test_tx_burst_host_zero_copy(n, form):
                 lens = np.full(n, stride - lead, np.uint16)
                 netcsum.tx_burst_host(hb, n, fl, off=offs, lens=lens)
         finally:
-            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
         got = hb.numpy()
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (zc, [(int(j) // stride, int(j) % stride) for j in bad[:8]])
@@ -365,7 +365,7 @@ def test_burst_server_idle_stop_and_relaunch():
         torch.cuda.synchronize()
     finally:
         netcsum.tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500)
-        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
 
 
 @pytest.mark.parametrize("zc", [2, 3])
@@ -404,4 +404,4 @@ def test_zero_copy_ring_rewritten_between_bursts(zc):
                 netcsum.tx_burst_host(hb[lead:], n, None, stride=stride, pkt_len=stride - lead)
                 assert np.array_equal(hv, txs[j]), (it, j)
     finally:
-        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 2)
+        netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)

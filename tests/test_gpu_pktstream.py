@@ -348,3 +348,40 @@ def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run, copies):
     rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, 2, True)
     assert f"pkts_per_wave={spw}" in d_rx and f"pkts_per_wave={spw}" in d_tx, (d_rx, d_tx)
     assert np.array_equal(rx, rx_ref) and np.array_equal(tx, tx_ref) and np.array_equal(txf, txf_ref)
+
+
+def test_graph_capture_then_larger_uncaptured_batch_on_the_same_stream():
+    """Scratch leases under stream capture (INTEGRATION §4 graph-capture note): a two-pass Tx batch is
+    captured into a HIP graph after one uncaptured warm-up call (its record slot is then pinned to the
+    graph); a LARGER uncaptured two-pass Tx batch on the same stream (1.1 MB of records: more than the
+    1-MiB slot) takes a slot of its own instead of failing or growing the graph's; the graph, replayed
+    afterwards, still finalizes its own batch. Every byte and flag equals the oracle's."""
+    netcsum.tune(netcsum.TUNE_TX_PASSES, 2)
+    rng = random.Random(5151)
+    n1, n2, L = 600, 140000, 64
+    buf1 = _batch(rng, n1, L, L, 0)
+    buf2 = _batch(rng, n2, L, L, 0)
+    _, tx1_w, txf1_w = _want(buf1, n1, L, L, 0, True)
+    _, tx2_w, txf2_w = _want(buf2, n2, L, L, 0, True)
+    s = torch.cuda.Stream(device=DEV)
+    b1 = torch.from_numpy(buf1).to(DEV)
+    f1 = torch.zeros(n1, dtype=torch.uint8, device=DEV)
+    with torch.cuda.stream(s):
+        netcsum.tx_finalize_ipv4(b1, n1, f1, stride=L, pkt_len=L, stream=s)      # uncaptured warm-up
+    s.synchronize()
+    b1.copy_(torch.from_numpy(buf1).to(DEV))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        netcsum.tx_finalize_ipv4(b1, n1, f1, stride=L, pkt_len=L, stream=s)
+    b2 = torch.from_numpy(buf2).to(DEV)
+    f2 = torch.zeros(n2, dtype=torch.uint8, device=DEV)
+    with torch.cuda.stream(s):
+        netcsum.tx_finalize_ipv4(b2, n2, f2, stride=L, pkt_len=L, stream=s)
+    s.synchronize()
+    assert np.array_equal(b2.cpu().numpy(), tx2_w) and np.array_equal(f2.cpu().numpy(), txf2_w)
+    b1.copy_(torch.from_numpy(buf1).to(DEV))
+    f1.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(b1.cpu().numpy(), tx1_w) and np.array_equal(f1.cpu().numpy(), txf1_w)

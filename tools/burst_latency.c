@@ -9,10 +9,10 @@
  *   rx_dev / tx_dev    RxBurst / TxBurst on a device-resident ring + hipStreamSynchronize
  *   rx_host / tx_host  RxBurstHost / TxBurstHost on a pinned host ring in one chunk, which return
  *                      with the results in host memory (_auto: n_chunks 0, the library's choice —
- *                      up to 4096 frames the kernel reads the pinned ring in place and the host
- *                      polls the results; _auto_copy: the same with NETCSUM_TUNE_BURST_ZERO_COPY
- *                      0; _server: 3, the resident burst server; from 1024 frames also in 2-16
- *                      chunks: _cK)
+ *                      up to 4096 frames the resident burst server reads the pinned ring in place
+ *                      and the host polls the results; _auto_copy: the same with
+ *                      NETCSUM_TUNE_BURST_ZERO_COPY 0, the copy pipeline; _launch: 2, a kernel launch
+ *                      per burst; from 1024 frames also in 2-16 chunks: _cK)
  * and a check that every Rx action is DELIVER. One JSON line per n on stdout.
  *
  * Built here (the binary travels with the tree; tools/build/ is git-ignored), run on the GPU box:
@@ -198,7 +198,7 @@ static int zc_only(void)
         }
     }
     NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_PKT_BOUND, -1));
-    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
+    NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 3));
     printf("}\n");
     return 0;
 }
@@ -243,14 +243,15 @@ int main(int argc, char **argv)
         /* n_chunks 0 without the zero-copy burst path (the copy pipeline in one chunk) */
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 0));
         printf(", \"rx_host_us_auto_copy\": %.2f", time_us(RX_HOST, n));
-        /* ... and with the resident burst server (TUNE_BURST_ZERO_COPY 3) */
         NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 3));
+        /* ... and with a kernel launch per burst, results polled (TUNE_BURST_ZERO_COPY 2) */
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
         if (n <= 4096u) {
             memset(g_hact, 0xEE, NMAX);
-            printf(", \"rx_host_us_server\": %.2f, \"tx_host_us_server\": %.2f", time_us(RX_HOST, n), time_us(TX_HOST, n));
+            printf(", \"rx_host_us_launch\": %.2f, \"tx_host_us_launch\": %.2f", time_us(RX_HOST, n), time_us(TX_HOST, n));
             for (i = 0; i < n; ++i) ok &= g_hact[i] == NETCSUM_RX_DELIVER;
         }
-        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 2));
+        NET_OK(NetUtil_MI355X_Tune(NETCSUM_TUNE_BURST_ZERO_COPY, 3));
         for (g_chunks = 2u; g_chunks <= 16u && n >= 1024u; g_chunks *= 2u) {
             printf(", \"rx_host_us_c%u\": %.2f", g_chunks, time_us(RX_HOST, n));
             printf(", \"tx_host_us_c%u\": %.2f", g_chunks, time_us(TX_HOST, n));

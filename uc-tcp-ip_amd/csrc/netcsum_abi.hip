@@ -33,7 +33,7 @@ thread_local netcsum::TuneKnob g_tune_chunks{0};
 thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read probe by default
 thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
-thread_local netcsum::TuneKnob g_tune_burst_zc{2};              // host bursts read pinned rings in place, results polled
+thread_local netcsum::TuneKnob g_tune_burst_zc{3};              // host bursts: pinned rings read in place by the resident server
 thread_local netcsum::TuneKnob g_tune_burst_idle{500};           // resident burst server: idle microseconds before it stops
 thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2

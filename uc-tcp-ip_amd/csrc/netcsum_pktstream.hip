@@ -419,18 +419,10 @@ __device__ __forceinline__ uint32_t piece_prefix_t(u32x4 v, uint32_t s4, uint32_
     pv = __builtin_amdgcn_sad_u16(v.w & (uint32_t)(m.m1 >> 32), 0u, pv);
     return (lane16 + 16u <= x) ? s4 : ((lane16 < x) ? pv : 0u);
 }
-// SYS (the resident burst server): the run's loads at system scope (sc0 sc1), so that no line of
-// the host ring an L2 holds from an earlier burst is used (the host rewrites its ring between
-// bursts; a kernel launch per burst gets that from the launch's cache invalidation).
-template <bool NT, bool SYS>
-__device__ __forceinline__ u32x4 ring_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, (NT ? 2 : 0) | (SYS ? 17 : 0));
-}
-
 // One wave run: packets s_begin .. s_begin + nres - 1, lane k's packet at run-relative offset prel
 // (from O, 128-B aligned) with `avail` bytes present; the run's bytes [O, O + span). VL: per-packet
 // starts (offset/length descriptors) instead of a stride.
-template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL, bool SYS = false>
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec, uint32_t w, uint32_t lane,
                                         uint32_t s_begin, uint32_t nres, uintptr_t O, uint32_t prel, uint32_t avail,
                                         uint32_t span) {
@@ -445,7 +437,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     constexpr int kSpec = BND == 0 || BND == 3 ? D : BND == 2 ? 1 : 0;   // pieces loaded before the parse
 #pragma unroll
     for (int j = 0; j < kSpec; ++j) {                          // the first pieces in flight ...
-        dv[j] = ring_load16<NT, SYS>(rd, ((uint32_t)j << 10) + lane16);
+        dv[j] = buf_load16<NT>(rd, ((uint32_t)j << 10) + lane16);
     }
 
     // ... while lane k parses packet k from its own 96-B window.
@@ -455,7 +447,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     u32x4 h[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-        h[c] = ring_load16<false, SYS>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
+        h[c] = buf_load16<false>(rd, mine ? pq + 16u * (uint32_t)c : kOOB);
     }
     uint32_t wd[24];
 #pragma unroll
@@ -517,7 +509,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 #pragma unroll
         for (int j = kSpec; j < D; ++j) {
             qd[j] = pop();
-            dv[j] = ring_load16<NT, SYS>(rd, live_voff(qd[j]));
+            dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
         }
     }
 
@@ -571,11 +563,11 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             if constexpr (BND >= 1) {
                 consume(qd[j], opaque_tuple(dv[j]));
                 qd[j] = pop();                                                // none left: OOB, zeros
-                dv[j] = ring_load16<NT, SYS>(rd, live_voff(qd[j]));
+                dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
             } else {
                 const uint32_t q = r * (uint32_t)D + (uint32_t)j;
                 consume(q, opaque_tuple(dv[j]));
-                dv[j] = ring_load16<NT, SYS>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
+                dv[j] = buf_load16<NT>(rd, ((q + (uint32_t)D) << 10) + lane16);   // past the run: zeros
             }
             asm volatile("" ::: "memory");
         }
@@ -637,24 +629,13 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         const uint64_t r = (uint64_t)((cip & 0xFFFFu) | ((cl4 & 0xFFFFu) << 16)) |
                            ((uint64_t)(pk.l4_csum_off & 0xFFFFu) << 32) | ((uint64_t)(f & 0xFFu) << 48) |
                            ((uint64_t)((cip != ~0u ? 1u : 0u) | (cl4 != ~0u ? 2u : 0u)) << 56);
-        if constexpr (SYS) {                                   // (written through to host memory)
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(rec) + idx, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-            reinterpret_cast<uint64_t*>(rec)[idx] = r;
-        }
+        reinterpret_cast<uint64_t*>(rec)[idx] = r;
     } else {
-    auto put8 = [](uint8_t* p, uint32_t v) {
-        if constexpr (SYS) {
-            __hip_atomic_store(p, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-            *p = (uint8_t)v;
-        }
-    };
     if (A.flags_out && !need) {
-        put8(A.flags_out + idx, f);
+        A.flags_out[idx] = (uint8_t)f;
     }
     if (!TX && A.action_out && !need) {
-        put8(A.action_out + idx, rx_action(f, pk.proto, pk.v6, A.rx_cfg));
+        A.action_out[idx] = (uint8_t)rx_action(f, pk.proto, pk.v6, A.rx_cfg);
     }
     if constexpr (TX) {
         uint8_t* p = reinterpret_cast<uint8_t*>(O + prel);
@@ -672,14 +653,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     }
     if constexpr (kWalkHere) {
         if (walk_here) {
-            const bool any = SYS && __builtin_amdgcn_ballot_w64(need) != 0u;
-            if (any) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the walk's plain loads: fresh host lines
-            }
             v6walk::walk_wave<TX>(A, s_begin, need, lane);
-            if (any) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // and its plain result stores out
-            }
         }
     }
 }
@@ -689,7 +663,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
 // 128-B line (the live-piece bitmap's reach); any other run is done one datagram at a time, each as
 // a run of its own (correct for any order or overlap, at one prologue per datagram).
 // Run `run` (packets run * spw ...) by wave w of its block.
-template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL, bool SYS = false>
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t spw, PktTxRecord* rec, uint64_t run,
                                                uint32_t w, uint32_t lane) {
     // (offset/length runs: the live-piece forms 1 / 2, and 0 for a datagram past the bitmap's reach)
@@ -705,7 +679,7 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
         const uintptr_t O = a_first & ~(uintptr_t)127;
         const uint32_t lead0 = (uint32_t)(a_first - O);
         const uint32_t st = (uint32_t)A.stride;
-        pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin, nres, O, lead0 + lane * st, A.len_u,
+        pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, lead0 + lane * st, A.len_u,
                                              lead0 + (nres - 1u) * st + A.len_u);
     } else {
         const bool mine = lane < nres;
@@ -722,7 +696,7 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
                                   (lane == 0u || (uint64_t)prev_end_lo <= rel));
         if (__builtin_amdgcn_ballot_w64(!ok) == 0u) {
             const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u));
-            pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin, nres, O, mine ? (uint32_t)rel : 0u,
+            pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin, nres, O, mine ? (uint32_t)rel : 0u,
                                                  len, span);
         } else {
             for (uint32_t k = 0; k < nres; ++k) {                // one datagram per run
@@ -732,9 +706,9 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
                 const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
                 const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
                 if (pk + lk <= kLiveReach) {
-                    pkt_run<D, NT, TX, REC, VER, BND, VL, SYS>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                    pkt_run<D, NT, TX, REC, VER, BND, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
                 } else {                                         // past the bitmap's reach: the whole span
-                    pkt_run<D, NT, TX, REC, VER, 0, VL, SYS>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+                    pkt_run<D, NT, TX, REC, VER, 0, VL>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
                 }
             }
         }
@@ -911,7 +885,7 @@ __device__ __forceinline__ void burst_serve(const PktBatchArgs& A, uint32_t spw,
                                             uint32_t lane) {
     const uint32_t runs = (A.n + spw - 1u) / spw;
     for (uint32_t r = blockIdx.x * 4u + w; r < runs; r += gridDim.x * 4u) {
-        pkt_stream_run<4, true, TX, TX, 0, BND, VL, true>(A, spw, rec, r, w, lane);
+        pkt_stream_run<4, true, TX, TX, 0, BND, VL>(A, spw, rec, r, w, lane);
     }
 }
 
@@ -948,9 +922,11 @@ __global__ void __launch_bounds__(256) burst_server_kernel(BurstServerArgs S) {
                 A.off = S.off;
                 A.len = S.len;
             }
-            // No fence: the ring is read and the results are written at system scope (pkt_run<SYS>),
-            // the descriptors lie in coherent host memory (an L2 invalidate and write-back per wave and
-            // burst were measured slower, tools/burst_latency.c zc)
+            // a wave with runs of this burst: the ring's and descriptors' bytes fresh from host memory
+            // (L1 / L2 invalidate)
+            if (blockIdx.x * 4u + w < (A.n + spw - 1u) / spw) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            }
             if (form & 1u) {
                 if ((form >> 1) == kBurstWhole) {
                     burst_serve<true, 0, false>(A, spw, S.rec, w, lane);
@@ -971,6 +947,14 @@ __global__ void __launch_bounds__(256) burst_server_kernel(BurstServerArgs S) {
                 }
             }
             seen = ((uint64_t)d[1] << 32) | d[0];
+            // the block's result stores have reached the L2 (the barrier's release), then one
+            // system-scope release writes them back to host memory. (Per wave: 64 frames 12.5 us;
+            // system-scope loads and stores instead of fences 13.0 us for Tx and 23.8 us for Rx, whose
+            // byte stores then cross PCIe one by one: tools/burst_latency.c zc, profiles/r4p_burst_zc.jsonl)
+            __syncthreads();
+            if (w == 0u && blockIdx.x * 4u < (A.n + spw - 1u) / spw) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            }
         }
         if (cmd & kServeExit) {
             break;
