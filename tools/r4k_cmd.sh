@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 evidence on the final sources, part B: per-row PMC sessions (tools/gpu_pmc_all.sh), the C
-# driver's burst latency table and breakdown, the NIC-ring probe.
+# driver's burst latency table and breakdown, the NIC-ring probe, the instruction mix of the sparse
+# layouts and the live-sector read probe.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -10,4 +11,7 @@ bash tools/gpu_pmc_all.sh $T || exit 1
 timeout -k 10 300 tools/build/burst_latency > $O/${T}_burst_latency.jsonl 2> $O/${T}_burst_latency.err || { tail $O/${T}_burst_latency.err; exit 1; }
 timeout -k 10 120 tools/build/burst_latency zc > $O/${T}_burst_zc.jsonl 2> $O/${T}_burst_zc.err || { tail $O/${T}_burst_zc.err; exit 1; }
 timeout -k 10 500 python -u tools/ring_probe.py > $O/${T}_ring_probe.jsonl 2> $O/${T}_ring_probe.err || { tail $O/${T}_ring_probe.err; exit 1; }
+for c in rx_nb2k rx_ring rx_nb2kv; do bash tools/gpu_instmix.sh $T $c > /dev/null || exit 1; done
+python3 tools/instmix_summary.py $O/${T}_*_instmix > $O/${T}_instmix.txt || exit 1
+timeout -k 10 400 tools/build/live_read_probe > $O/${T}_live_read_probe.jsonl 2> $O/${T}_live_read_probe.err || { tail $O/${T}_live_read_probe.err; exit 1; }
 echo "session $T done"
