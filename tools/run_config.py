@@ -16,7 +16,8 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   rx_ring / tx_ring  1 M mixed 40/576/1500-B datagrams (7:4:1) in 1520-B slots at +14, strided,
        pkt_len 1506; rx_ringv / tx_ringv the same ring by offset/length descriptors; rx_nb2kv /
        tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
-  suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run (e.g. rx_ring.b0.s32)
+  suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N
+  (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
@@ -36,8 +37,12 @@ from bench import SEED, c2_pseudo_headers  # noqa: E402
 def main():
     name = sys.argv[1]
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-    # suffixes: ".bN" = NETCSUM_TUNE_PKT_BOUND N, ".sN" = TUNE_TILE N (packets per wave run)
+    # suffixes: ".bN" = NETCSUM_TUNE_PKT_BOUND N, ".sN" = TUNE_TILE N (packets per wave run),
+    # ".ntN" = NETCSUM_TUNE_NT N (NETCSUM_TUNE_NT_LOADS; 0: plain-policy stream loads)
     for part in name.split(".")[1:]:
+        if part.startswith("nt"):
+            netcsum.tune(netcsum.TUNE_NT_LOADS, int(part[2:]))
+            continue
         if part[:1] == "b":
             netcsum.tune(netcsum.TUNE_PKT_BOUND, int(part[1:]))
         elif part[:1] == "s":
