@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--pmc", choices=["live", "file", "off"], default="live",
                     help="roofline.traffic source: live rocprofv3 --pmc passes over a child run (rank 0, N=1; "
                          "falls back to the committed summaries), committed file only, or none")
-    ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block)")
+    ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block/kernel/chunks/tile/mult/xcd/touch/waves)")
     ap.add_argument("--no-c5-point", action="store_true",
                     help="N=1: skip the same-workload retention point (the C5 16 M-segment shard on this GPU)")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
@@ -551,7 +551,8 @@ def main():
 
     keymap = {"grid": netcsum.TUNE_GRID_BLOCKS, "group": netcsum.TUNE_GROUP_LANES,
               "nt": netcsum.TUNE_NT_LOADS, "block": netcsum.TUNE_BLOCK_THREADS, "kernel": netcsum.TUNE_KERNEL,
-              "chunks": netcsum.TUNE_CHUNKS, "tile": netcsum.TUNE_TILE, "mult": netcsum.TUNE_GRID_MULT}
+              "chunks": netcsum.TUNE_CHUNKS, "tile": netcsum.TUNE_TILE, "mult": netcsum.TUNE_GRID_MULT,
+              "xcd": netcsum.TUNE_STREAM_XCD, "touch": netcsum.TUNE_STREAM_TOUCH, "waves": netcsum.TUNE_STREAM_WAVES}
     for kv in args.tune:
         k, v = kv.split("=")
         netcsum.tune(keymap[k], int(v))

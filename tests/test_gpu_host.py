@@ -3,6 +3,7 @@ pointer in host memory, the batch pipelined in chunks over three streams (H2D of
 span and rebased descriptors -> the device form -> D2H of the results; Tx writes the span back).
 Results equal the oracle's for 1, 2, 3, 7 and 64 chunks, packed and unsorted offset/length batches,
 strided batches, odd base offsets; an overlapping Tx batch (chunk spans that overlap) is still exact."""
+import os
 import random
 
 import numpy as np
@@ -16,6 +17,7 @@ from packets import KINDS, KINDS6, make_packet, make_packet_v6, packed_batch
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(autouse=True)
@@ -405,3 +407,36 @@ def test_zero_copy_ring_rewritten_between_bursts(zc):
                 assert np.array_equal(hv, txs[j]), (it, j)
     finally:
         netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
+
+
+def test_burst_server_process_exit_and_thread_release():
+    """A process whose threads leave resident burst servers running exits cleanly: a child process
+    posts bursts from its main thread and from a worker thread that ends without ThreadRelease (its
+    context is released at thread exit, which stops its server), then exits while the main thread's
+    server is still resident (stopped by the thread-local destructor at exit). Exit status 0, well
+    inside the time limit; ThreadRelease on a live server returns at once."""
+    import subprocess
+    import sys
+    import time
+    code = r"""
+import threading, time, numpy as np, torch, netcsum
+stride, n = 1520, 32
+buf = torch.zeros(n * stride, dtype=torch.uint8).pin_memory()
+fl = np.zeros(n, np.uint8)
+netcsum.rx_validate_ip_host(buf, n, fl, stride=stride, pkt_len=stride)
+def worker():
+    f2 = np.zeros(n, np.uint8)
+    for _ in range(50):
+        netcsum.rx_validate_ip_host(buf, n, f2, stride=stride, pkt_len=stride)
+t = threading.Thread(target=worker); t.start(); t.join()
+t0 = time.perf_counter(); netcsum.thread_release(); dt = time.perf_counter() - t0
+assert dt < 0.5, dt
+netcsum.rx_validate_ip_host(buf, n, fl, stride=stride, pkt_len=stride)   # a new server, left running
+print("ok", flush=True)
+"""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(REPO, "uc-tcp-ip_amd"), env.get("PYTHONPATH", "")])
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-400:], r.stderr[-800:])
+    assert time.perf_counter() - t0 < 100
