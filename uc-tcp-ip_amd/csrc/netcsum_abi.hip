@@ -1256,19 +1256,21 @@ NET_ERR NetUtil_MI355X_ChkSumBatchVarLenHost(const void* h_base, const uint64_t*
 // Cfg/Template/net_dev_cfg.c:147), so its cost is fixed, not bandwidth: an H2D copy, a launch, a D2H
 // copy and a stream synchronisation took 19.3 us for one frame (profiles/r3x_burst_latency.jsonl).
 // When the caller's ring is pinned (device-accessible host memory) the kernel reads it in place over
-// PCIe. By default (TUNE_BURST_ZERO_COPY 2) its flags and actions (Tx: 8-B field records) go straight
-// into coherent pinned memory that the host set to a sentinel no result can take (0xFF), and the host
-// polls them until every one has arrived — each is written once, so no completion protocol is needed —
-// instead of synchronising the stream. TUNE_BURST_ZERO_COPY 1: the results go to device memory and a
-// one-wave completion kernel copies them into coherent memory, then stores a tagged completion word
+// PCIe, and its flags and actions (Tx: 8-B field records) go straight into coherent pinned memory that
+// the host set to a sentinel no result can take (0xFF); the host polls them until every one has
+// arrived — each is written once, so no completion protocol is needed — instead of synchronising a
+// stream. By default (TUNE_BURST_ZERO_COPY 3) the kernel is this thread's resident burst server
+// (burst_server_run below), which takes each burst from a posted line: no launch per burst.
+// TUNE_BURST_ZERO_COPY 2: a launch per burst; 1: the results go to device memory and a one-wave
+// completion kernel copies them into coherent memory, then stores a tagged completion word
 // (system-scope release after the wave's own stores) that the host polls. tools/burst_latency.c zc,
-// profiles/r4f_burst_zc.jsonl: 64 frames 16.3 us (1) against 14.1 us (2); 1 frame 14.1 / 12.4 us. A
-// pageable ring takes the copy path.
+// profiles/r4k_burst_zc.jsonl: 1 / 64 frames 6.9 / 11.2 us (3), 10.8 / 12.9 us (2), 12.7 / 15.1 us
+// (1). A pageable ring takes the copy path.
 constexpr uint32_t kBurstZC = 4096u;                    // frames
 // Over PCIe a burst is latency-bound: the whole-slot stream (bound 0) issues the pieces with the
 // parse's loads (one round trip) where the live-piece forms parse first (two); it applies to
 // strided rings with gaps <= 64 B, the others keep the default (tools/burst_latency.c zc,
-// profiles/r4d_burst_zc.jsonl: 64 frames 17.4 -> 15.6 us)
+// profiles/r4k_burst_zc.jsonl: a launch per burst, 64 frames 12.9 us against 13.9 us in form 2)
 constexpr int kBurstBound = 0;
 constexpr uint64_t kBurstZCSpan = 64ull << 20;          // ring bytes the kernel may read in place
 constexpr size_t kBurstWord = 0, kBurstPost = 64, kBurstClosed = 128, kBurstFlags = 256, kBurstAct = kBurstFlags + kBurstZC,
