@@ -385,3 +385,48 @@ def test_graph_capture_then_larger_uncaptured_batch_on_the_same_stream():
     g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(b1.cpu().numpy(), tx1_w) and np.array_equal(f1.cpu().numpy(), txf1_w)
+
+
+@pytest.mark.parametrize("ver", [4, 6, 0])
+@pytest.mark.parametrize("bound", [-1, 0, 1, 3])
+@pytest.mark.parametrize("passes", [1, 2])
+def test_pkt_stream_datagrams_ending_at_the_window_edge(ver, bound, passes):
+    """The live forms sum a datagram whose bytes end inside the lane's 96-B header window from that
+    window and leave it out of the stream (no sectors marked, no event walked): short datagrams at
+    every window offset (stride 1521 walks the start through all 16 positions of a 16-B chunk),
+    ending before, at and past the window's end, among longer ones, odd and even starts, against
+    the oracle; form 0 (bound 0) keeps them in the stream and must agree."""
+    from packets import KINDS6, make_packet_v6
+    netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
+    try:
+        rng = random.Random(4099 + 10 * ver + bound + 7 * passes)
+        stride, pkt_len, lead, n = 1521, 1506, 5, 1600
+        buf = np.frombuffer(rng.randbytes(lead + n * stride + 96), np.uint8).copy()
+        for i in range(n):
+            v6 = ver == 6 or (ver == 0 and rng.random() < 0.5)
+            big = rng.random() < 0.15
+            if v6:
+                p = make_packet_v6(rng, rng.choice(KINDS6), payload=rng.randint(0, 1200 if big else 48))
+            else:
+                p = make_packet(rng, rng.choice(KINDS + ["udp", "tcp", "icmp"]), payload=rng.randint(0, 1200 if big else 70))
+            p = bytearray(p[:pkt_len])
+            if len(p) >= 12 and not v6 and rng.random() < 0.3:
+                p[10:12] = rng.randbytes(2)                       # stale IP checksum field
+            o = lead + i * stride
+            buf[o:o + len(p)] = np.frombuffer(bytes(p), np.uint8)
+        udp_tx_csum = True
+        if ver == 4:
+            rx_w, tx_w, txf_w = _want(buf, n, stride, pkt_len, lead, udp_tx_csum)
+            rx, tx, txf, d_rx, d_tx = _run(buf, n, stride, pkt_len, lead, udp_tx_csum)
+        else:
+            rx_w, tx_w, txf_w = _want_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
+            rx, tx, txf, d_rx, d_tx = _run_ip(buf, n, stride, pkt_len, lead, udp_tx_csum, ver)
+        assert d_rx.startswith("pkt_stream_kernel"), d_rx
+        bad = np.nonzero(rx != rx_w)[0]
+        assert bad.size == 0, [(int(i), int(rx[i]), int(rx_w[i])) for i in bad[:6]]
+        bad = np.nonzero(tx != tx_w)[0]
+        assert bad.size == 0, [(int(j), (int(j) - lead) // stride, (int(j) - lead) % stride) for j in bad[:8]]
+        assert np.array_equal(txf, txf_w)
+    finally:
+        netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)

@@ -66,22 +66,27 @@ __device__ __forceinline__ uint32_t ov(uint32_t x) {
     return x;
 }
 
-// Dword t of the lane's 24-dword window (t wave-divergent): a select chain in registers.
-__device__ __forceinline__ uint32_t win_dword(const uint32_t (&wd)[24], uint32_t t) {
-    uint32_t r = 0u;
+// Little-endian dword at packet offset x (lead + x + 3 < 96, lead + x >= 16 * C0): the 16-B chunk
+// holding byte lead + x and the next chunk's first dword by one select chain over chunks [C0, 6), then
+// a 4-way dword pick and one alignbyte (alignbyte by 0 is the low dword). About 40 VALU, against
+// about 75 for two 24-way dword selects over the window.
+template <int C0>
+__device__ __forceinline__ uint32_t pkt_dword_at(const u32x4 (&h)[6], uint32_t lead, uint32_t x) {
+    const uint32_t r = lead + x, c = r >> 4, q = (r >> 2) & 3u;
+    uint32_t a0 = ov(h[C0].x), a1 = ov(h[C0].y), a2 = ov(h[C0].z), a3 = ov(h[C0].w);
+    uint32_t a4 = C0 < 5 ? ov(h[C0 + 1].x) : 0u;
 #pragma unroll
-    for (int i = 0; i < 24; ++i) {
-        r = (t == (uint32_t)i) ? ov(wd[i]) : r;
+    for (int k = C0 + 1; k < 6; ++k) {
+        const bool m = c == (uint32_t)k;
+        a0 = m ? ov(h[k].x) : a0;
+        a1 = m ? ov(h[k].y) : a1;
+        a2 = m ? ov(h[k].z) : a2;
+        a3 = m ? ov(h[k].w) : a3;
+        a4 = m ? (k < 5 ? ov(h[k < 5 ? k + 1 : 5].x) : 0u) : a4;
     }
-    return r;
-}
-
-// Little-endian dword at packet offset x (lead + x + 3 < 96).
-__device__ __forceinline__ uint32_t pkt_dword_at(const uint32_t (&wd)[24], uint32_t lead, uint32_t x) {
-    const uint32_t r = lead + x;
-    const uint32_t lo = win_dword(wd, r >> 2), hi = win_dword(wd, (r >> 2) + 1u);
-    const uint32_t b = r & 3u;
-    return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+    const uint32_t lo = q == 0u ? a0 : q == 1u ? a1 : q == 2u ? a2 : a3;
+    const uint32_t hi = q == 0u ? a1 : q == 1u ? a2 : q == 2u ? a3 : a4;
+    return __builtin_amdgcn_alignbyte(hi, lo, r & 3u);
 }
 
 // The same for a fixed offset X (a multiple of 4): only lead >> 2 varies, a 4-way select.
@@ -92,8 +97,7 @@ __device__ __forceinline__ uint32_t pkt_dword_fixed(const uint32_t (&wd)[24], ui
     const uint32_t w0 = ov(wd[B]), w1 = ov(wd[B + 1]), w2 = ov(wd[B + 2]), w3 = ov(wd[B + 3]), w4 = ov(wd[B + 4]);
     const uint32_t lo = j == 0u ? w0 : j == 1u ? w1 : j == 2u ? w2 : w3;
     const uint32_t hi = j == 0u ? w1 : j == 1u ? w2 : j == 2u ? w3 : w4;
-    const uint32_t b = lead & 3u;
-    return b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+    return __builtin_amdgcn_alignbyte(hi, lo, lead & 3u);
 }
 
 // What the 2 bytes of a checksum field (even packet offset; b0 first) add to an exact sum in the
@@ -125,6 +129,44 @@ __device__ __forceinline__ uint32_t win_prefix(const u32x4 (&h)[6], uint32_t lea
         s += low_bytes(h[c], min(max((int)(lead + x) - 16 * c, 0), 16));
     }
     return s;
+}
+
+// Adds packet-frame dword d to an exact half-word sum in the absolute little-endian frame: for a
+// packet at an odd address the absolute half-words pair each byte with its packet-frame neighbour
+// the other way round, so sel (pkt_frame_sel) swaps the bytes of each half-word first.
+__device__ __forceinline__ uint32_t frame_sum(uint32_t d, uint32_t sel, uint32_t acc) {
+    return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(d, d, sel), 0u, acc);
+}
+
+__device__ __forceinline__ uint32_t pkt_frame_sel(bool odd) { return odd ? 0x02030001u : 0x03020100u; }
+
+// Exact half-word sum of the window's bytes [lead, lead + x) (absolute frame; lead < 16, lead + x <= 96):
+// the dwords below the end's dword by one compare each, the end's partial dword by a chunk select,
+// less the lead's bytes.
+__device__ __forceinline__ uint32_t win_range_sum(const u32x4 (&h)[6], uint32_t lead, uint32_t x) {
+    const uint32_t e = lead + x, je = e >> 2;
+    uint32_t s = 0u;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        s = __builtin_amdgcn_sad_u16(4u * c + 0u < je ? h[c].x : 0u, 0u, s);
+        s = __builtin_amdgcn_sad_u16(4u * c + 1u < je ? h[c].y : 0u, 0u, s);
+        s = __builtin_amdgcn_sad_u16(4u * c + 2u < je ? h[c].z : 0u, 0u, s);
+        s = __builtin_amdgcn_sad_u16(4u * c + 3u < je ? h[c].w : 0u, 0u, s);
+    }
+    // dword je's low e & 3 bytes (e = 96: none, and chunk 5 stands in for the absent chunk 6)
+    const uint32_t c = je >> 2, q = je & 3u;
+    uint32_t a0 = ov(h[0].x), a1 = ov(h[0].y), a2 = ov(h[0].z), a3 = ov(h[0].w);
+#pragma unroll
+    for (int k = 1; k < 6; ++k) {
+        const bool m = c >= (uint32_t)k;
+        a0 = m ? ov(h[k].x) : a0;
+        a1 = m ? ov(h[k].y) : a1;
+        a2 = m ? ov(h[k].z) : a2;
+        a3 = m ? ov(h[k].w) : a3;
+    }
+    const uint32_t de = q == 0u ? a0 : q == 1u ? a1 : q == 2u ? a2 : a3;
+    s = __builtin_amdgcn_sad_u16(de & ((1u << (8u * (e & 3u))) - 1u), 0u, s);
+    return s - low_bytes(h[0], (int)lead);
 }
 
 __device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
@@ -160,7 +202,7 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
             p.flags = NETCSUM_PKT_EXT_HDR;
             return p;
         }
-        const uint32_t d = pkt_dword_at(wd, lead, off);
+        const uint32_t d = pkt_dword_at<2>(h, lead, off);
         if (((d >> 16) & 0xFFu) > 2u && (d >> 24) != 0u) {
             p.flags = NETCSUM_PKT_EXT_HDR;
             return p;
@@ -199,7 +241,7 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
             p.flags = NETCSUM_PKT_L4_MALFORMED;
             return p;
         }
-        const uint32_t du = pkt_dword_at(wd, lead, off + 4u);
+        const uint32_t du = pkt_dword_at<2>(h, lead, off + 4u);
         if (be16(du, 0) != ulen) {
             p.flags = NETCSUM_PKT_L4_MALFORMED;
             return p;
@@ -225,7 +267,7 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
         if constexpr (TX) {
             p.check_l4 = true;
         } else {
-            const uint32_t type = pkt_dword_at(wd, lead, off) & 0xFFu;
+            const uint32_t type = pkt_dword_at<2>(h, lead, off) & 0xFFu;
             if (type == 1u || type == 3u || type == 4u) {
                 p.check_l4 = true;
                 nopseudo = true;                                 // message alone (net_icmpv6.c:2910-2920)
@@ -239,11 +281,17 @@ __device__ __forceinline__ LanePkt lane_parse6(const uint32_t (&wd)[24], const u
     }
     if (p.check_l4) {
         p.end = tot;
-        const uint32_t s_off = win_prefix(h, lead, off);
-        p.ip_sum = nopseudo ? s_off : s_off - (win_prefix(h, lead, 40u) - win_prefix(h, lead, 8u));
+        if (off == 40u && !nopseudo) {
+            // the bytes before the addresses: the fixed header's first 8 B, from d0 / d1
+            const uint32_t sel = pkt_frame_sel(odd);
+            p.ip_sum = frame_sum(d0, sel, frame_sum(d1, sel, 0u));
+        } else {                                                 // walked routing headers / ICMPv6 errors
+            const uint32_t s_off = win_prefix(h, lead, off);
+            p.ip_sum = nopseudo ? s_off : s_off - (win_prefix(h, lead, 40u) - win_prefix(h, lead, 8u));
+        }
         p.pseudo_le = nopseudo ? 0u : pseudo;
         if constexpr (TX) {
-            const uint32_t fd = pkt_dword_at(wd, lead, p.l4_csum_off);
+            const uint32_t fd = pkt_dword_at<2>(h, lead, p.l4_csum_off);
             p.l4_field = field_le(fd & 0xFFu, (fd >> 8) & 0xFFu, odd);
         }
     }
@@ -271,13 +319,19 @@ __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u3
         p.malformed = true;
         return p;                                                // end 0: nothing summed
     }
-    // exact sum of the IP header [0, hlen) from the window (lead + hlen <= 75 < 96)
-    uint32_t s = 0u - low_bytes(h[0], (int)lead);
+    // exact sum of the IP header [0, hlen): the 20-B base header from d0..d4; with options, from the
+    // window (lead + hlen <= 75 < 96)
+    if (hlen == 20u) {
+        const uint32_t sel = pkt_frame_sel(odd);
+        p.ip_sum = frame_sum(d0, sel, frame_sum(d1, sel, frame_sum(d2, sel, frame_sum(d3, sel, frame_sum(d4, sel, 0u)))));
+    } else {
+        uint32_t s = 0u - low_bytes(h[0], (int)lead);
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-        s += low_bytes(h[c], min(max((int)(lead + hlen) - 16 * c, 0), 16));
+        for (int c = 0; c < 5; ++c) {
+            s += low_bytes(h[c], min(max((int)(lead + hlen) - 16 * c, 0), 16));
+        }
+        p.ip_sum = s;
     }
-    p.ip_sum = s;
     p.fields = TX ? field_le((d2 >> 16) & 0xFFu, d2 >> 24, odd) : 0u;   // IP checksum field, offset 10
     p.end = hlen;
     if (frag != 0u) {
@@ -287,7 +341,7 @@ __device__ __forceinline__ LanePkt lane_parse(const uint32_t (&wd)[24], const u3
     const uint32_t l4len = tot - hlen;
     const uint32_t src_dst = __builtin_amdgcn_sad_u16(d3, 0u, __builtin_amdgcn_sad_u16(d4, 0u, 0u));
     const uint32_t fo = p.proto == 17u ? hlen + 4u : (p.proto == 6u ? hlen + 16u : hlen + 2u);
-    const uint32_t fd = pkt_dword_at(wd, lead, fo);              // UDP: len | csum; TCP / ICMP / IGMP: csum
+    const uint32_t fd = pkt_dword_at<1>(h, lead, fo);              // UDP: len | csum; TCP / ICMP / IGMP: csum
     switch (p.proto) {
     case 6u:
         if (l4len < 20u) {
@@ -426,7 +480,6 @@ template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
 __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec, uint32_t w, uint32_t lane,
                                         uint32_t s_begin, uint32_t nres, uintptr_t O, uint32_t prel, uint32_t avail,
                                         uint32_t span) {
-    const uint32_t s_end = s_begin + nres;
     const uint32_t st = (uint32_t)A.stride;
     const uint32_t lead0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)prel);
     const uint32_t npieces = (span + 1023u) >> 10;
@@ -459,11 +512,21 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
     }
     const bool odd = (prel & 1u) != 0u;                        // O is 128-B aligned
     const LanePkt pk = lane_parse_ver<VER, TX>(wd, h, plead, avail, odd, A.udp_tx_csum);
+    const uint32_t end_v = mine ? pk.end : 0u;
+    // Live forms: datagrams whose summed bytes lie inside the lane's window (40-B ACKs; nothing to
+    // sum) are summed here from the window: the stream neither marks their sectors nor walks their
+    // events. (Form 0, the packed layouts, keeps every datagram in the stream: enabled there, the
+    // window sum raised the VGPR count of the IPv6 offset/length kernels, which inline form 0.)
+    const bool inwin = BND >= 1 ? plead + end_v <= 96u : end_v == 0u;
+    uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k
+    if (BND >= 1 && mine && inwin && end_v != 0u) {
+        tot_v = win_range_sum(h, plead, end_v);
+    }
+    uint64_t srest = __builtin_amdgcn_ballot_w64(mine && !inwin);   // the stream's packets (lanes)
     // Row touch (off by default here: the header loads above already touch every datagram) issued
     // after the parse, when the window's registers are free (issued before it, its two VGPRs raised
     // the prologue's peak to 73 = 6 waves/SIMD).
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);
-    const uint32_t end_v = mine ? pk.end : 0u;
     uint64_t lm0 = 0u;                                         // live pieces of the run (<= 64)
     uint32_t pm0 = 0u;                                         // sector mask of piece `lane`
     uint32_t nlive = npieces;
@@ -474,7 +537,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             sect[lane] = 0u;
         }
         __builtin_amdgcn_wave_barrier();
-        if (end_v != 0u) {
+        if (!inwin) {
             const uint32_t s0 = prel >> 6, s1 = (prel + end_v - 1u) >> 6;
             for (uint32_t d = s0 >> 5; d <= (s1 >> 5); ++d) {
                 const uint32_t lo = max(s0, d << 5) - (d << 5), hi = min(s1, (d << 5) + 31u) - (d << 5);
@@ -513,10 +576,20 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         }
     }
 
-    uint32_t tot_v = 0u;                                       // packet k's [start, end) sum: lane k
-    uint32_t cur = s_begin;                                    // next packet to finish
-    uint32_t cs = lead0;                                       // its start / end, run-relative
-    uint32_t ce = lead0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)end_v);
+    // The stream's next packet to finish (its lane; srest: the later ones) and its start / end,
+    // run-relative; none: kDone.
+    auto start_of = [&](uint32_t k) -> uint32_t {
+        if constexpr (VL) {
+            return (uint32_t)__builtin_amdgcn_readlane((int)prel, (int)k);
+        } else {
+            return lead0 + k * st;
+        }
+    };
+    const bool any = srest != 0u;
+    uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
+    srest &= srest - 1u;
+    uint32_t cs = start_of(cur);
+    uint32_t ce = any ? cs + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)cur) : kDone;
     uint32_t acc = 0u;
 
     // General walk of seg_stream_kernel with per-packet ends (state written back unconditionally).
@@ -527,6 +600,7 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
         const uint32_t pend = qb + 1024u;
         const uint32_t full = sum4(v, 0u);
         uint32_t u = cur, c = cs, e = ce, a = acc, t = tot_v;
+        uint64_t rs = srest;
         if (e > pend) {                                        // no packet ends in this piece
             a += (c <= qb) ? full : full - piece_prefix_t(v, full, lane16, min(c - qb, 1024u));
         } else {
@@ -535,21 +609,20 @@ __device__ __forceinline__ void pkt_run(const PktBatchArgs& A, PktTxRecord* rec,
             do {
                 const uint32_t Pe = piece_prefix_t(v, full, lane16, e <= qb ? 0u : e - qb);
                 const uint32_t T = wave_total(a + (Pe - Ps));
-                t = (lane == u - s_begin) ? T : t;
+                t = (lane == u) ? T : t;
                 a = 0u;
-                ++u;
-                if constexpr (VL) {
-                    c = (uint32_t)__builtin_amdgcn_readlane((int)prel, (int)min(u - s_begin, 63u));
-                } else {
-                    c += st;
-                }
+                const bool more = rs != 0u;
+                u = more ? (uint32_t)__builtin_ctzll(rs) : 63u;
+                rs &= rs - 1u;
+                c = start_of(u);
                 const bool adj = c == e;                       // dense: the next packet starts at this end
-                e = u < s_end ? c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)(u - s_begin)) : kDone;
+                e = more ? c + (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)u) : kDone;
                 Ps = adj ? Pe : piece_prefix_t(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
             } while (e <= pend);
             a = full - Ps;
         }
         cur = u;
+        srest = rs;
         cs = c;
         ce = e;
         acc = a;
