@@ -65,12 +65,15 @@ def main():
         netcsum.tx_finalize_ipv4(r["base"], n, None, stream=st, **strided)
         torch.cuda.synchronize()
         ref = r["buf"].clone()
-        # (tag, bound, datagrams per run, form, pieces in flight); RING_VARIANTS=dN selects the D=8 set
+        # (tag, bound, datagrams per run, form, pieces in flight); RING_VARIANTS=d8 selects the D=8 set,
+        # RING_VARIANTS=runs a sweep of run lengths
         if os.environ.get("RING_VARIANTS") == "d8":
             variants = [("strided.b0", 0, -1, strided, 4), ("strided.b2", 2, -1, strided, 4),
                         ("strided.b2.d8", 2, -1, strided, 8), ("strided.b3.d8", 3, -1, strided, 8),
                         ("strided.b2.s32.d8", 2, 32, strided, 8), ("offlen", -1, -1, desc, 4),
                         ("offlen.d8", -1, -1, desc, 8)]
+        elif os.environ.get("RING_VARIANTS") == "runs":                 # run lengths of the default form
+            variants = [("strided.b2.s%d" % s, 2, s, strided, 4) for s in (8, 12, 16, 20, 24, 28, 32)]
         else:
             variants = [("strided.b0", 0, -1, strided, 4), ("strided.b1", 1, -1, strided, 4),
                         ("strided.b2", 2, -1, strided, 4), ("strided.b3", 3, -1, strided, 4),
