@@ -72,15 +72,39 @@ def parse():
     ap.add_argument("--tune", action="append", default=[], help="key=value launch tuning (grid/group/nt/block/kernel/chunks/tile/mult/xcd/touch/waves)")
     ap.add_argument("--no-c5-point", action="store_true",
                     help="N=1: skip the same-workload retention point (the C5 16 M-segment shard on this GPU)")
-    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+    # below the driver's own 600-s limit on a bench run, so that a hung rank is named by the launcher
+    # (with its last stage marker) before the driver kills the whole run
+    ap.add_argument("--launch-timeout", type=float, default=540.0,
                     help="launcher (--gpus N > 1 without WORLD_SIZE): seconds before the rank processes are killed")
     # CPU test of the launcher only: each rank prints its rendezvous environment and exits before any
-    # torch import ("ok"), or rank 1 exits 3 ("fail1"); tests/test_bench_launch_cpu.py
-    ap.add_argument("--launcher-selftest", choices=["ok", "fail1"], default=None, help=argparse.SUPPRESS)
+    # torch import ("ok"), rank 1 exits 3 ("fail1"), or rank 1 stops after its "process group up" marker
+    # while rank 0 waits in the timed region's closing barrier ("hang1"); tests/test_bench_launch_cpu.py
+    ap.add_argument("--launcher-selftest", choices=["ok", "fail1", "hang1"], default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+STAGE_TAG = "bench-stage"
+STAGES = ("start", "torch imported", "process group up", "shard generated", "warm-up done", "timed region done",
+          "reported")
+_T_START = time.monotonic()
+
+
+def stage(name):
+    """A rank's progress marker on stderr (one line, flushed): the launcher names the last one a hung or
+    failed rank reached. Stages: start, torch imported, process group up, shard generated, warm-up
+    done, timed region done, reported."""
+    print(f"{STAGE_TAG} rank={os.environ.get('RANK', '0')} stage={name} t={time.monotonic() - _T_START:.1f}s",
+          file=sys.stderr, flush=True)
+
+
+def parse_stage(line):
+    """(rank, stage) of a stage-marker line, else None."""
+    if not line.startswith(STAGE_TAG + " "):
+        return None
+    f = dict(kv.split("=", 1) for kv in line[len(STAGE_TAG) + 1:].split(" ") if "=" in kv)
+    rest = line.split(" stage=", 1)[1].rsplit(" t=", 1)[0] if " stage=" in line else None
+    return (int(f["rank"]), rest) if "rank" in f and rest else None
 
 
 def rank_environments(n, port, base=None):
@@ -127,22 +151,60 @@ def launch_ranks(args):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     argv = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
-    procs, outs = [], []
+    procs, outs, errs = [], [], []
+    t0 = time.monotonic()
+    last = {}                                    # rank -> (stage, monotonic time the marker arrived)
     for r, env in enumerate(rank_environments(args.gpus, port)):
         f = tempfile.TemporaryFile(mode="w+")
         outs.append(f)
-        procs.append(subprocess.Popen(argv, env=env, stdout=f, start_new_session=True))
-    deadline = time.monotonic() + args.launch_timeout
+        ef = tempfile.NamedTemporaryFile(mode="w+", delete=False, prefix=f"bench_rank{r}_", suffix=".err")
+        errs.append([ef, 0, ""])                 # file, read offset, partial line
+        procs.append(subprocess.Popen(argv, env=env, stdout=f, stderr=ef, start_new_session=True))
+
+    def pump():
+        """Forward every rank's new stderr lines (live, prefixed) and note its stage markers."""
+        for r, e in enumerate(errs):
+            with open(e[0].name) as fh:
+                fh.seek(e[1])
+                chunk = fh.read()
+                e[1] = fh.tell()
+            text = e[2] + chunk
+            lines = text.split("\n")
+            e[2] = lines.pop()
+            for ln in lines:
+                st = parse_stage(ln)
+                if st is not None:
+                    last[r] = (st[1], time.monotonic())
+                print(f"[rank {r}] {ln}", file=sys.stderr, flush=True)
+
+    def stage_report():
+        now = time.monotonic()
+        return "; ".join(f"rank {r}: " + (f"last stage '{last[r][0]}' ({now - last[r][1]:.0f} s ago)" if r in last
+                                          else "no stage marker") + (" [still running]" if rc[r] is None else
+                                                                     f" [exit {rc[r]}]")
+                         for r in range(len(procs)))
+
+    deadline = t0 + args.launch_timeout
     rc = [None] * len(procs)
     failed = None
     while any(c is None for c in rc):
+        pump()
         for r, p in enumerate(procs):
             if rc[r] is None:
                 rc[r] = p.poll()
                 if rc[r] not in (None, 0) and failed is None:
-                    failed = f"rank {r} exited {rc[r]}"
+                    failed = f"rank {r} exited {rc[r]}" + (f" after stage '{last[r][0]}'" if r in last else "")
         if failed or time.monotonic() > deadline:
-            failed = failed or f"timeout after {args.launch_timeout:.0f} s"
+            if failed is None:
+                hung = [r for r in range(len(procs)) if rc[r] is None]
+                # the hung rank is the one furthest behind: the earliest stage in STAGES (or no marker at
+                # all); ranks ahead of it wait for it in a collective
+                order = sorted(hung, key=lambda r: (STAGES.index(last[r][0]) if r in last and last[r][0] in STAGES
+                                                    else -1, last[r][1] if r in last else -1.0))
+                failed = (f"timeout after {args.launch_timeout:.0f} s: rank {order[0]} hung"
+                          + (f" after stage '{last[order[0]][0]}'" if order[0] in last else " before its first stage marker")
+                          + f" ({len(hung)} rank(s) still running)")
+            report = stage_report()
             for r, p in enumerate(procs):        # end every rank's own process group, nothing else
                 if p.poll() is None:
                     try:
@@ -151,8 +213,15 @@ def launch_ranks(args):
                         pass
             for r, p in enumerate(procs):
                 rc[r] = p.wait()
+            print(f"bench.py launcher: {report}", file=sys.stderr, flush=True)
             break
         time.sleep(0.05)
+    pump()
+    for e in errs:
+        if e[2]:
+            print(e[2], file=sys.stderr, flush=True)
+        e[0].close()
+        os.unlink(e[0].name)
     line = None
     for r, f in enumerate(outs):
         f.seek(0)
@@ -181,6 +250,13 @@ def launcher_selftest(mode):
     if mode == "fail1" and rank == 1:
         print("selftest: rank 1 fails on purpose", file=sys.stderr, flush=True)
         return 3
+    if mode == "hang1":
+        stage("process group up")
+        if rank == 1:                            # e.g. stuck generating its shard
+            time.sleep(3600)
+        stage("shard generated")
+        stage("warm-up done")
+        time.sleep(3600)                         # rank 0: waits in the barrier for rank 1
     print(json.dumps({k: os.environ.get(k) for k in RANK_ENV}), flush=True)
     return 0
 
@@ -518,12 +594,14 @@ def main():
     args = parse()
     if world_check(args.gpus) == "launch":
         return launch_ranks(args)
+    stage("start")
     if args.launcher_selftest:
         return launcher_selftest(args.launcher_selftest)
     import torch
     import torch.distributed as dist
 
     import netcsum
+    stage("torch imported")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -546,6 +624,7 @@ def main():
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend=backend)
+        stage("process group up")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -564,6 +643,7 @@ def main():
     seg, ph = make_c2_shard(torch, netcsum, start, n, L, plen, dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
+    stage("shard generated")
 
     def step():
         netcsum.batch_strided(seg, L, L, ph, plen, plen, n, out, netcsum.OP_DATA_CALC, stream=stream)
@@ -579,6 +659,7 @@ def main():
         step()
     torch.cuda.synchronize()
     kernel_desc = "netcsum::" + netcsum.last_launch()
+    stage("warm-up done")
 
     # timed region: exactly K steps, barrier + synchronize on both sides, nothing else enqueued
     if world > 1:
@@ -591,6 +672,7 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    stage("timed region done")
 
     # roofline pass (untimed for `value`): HIP events on the launch stream around each of K launches
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -729,6 +811,7 @@ def main():
             except Exception as e:
                 line["c1_per_datagram"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
+    stage("reported")
 
     if world > 1:
         dist.destroy_process_group()

@@ -396,7 +396,9 @@ NET_ERR  NetUtil_MI355X_RxBurstTally       (const uint8_t   *h_action,
  * thread's resident burst server kernel reads them in place over PCIe and writes the results into
  * coherent pinned memory the call polls (NETCSUM_TUNE_BURST_ZERO_COPY; 1 frame ~7 us, 64 frames
  * ~11 us). The server stays resident until idle for NETCSUM_TUNE_BURST_SERVER_IDLE_US (500 us), so a
- * device-wide synchronisation right after a burst may wait up to that long.
+ * device-wide synchronisation right after a burst may wait up to that long, and never longer than
+ * NETCSUM_TUNE_BURST_SERVER_LIFE_US (1000 us) per launch while bursts keep coming: work on other
+ * streams that share the server's hardware queue waits at most that long plus one burst.
  * ============================================================================================ */
 NET_ERR  NetUtil_MI355X_ChkSumBatchVarLenHost(const void      *h_base,
                                               const uint64_t  *h_seg_off,
@@ -677,9 +679,13 @@ typedef enum netcsum_tune_key {
                                          host polls them; 1 = a completion kernel copies the results out
                                          and stores a completion word the host polls; 0 = the copy
                                          pipeline (H2D, kernel, D2H, stream synchronisation)            */
-    NETCSUM_TUNE_BURST_SERVER_IDLE_US = 23 /* mode 3: microseconds without a burst after which the server
+    NETCSUM_TUNE_BURST_SERVER_IDLE_US = 23,/* mode 3: microseconds without a burst after which the server
                                          stops (the next burst relaunches it); a device-wide
                                          synchronisation waits up to this long. 1..1000000, default 500 */
+    NETCSUM_TUNE_BURST_SERVER_LIFE_US = 24 /* mode 3: microseconds one server launch stays resident even
+                                         while bursts keep coming (kernels of other streams sharing its
+                                         hardware queue wait behind it at most this long plus one
+                                         burst); the next burst relaunches it. 1..1000000, default 1000 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

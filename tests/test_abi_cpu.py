@@ -110,10 +110,12 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(24, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(25, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_ZERO_COPY, 4) == 219       # 0..3
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 0) == 219  # 1..10^6
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500) == 200
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 0) == 219  # 1..10^6
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 1000) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, 4) == 219             # -1..3
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, -1) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_VARLEN_RUN_BYTES, -2) == 219     # -1 .. 2^20

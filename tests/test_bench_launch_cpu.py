@@ -37,7 +37,7 @@ def test_launcher_starts_n_ranks_with_their_environment(n):
     assert len(lines) == 1, r.stdout                      # the contract: rank 0's ONE JSON line
     envs = {0: json.loads(lines[0])}
     for ln in r.stderr.splitlines():
-        if ln.startswith("[rank "):
+        if ln.startswith("[rank ") and ln[ln.index("]") + 2:].startswith("{"):
             rk = int(ln[len("[rank "):ln.index("]")])
             envs[rk] = json.loads(ln[ln.index("]") + 2:])
     assert sorted(envs) == list(range(n))
@@ -52,8 +52,38 @@ def test_launcher_starts_n_ranks_with_their_environment(n):
 def test_launcher_fails_when_a_rank_fails():
     r = _run(["--gpus", "3", "--launcher-selftest", "fail1"])
     assert r.returncode != 0
-    assert "rank 1 exited 3" in r.stderr
+    assert "rank 1 exited 3 after stage 'start'" in r.stderr
     assert r.stdout.strip() == ""                          # no JSON line from a failed world
+
+
+def test_launcher_names_a_hung_rank_and_its_last_stage():
+    """a rank that hangs (here rank 1 after "process group up", while rank 0 waits
+    in the closing barrier) is killed at --launch-timeout — by default below the driver's 600-s limit —
+    and named with the last stage marker it printed; the launcher exits non-zero with no JSON line,
+    and every rank's markers were forwarded to stderr as they arrived."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "2", "--launcher-selftest", "hang1", "--launch-timeout", "4"])
+    assert time.monotonic() - t0 < 60
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert "timeout after 4 s: rank 1 hung after stage 'process group up'" in r.stderr, r.stderr
+    assert "rank 0: last stage 'warm-up done'" in r.stderr and "[still running]" in r.stderr, r.stderr
+    assert "[rank 1] bench-stage rank=1 stage=process group up" in r.stderr, r.stderr
+    b = _bench_module()
+    assert b.parse_stage("bench-stage rank=3 stage=timed region done t=12.5s") == (3, "timed region done")
+    assert b.parse_stage("something else") is None
+
+
+def test_launch_timeout_default_is_below_the_drivers_limit():
+    import argparse
+    import sys as _sys
+    b = _bench_module()
+    argv, _sys.argv = _sys.argv, ["bench.py"]
+    try:
+        args = b.parse()
+    finally:
+        _sys.argv = argv
+    assert isinstance(args, argparse.Namespace) and 0 < args.launch_timeout < 600
 
 
 @pytest.mark.parametrize("ws,gpus", [("2", 4), ("1", 8), ("8", 1)])

@@ -1,0 +1,154 @@
+"""The resident burst server shares a hardware queue with other streams.
+
+HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 on the MI355X boxes) and a
+kernel waits behind the kernels ahead of it on its queue. The burst server (TUNE_BURST_ZERO_COPY 3,
+netcsum_pktstream.hip burst_server_kernel) is a kernel that stays resident while its thread keeps
+posting bursts, so work on any stream sharing its queue — batches on the caller's streams, another
+thread's own burst server — waits behind it. Each server launch is therefore bounded
+(TUNE_BURST_SERVER_LIFE_US, default 1000 us; the blocks stop together, the next burst relaunches it).
+
+Thread A posts 64-frame RxBurstHost bursts back to back for ~1.5 s with an idle limit of 100 ms, so
+its server never stops for lack of work; meanwhile thread B runs, on each of 12 streams (more than
+the 4 hardware queues, so several share A's queue), a device-resident ChkSumBatchStrided followed by
+a synchronisation of that stream, then an RxBurstHost of its own (B's own server). Every B call
+returns within 10 ms and every result of both threads equals the oracle's. With
+NETCSUM_BURST_SERVER_RECORD set, the latencies are written there as one JSON line.
+"""
+import json
+import os
+import random
+import statistics
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import netcsum
+import oracle
+import oracle_packets as op
+from packets import KINDS, KINDS6, make_packet, make_packet_v6
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+B_BOUND_S = 0.010          # every one of B's calls, batch + stream sync or a burst
+
+
+def _ring(seed, n, stride=1520, lead=14):
+    rng = random.Random(seed)
+    buf = np.frombuffer(rng.randbytes(n * stride), np.uint8).copy()
+    for i in range(n):
+        p = (make_packet(rng, rng.choice(KINDS), payload=rng.randint(0, 1400)) if i % 2 else
+             make_packet_v6(rng, rng.choice(KINDS6), payload=rng.randint(0, 1400)))[:stride - lead]
+        buf[i * stride + lead:i * stride + lead + len(p)] = np.frombuffer(p, np.uint8)
+    want = np.array([op.rx_validate_ip(bytes(buf[i * stride + lead:(i + 1) * stride])) for i in range(n)], np.uint8)
+    return torch.from_numpy(buf).pin_memory(), want, stride, lead
+
+
+def test_busy_burst_server_does_not_starve_streams_sharing_its_queue():
+    old_switch = sys.getswitchinterval()
+    sys.setswitchinterval(1e-4)                       # the threads' Python glue, not the GPU, is timed
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    n_frames = 64
+    a_ring, a_want, stride, lead = _ring(11, n_frames)
+    b_ring, b_want, _, _ = _ring(12, n_frames)
+    # B's device-resident batch: 4096 x 1500-B segments + 12-B pseudo-headers
+    rng = np.random.default_rng(5)
+    n_seg, L = 4096, 1500
+    seg = rng.integers(0, 256, size=n_seg * L, dtype=np.uint8)
+    ph = rng.integers(0, 256, size=n_seg * 12, dtype=np.uint8)
+    seg_want = oracle.batch_strided(seg, L, L, ph, 12, 12, n_seg, oracle.OP_DATA_CALC)
+    seg_d, ph_d = torch.from_numpy(seg).to(dev), torch.from_numpy(ph).to(dev)
+    torch.cuda.synchronize()
+
+    a_run_s = 1.5
+    a_lat, a_bad, a_err, a_paths = [], [], [], set()
+    a_started = threading.Event()
+
+    def thread_a():
+        try:
+            torch.cuda.set_device(dev)
+            netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
+            netcsum.tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 100000)   # never idle out: only the life limit
+            fl = np.zeros(n_frames, np.uint8)
+            t_end = time.perf_counter() + a_run_s
+            k = 0
+            while time.perf_counter() < t_end:
+                t = time.perf_counter()
+                netcsum.rx_validate_ip_host(a_ring[lead:], n_frames, fl, stride=stride, pkt_len=stride - lead)
+                a_lat.append(time.perf_counter() - t)
+                a_paths.add(netcsum.last_launch().split(" ")[0])
+                if not np.array_equal(fl, a_want):
+                    a_bad.append(k)
+                k += 1
+                if k == 20:
+                    a_started.set()
+        except Exception as e:                    # noqa: BLE001
+            a_err.append(repr(e))
+        finally:
+            a_started.set()
+            netcsum.tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500)
+            netcsum.thread_release()
+
+    b_batch, b_burst, b_bad = [], [], []
+    b_paths = set()
+    # B's streams and its own burst server exist before A starts: a stream's first launch (its queue's
+    # setup) is not what is measured
+    streams = [torch.cuda.Stream(device=dev) for _ in range(12)]
+    outs = [torch.empty(n_seg, dtype=torch.int16, device=dev) for _ in streams]
+    fl = np.zeros(n_frames, np.uint8)
+    for s, o in zip(streams, outs):
+        netcsum.batch_strided(seg_d, L, L, ph_d, 12, 12, n_seg, o, netcsum.OP_DATA_CALC, stream=s)
+    netcsum.rx_validate_ip_host(b_ring[lead:], n_frames, fl, stride=stride, pkt_len=stride - lead)
+    torch.cuda.synchronize()
+    th = threading.Thread(target=thread_a)
+    th.start()
+    try:
+        assert a_started.wait(30)
+        t_end = time.perf_counter() + a_run_s * 0.6
+        rounds = 0
+        while time.perf_counter() < t_end and th.is_alive():
+            for s, o in zip(streams, outs):
+                t = time.perf_counter()
+                netcsum.batch_strided(seg_d, L, L, ph_d, 12, 12, n_seg, o, netcsum.OP_DATA_CALC, stream=s)
+                s.synchronize()
+                b_batch.append(time.perf_counter() - t)
+                t = time.perf_counter()
+                netcsum.rx_validate_ip_host(b_ring[lead:], n_frames, fl, stride=stride, pkt_len=stride - lead)
+                b_burst.append(time.perf_counter() - t)
+                b_paths.add(netcsum.last_launch().split(" ")[0])
+                if not np.array_equal(fl, b_want):
+                    b_bad.append(("burst", rounds))
+            for j, o in enumerate(outs):
+                if not np.array_equal(o.cpu().numpy().view(np.uint16), seg_want):
+                    b_bad.append(("batch", rounds, j))
+            rounds += 1
+        a_alive_after_b = th.is_alive()
+    finally:
+        th.join(60)
+        sys.setswitchinterval(old_switch)
+        netcsum.thread_release()
+    rec = {"a_bursts": len(a_lat), "a_max_ms": round(max(a_lat) * 1e3, 3) if a_lat else None,
+           "a_median_us": round(statistics.median(a_lat) * 1e6, 2) if a_lat else None,
+           "b_calls": len(b_batch), "b_rounds": rounds,
+           "b_batch_max_ms": round(max(b_batch) * 1e3, 3) if b_batch else None,
+           "b_batch_median_us": round(statistics.median(b_batch) * 1e6, 2) if b_batch else None,
+           "b_burst_max_ms": round(max(b_burst) * 1e3, 3) if b_burst else None,
+           "b_burst_median_us": round(statistics.median(b_burst) * 1e6, 2) if b_burst else None,
+           "b_p99_ms": round(float(np.percentile(b_batch + b_burst, 99)) * 1e3, 3) if b_batch else None,
+           "b_over_bound": sum(x > B_BOUND_S for x in b_batch + b_burst), "bound_ms": B_BOUND_S * 1e3,
+           "a_paths": sorted(a_paths), "b_paths": sorted(b_paths), "lib": os.path.basename(netcsum.LIB_PATH)}
+    print(json.dumps(rec))
+    path = os.environ.get("NETCSUM_BURST_SERVER_RECORD")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    assert not a_err, a_err
+    assert a_paths == {"burst_server_kernel"} and b_paths == {"burst_server_kernel"}, rec
+    assert a_alive_after_b, "thread A must keep its server busy for the whole of B's phase"
+    assert not a_bad and not b_bad, (a_bad[:5], b_bad[:5])
+    assert rounds >= 3, rec
+    assert rec["b_over_bound"] == 0, rec

@@ -267,16 +267,18 @@ def test_rx_burst_host_zero_copy_many_calls_and_threads(zc):
 
 
 @pytest.mark.parametrize("n", [1, 3, 64, 500, 4096])
-@pytest.mark.parametrize("form", ["strided", "offlen"])
+@pytest.mark.parametrize("form", ["strided", "offlen", "sparse"])
 def test_tx_burst_host_zero_copy(n, form):
-    """TxBurstHost with n_chunks 0 on a pinned strided ring (the IPv4 header at +14 of 1520-B slots):
-    the checksum pass reads the ring in place and returns 8-B records that the host applies
-    (tx_burst_zero_copy); IPv6 datagrams behind a long Destination Options header (flag EXT_HDR) are
-    finished by the copy path. Same bytes and flags as the oracle and as the copy pipeline."""
+    """TxBurstHost with n_chunks 0 on a pinned ring (the IPv4 header at +14 of 1520-B slots, strided or
+    per-frame offset/length; sparse: +64 of 2048-B slots): the checksum pass reads the ring in place
+    and returns 8-B records that the host applies (tx_burst_zero_copy); IPv6 datagrams behind a long
+    Destination Options header (flag EXT_HDR) are finished by the copy path. Same bytes and flags as
+    the oracle and as the copy pipeline, and the zero-copy path (the server in mode 3) is the one
+    taken in every layout (round-4 advisor: offset/length and sparse Tx took the copy path)."""
     import struct
     from packets import ext_body
-    rng = random.Random(1300 + n)
-    stride, lead = 1520, 14
+    rng = random.Random(1300 + n + 7 * (form == "sparse"))
+    stride, lead = (2048, 64) if form == "sparse" else (1520, 14)
     pairs = []
     for i in range(n):
         if i % 7 == 3:
@@ -305,14 +307,21 @@ def test_tx_burst_host_zero_copy(n, form):
         try:
             hb = _pinned(buf)
             fl = np.zeros(n, np.uint8)
-            if form == "strided":
+            if form != "offlen":
                 netcsum.tx_burst_host(hb[lead:], n, fl, stride=stride, pkt_len=stride - lead)
             else:                                          # per-frame lengths (whole present bytes)
                 offs = np.arange(n, dtype=np.uint64) * stride + lead
                 lens = np.full(n, stride - lead, np.uint16)
                 netcsum.tx_burst_host(hb, n, fl, off=offs, lens=lens)
+            path = netcsum.last_launch()
         finally:
             netcsum.tune(netcsum.TUNE_BURST_ZERO_COPY, 3)
+        if zc == 3:
+            assert path.startswith("burst_server_kernel tx"), (zc, path)
+        elif zc in (1, 2):
+            assert "zero-copy" in path, (zc, path)
+        else:
+            assert "zero-copy" not in path, (zc, path)
         got = hb.numpy()
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (zc, [(int(j) // stride, int(j) % stride) for j in bad[:8]])

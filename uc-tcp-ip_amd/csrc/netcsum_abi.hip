@@ -35,6 +35,7 @@ thread_local netcsum::TuneKnob g_tune_grid_mult{1};
 thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 segments per group per block tile)
 thread_local netcsum::TuneKnob g_tune_burst_zc{3};              // host bursts: pinned rings read in place by the resident server
 thread_local netcsum::TuneKnob g_tune_burst_idle{500};           // resident burst server: idle microseconds before it stops
+thread_local netcsum::TuneKnob g_tune_burst_life{1000};          // resident burst server: microseconds of residency per launch
 thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
@@ -517,7 +518,7 @@ struct HostCtx {
         for (int j = 0; j < 3; ++j) {
             if (pstream[j]) (void)hipStreamSynchronize(pstream[j]);
         }
-        stop_server();
+        (void)stop_server(0);                     // (no limit: the server reads h_burst, freed below)
         if (sstream) (void)hipStreamDestroy(sstream);
         if (stream) (void)hipStreamDestroy(stream);
         if (h_stage) (void)hipHostFree(h_stage);
@@ -535,7 +536,7 @@ struct HostCtx {
         *this = HostCtx{};
     }
     ~HostCtx() { release(); }
-    void stop_server();
+    bool stop_server(int limit_ms);
 };
 
 thread_local HostCtx tls_ctx[kMaxDev];
@@ -1343,9 +1344,13 @@ static NET_ERR burst_poll(HostCtx& c, Ready ready, uint32_t n) {
 
 // ---- resident burst server (TUNE_BURST_ZERO_COPY 3; netcsum_pktstream.hip burst_server_kernel)
 // A launch per burst is most of a small burst's cost (launch, dispatch, then the kernel's PCIe round
-// trips). This context's server is launched once, on a stream of its own, and serves every burst
-// posted to it until it has been idle for TUNE_BURST_SERVER_IDLE_US (default 500 us: a device-wide
-// synchronisation waits at most that long for it after the last burst). Posting: the line's fields,
+// trips). This context's server is launched on a stream of its own and serves every burst posted to
+// it until it has been idle for TUNE_BURST_SERVER_IDLE_US (default 500 us: a device-wide
+// synchronisation waits at most that long for it after the last burst) or resident for
+// TUNE_BURST_SERVER_LIFE_US (default 1000 us) even while bursts keep coming: HIP maps the process's
+// streams onto GPU_MAX_HW_QUEUES hardware queues, and kernels of a stream sharing the server's queue
+// wait behind it, so each launch is bounded and the next burst relaunches it (one launch per ms of
+// continuous service). Posting: the line's fields,
 // then its burst number (a read that sees the new number with stale fields fails the check), a
 // full fence, then the blocks' closed marks — a block that closed may have missed the post
 // (Dekker's handshake, see the kernel), so the host waits the server out and relaunches it if the
@@ -1382,20 +1387,43 @@ static NET_ERR launch_server(HostCtx& c, uint64_t seq0) {
     a.len = reinterpret_cast<const uint16_t*>(c.h_burst_dev + kBurstLen);
     a.seq0 = seq0;
     a.idle_ticks = (uint64_t)std::max(1, g_tune_burst_idle.load()) * (uint64_t)std::max(khz, 1) / 1000u;
+    a.life_ticks = (uint64_t)std::max(1, g_tune_burst_life.load()) * (uint64_t)std::max(khz, 1) / 1000u;
     NC_HIP(netcsum::launch_burst_server(a, kServerBlocks, c.sstream));
     c.server_live = true;
     return NET_UTIL_ERR_NONE;
 }
 
-void HostCtx::stop_server() {
+// Waits for the server's stream for at most limit_ms (a stream query loop, never a blocking
+// synchronisation): a server launch queued behind other work on its hardware queue still ends, since
+// every launch of every server is bounded by its residency limit, but the caller's wait must not
+// depend on that. hipErrorNotReady when the stream is still busy at the deadline.
+static hipError_t server_stream_wait(hipStream_t s, int limit_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
+            return e;
+        }
+    }
+}
+
+// Posts the stop line and waits for the server: limit_ms 0 without limit (release(), which frees the
+// memory the server reads), else at most limit_ms; false if the server is still queued or running
+// then (server_live stays set: it will serve whatever is posted next, or stop).
+bool HostCtx::stop_server(int limit_ms) {
     if (server_live && sstream && h_burst) {
         netcsum::BurstPost p{};
         p.seq = netcsum::kBurstStop;
         p.check = netcsum::burst_post_check(p);
         write_post(*this, p);
-        (void)hipStreamSynchronize(sstream);
+        if (limit_ms <= 0) {
+            (void)hipStreamSynchronize(sstream);
+        } else if (server_stream_wait(sstream, limit_ms) == hipErrorNotReady) {
+            return false;
+        }
     }
     server_live = false;
+    return true;
 }
 
 template <class Ready>
@@ -1408,7 +1436,7 @@ static NET_ERR burst_server_run(HostCtx& c, netcsum::BurstPost p, Ready ready, u
         return true;
     };
     auto wait_out = [&](uint32_t from) -> NET_ERR {     // the server has stopped, or is stopping
-        NC_HIP(hipStreamSynchronize(c.sstream));
+        NC_HIP(server_stream_wait(c.sstream, 2000));    // (its blocks stop together, after one burst at most)
         c.server_live = false;
         return all_ready(from) ? NET_UTIL_ERR_NONE : launch_server(c, p.seq - 1u);
     };
@@ -1442,11 +1470,26 @@ static NET_ERR burst_server_run(HostCtx& c, netcsum::BurstPost p, Ready ready, u
             e = wait_out(i);
             if (e != NET_UTIL_ERR_NONE) return e;
         } else if (t - t0 > std::chrono::seconds(2)) {
-            c.stop_server();
+            if (!c.stop_server(2000)) return dev_fail("burst server still queued or running", hipErrorNotReady);
             if (!all_ready(i)) return dev_fail("burst server results", hipErrorUnknown);
         }
     }
     return NET_UTIL_ERR_NONE;
+}
+
+// NetUtil_MI355X_LastLaunch after a zero-copy burst: which path served it (the tests check that the
+// zero-copy path, not the copy pipeline, was taken)
+static void server_launch_name(uint32_t form, uint32_t spw, bool tx) {
+    char d[96];
+    snprintf(d, sizeof d, "burst_server_kernel %s form=%s pkts_per_wave=%u zero-copy", tx ? "tx" : "rx",
+             form == netcsum::kBurstWhole ? "whole" : form == netcsum::kBurstLive ? "live" : "offlen", spw);
+    netcsum::set_last_launch(d);
+}
+
+static void mark_zero_copy_launch(int zc) {
+    char d[200];
+    snprintf(d, sizeof d, "%s zero-copy%s", NetUtil_MI355X_LastLaunch(), zc == 1 ? " +burst_done_kernel" : "");
+    netcsum::set_last_launch(d);
 }
 
 // The server's form for a burst (BurstPost::form >> 1 and its run length), or false when the burst is
@@ -1519,6 +1562,7 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
         p.spw = spw;
         p.form = form << 1;
         p.rx_cfg = rx_cfg;
+        server_launch_name(form, spw, false);
         e = burst_server_run(c, p, [&](uint32_t i) { return *(volatile uint8_t*)(hf + i) != 0xFFu &&
                                                             *(volatile uint8_t*)(ha + i) != 0xFFu; }, n_pkt);
         if (e != NET_UTIL_ERR_NONE) return e;
@@ -1534,6 +1578,7 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, c.h_burst_dev + kBurstFlags, 1u, false, 0, c.stream,
                       c.h_burst_dev + kBurstAct, rx_cfg, nullptr, nullptr, kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
+        mark_zero_copy_launch(2);
         e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hf + i) != 0xFFu &&
                                                    *(volatile uint8_t*)(ha + i) != 0xFFu; }, n_pkt);
         if (e != NET_UTIL_ERR_NONE) return e;
@@ -1546,6 +1591,7 @@ static NET_ERR rx_burst_zero_copy(HostCtx& c, const void* h_base, const uint64_t
     e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, d_fl, 1u, false, 0, c.stream, d_act, rx_cfg, nullptr,
                   nullptr, kBurstBound);
     if (e != NET_UTIL_ERR_NONE) return e;
+    mark_zero_copy_launch(1);
     if (++c.seq == 0u) c.seq = 1u;
     const uint32_t tag = c.seq;
     *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
@@ -1579,7 +1625,12 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
     a.n = n_pkt;
     a.off = h_off;                                      // (only tested against nullptr here)
     a.len = h_len;
-    if (!netcsum::pkt_stream_supported(a, 0, g_tune_pkt_bound.load() < 0 ? 3 : g_tune_pkt_bound.load())) {
+    // the records come from the run-stream kernel only: the burst qualifies where pkt_batch picks it
+    // (the tuned bound, else the whole-span form 0 or the live-piece form 2), and the server's form
+    // where the server serves it (server_form: strided dense, sparse and offset/length rings)
+    const int tb = g_tune_pkt_bound.load();
+    if (!(tb >= 0 ? netcsum::pkt_stream_supported(a, 0, tb)
+                  : netcsum::pkt_stream_supported(a, 0, kBurstBound) || netcsum::pkt_stream_supported(a, 0, 2))) {
         return NET_UTIL_ERR_NONE;
     }
     uint64_t span = 0;
@@ -1615,6 +1666,7 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         p.spw = spw;
         p.form = (form << 1) | 1u;
         p.udp_mode = udp_mode;
+        server_launch_name(form, spw, true);
         e = burst_server_run(c, p, [&](uint32_t i) { return *(volatile uint8_t*)(hr + 8u * i + 7u) != 0xFFu; }, n_pkt);
         if (e != NET_UTIL_ERR_NONE) return e;
     } else if (zc >= 2) {                               // records straight into coherent memory, polled
@@ -1623,6 +1675,7 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
                       nullptr, reinterpret_cast<netcsum::PktTxRecord*>(c.h_burst_dev + kBurstRec), kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
+        mark_zero_copy_launch(2);
         e = burst_poll(c, [&](uint32_t i) { return *(volatile uint8_t*)(hr + 8u * i + 7u) != 0xFFu; }, n_pkt);
         if (e != NET_UTIL_ERR_NONE) return e;
     } else {
@@ -1630,6 +1683,7 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
         e = pkt_batch(d_ring, d_off, d_len, stride, pkt_len, n_pkt, nullptr, udp_mode, true, 0, c.stream, nullptr, 0u,
                       nullptr, d_rec, kBurstBound);
         if (e != NET_UTIL_ERR_NONE) return e;
+        mark_zero_copy_launch(1);
         if (++c.seq == 0u) c.seq = 1u;
         const uint32_t tag = c.seq;
         *reinterpret_cast<volatile unsigned long long*>(c.h_burst + kBurstWord) = 0ull;
@@ -1664,9 +1718,14 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
     if (!walk_off.empty()) {                            // the rare long IPv6 chains: the copy path
         const uint32_t m = (uint32_t)walk_off.size();
         std::vector<uint8_t> fl(m);
+        char zc_name[256];
+        snprintf(zc_name, sizeof zc_name, "%s", NetUtil_MI355X_LastLaunch());
         e = pkt_host_copy(h_base, walk_off.data(), walk_len.data(), 0, 0, m, h_flags ? fl.data() : nullptr, nullptr,
                           0u, udp_mode, true, 1u);
         if (e != NET_UTIL_ERR_NONE) return e;
+        char d[256];
+        snprintf(d, sizeof d, "%.180s +copy path for %u EXT_HDR datagrams", zc_name, m);
+        netcsum::set_last_launch(d);
         if (h_flags) {
             for (uint32_t k = 0; k < m; ++k) h_flags[walk_idx[k]] = fl[k];
         }
@@ -1949,6 +2008,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_BURST_SERVER_IDLE_US:
         if (value < 1 || value > 1000000) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_burst_idle.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_BURST_SERVER_LIFE_US:
+        if (value < 1 || value > 1000000) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_burst_life.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
         if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

@@ -216,6 +216,9 @@ struct BurstServerArgs {
     const uint16_t*     len;
     uint64_t            seq0;      // the last burst number already served
     uint64_t            idle_ticks;   // wall-clock ticks without a post after which a block stops
+    uint64_t            life_ticks;   // wall-clock ticks after the block's start after which it stops
+                                      // even while bursts keep coming (bounds how long the server holds
+                                      // the hardware queue its stream shares with other streams)
 };
 // blocks x 256 threads on stream s (a stream of its own: the kernel runs until it is idle)
 hipError_t launch_burst_server(const BurstServerArgs& a, int blocks, hipStream_t s);

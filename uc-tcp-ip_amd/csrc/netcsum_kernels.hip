@@ -958,7 +958,7 @@ static hipError_t launch_tile_dispatch(const SegBatchArgs& a, const LaunchCfg& c
     return hipErrorInvalidValue;
 }
 
-thread_local char g_last_launch[160];
+thread_local char g_last_launch[256];
 
 const char* last_launch() {
     return g_last_launch;

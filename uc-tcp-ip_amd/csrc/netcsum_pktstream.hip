@@ -899,21 +899,31 @@ __global__ void __launch_bounds__(64) burst_done_kernel(const uint8_t* fl, const
 // line of coherent host memory read as a whole (one request: its check catches a read that tore it),
 // and hands a burst it has not served to its block through LDS; the block's 4 waves then take runs
 // blockIdx * 4 + w, + 4 * blocks, ... of the burst with the run-stream code above (mixed IPv4 / IPv6,
-// 4 pieces in flight), write the results into coherent host memory and release them. A block idle for
-// idle_ticks stops (Dekker's handshake with the host: it marks itself closed, fences, and reads the
-// line once more; the host posts, fences and reads the marks, so a burst posted meanwhile is taken
-// here or found by the host, which waits the server out and relaunches it when the burst is unserved).
+// 4 pieces in flight), write the results into coherent host memory and release them. A block stops
+// when it has been idle for idle_ticks, when life_ticks have passed since it started (even while
+// bursts keep coming: the server's stream shares a hardware queue with other streams of the process,
+// GPU_MAX_HW_QUEUES, and their kernels wait behind it), or when it sees another block's closed mark
+// (the marks are read with the post line, so the blocks stop together and the host, which waits for
+// the whole grid, waits for one burst at most). Stopping is Dekker's handshake with the host: the
+// block marks itself closed, fences, and reads the line once more; the host posts, fences and reads
+// the marks, so a burst posted meanwhile is taken here or found by the host, which waits the server
+// out and relaunches it when the burst is unserved.
 constexpr uint32_t kServeRun = 1u, kServeExit = 2u;
 
-__device__ uint32_t burst_leader_wait(const BurstServerArgs& S, uint64_t seen, uint32_t lane, uint32_t* s_line) {
+__device__ uint32_t burst_leader_wait(const BurstServerArgs& S, uint64_t seen, uint64_t t_start, uint32_t lane,
+                                      uint32_t* s_line) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t nb = gridDim.x;
     bool closing = false;
     for (;;) {
         uint64_t v = 0u;
         if (lane < 8u) {                                        // lanes 0..7: the line's 8 quadwords
             v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(S.post) + lane, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (lane < 8u + nb) {                            // lanes 8..: every block's closed mark
+            v = __hip_atomic_load(S.closed + (lane - 8u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        const bool others_closed = __ballot(lane >= 8u && lane < 8u + nb && v != 0u) != 0u;
         uint32_t d[12];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -936,12 +946,14 @@ __device__ uint32_t burst_leader_wait(const BurstServerArgs& S, uint64_t seen, u
                 s_line[2u * lane] = (uint32_t)v;
                 s_line[2u * lane + 1u] = (uint32_t)(v >> 32);
             }
-            return p.seq == kBurstStop ? kServeExit : closing ? (kServeRun | kServeExit) : kServeRun;
+            return p.seq == kBurstStop ? kServeExit
+                   : (closing || others_closed) ? (kServeRun | kServeExit) : kServeRun;
         }
         if (closing) {
             return kServeExit;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > S.idle_ticks) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (others_closed || now - t0 > S.idle_ticks || now - t_start > S.life_ticks) {
             closing = true;
             if (lane == 0u) {
                 __hip_atomic_store(S.closed + blockIdx.x, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -967,10 +979,11 @@ __global__ void __launch_bounds__(256) burst_server_kernel(BurstServerArgs S) {
     __shared__ uint32_t s_cmd;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint64_t seen = S.seq0;
     for (;;) {
         if (w == 0u) {
-            const uint32_t cmd = burst_leader_wait(S, seen, lane, s_line);
+            const uint32_t cmd = burst_leader_wait(S, seen, t_start, lane, s_line);
             if (lane == 0u) {
                 s_cmd = cmd;
             }
@@ -1115,8 +1128,8 @@ void set_tx_flush(int mode) {
 }
 
 // Strided batches of >= 64-B packets (IPv4, IPv6 or mixed) whose runs span < 2^31 bytes: any gap
-// between slots in the live-piece form (bound 3), at most 64 B in the others; offset/length batches
-// in the live-piece form.
+// between slots in the live-piece forms of bounds 1 and 2, at most 64 B in the others (bound 0, and
+// bound 3, which loads a run's first pieces whole); offset/length batches in bounds 1 and 2.
 bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (!(ip_ver == 4 || ip_ver == 6 || ip_ver == 0)) return false;
     if (a.off != nullptr) return (bound == 1 || bound == 2) && a.len != nullptr;

@@ -71,6 +71,7 @@ TUNE_VARLEN_RUN_BYTES = 20
 TUNE_PKT_BOUND = 21
 TUNE_BURST_ZERO_COPY = 22
 TUNE_BURST_SERVER_IDLE_US = 23
+TUNE_BURST_SERVER_LIFE_US = 24
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
