@@ -667,9 +667,15 @@ typedef enum netcsum_tune_key {
                                          parse first; 2 = live pieces with the run's first piece loaded
                                          during the parse; 3 = live pieces with the run's first 4 (8)
                                          pieces loaded during the parse (dense strided layouts);
-                                         -1 = the default: 0 for packed batches (stride == pkt_len), 3 for
-                                         other dense strided ones, 2 for sparse strided and offset/length
-                                         batches                                                     */
+                                         4 = ring plans (strided batches that are not packed): each launch
+                                         samples 1024 of its datagrams on the device (one extra block)
+                                         and leaves the form and run length for the next batch on the
+                                         same ring (base, stride, pkt_len, count, IP version): form 0
+                                         when the datagrams fill their slots, else live pieces in runs
+                                         of 8 / 16 / 32 by the bytes they stream; a ring's first batch
+                                         runs as 2; -1 = the default: 0 for packed batches (stride ==
+                                         pkt_len), 4 for other strided batches of >= 16 Ki datagrams, 2
+                                         for smaller ones and offset/length batches                  */
     NETCSUM_TUNE_BURST_ZERO_COPY = 22,/* host-memory packet batches with n_chunks 0 of <= 4096 frames whose
                                          ring is pinned host memory: the kernel reads the ring in place;
                                          3 (default) = a resident server kernel (one per calling thread,

@@ -116,7 +116,7 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 0) == 219  # 1..10^6
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 1000) == 200
-    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, 4) == 219             # -1..3
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, 5) == 219             # -1..4
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, -1) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_VARLEN_RUN_BYTES, -2) == 219     # -1 .. 2^20
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_HDR_BURST, 2) == 219             # 0 or 1

@@ -97,7 +97,7 @@ def _check(got, want, what):
     assert bad.size == 0, (what, [(int(i), int(got[i]), int(want[i])) for i in bad[:6]])
 
 
-@pytest.mark.parametrize("bound", [0, 1, 2, 3])
+@pytest.mark.parametrize("bound", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("slot,lead", [(1520, 14), (2048, 64), (1536, 1), (9216, 2)])
 @pytest.mark.parametrize("passes", [1, 2])
 def test_strided_ring_every_bound_vs_oracle(bound, slot, lead, passes):
@@ -312,3 +312,95 @@ def test_datagrams_past_the_bitmap_reach(form, bound):
     torch.cuda.synchronize()
     _check(b.cpu().numpy(), want[1], "tx bytes")
     _check(ft.cpu().numpy(), want[2], "tx flags")
+
+
+def _np_ring(n, slot, lead, sizes, seed, v6_every=0):
+    """A ring of n IPv4 TCP / UDP datagrams of the given sizes (numpy-built: the plan needs batches
+    of >= 64 Ki frames for its longest runs); every 3rd datagram UDP, headers well-formed, checksum
+    fields random (Rx flags then vary), the rest random bytes. v6_every k: every k-th frame IPv6."""
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 256, size=n * slot + 64, dtype=np.uint8)
+    v = buf[: n * slot].reshape(n, slot)
+    udp = (np.arange(n) % 3) == 1
+    h = v[:, lead:lead + 40]
+    h[:, 0], h[:, 1], h[:, 2], h[:, 3] = 0x45, 0, sizes >> 8, sizes & 0xFF
+    h[:, 6], h[:, 7], h[:, 8], h[:, 9] = 0x40, 0, 64, np.where(udp, 17, 6)
+    h[:, 24] = np.where(udp, (sizes - 20) >> 8, h[:, 24])
+    h[:, 25] = np.where(udp, (sizes - 20) & 0xFF, h[:, 25])
+    h[:, 32] = np.where(udp, h[:, 32], 0x50)
+    if v6_every:
+        k = np.arange(n) % v6_every == 0
+        pl = sizes - 40
+        h[k, 0], h[k, 1], h[k, 2], h[k, 3] = 0x60, 0, 0, 0
+        h[k, 4], h[k, 5], h[k, 6], h[k, 7] = (pl[k] >> 8) & 0xFF, pl[k] & 0xFF, 6, 64   # next header TCP
+        v[k, lead + 52] = 0x50                                        # its TCP data offset 5 (at +40 + 12)
+    return buf
+
+
+@pytest.mark.parametrize("case", ["template", "ring", "nb2k", "short", "v6mix"])
+def test_ring_plan_per_layout_vs_oracle(case):
+    """Ring plans (TUNE_PKT_BOUND 4, the default for strided batches of >= 16 Ki frames that are not
+    packed): each launch samples 1024 of its datagrams in one extra block (netcsum_pktstream.hip
+    pkt_plan_block) and leaves the form and run length for the next batch on the same ring. A ring's
+    first batch runs in the host's default (live pieces, runs by slot size); the next ones in the plan:
+    full slots the whole-span form 0 (IPv4 runs of 8, mixed-version rings 16), the 40 / 576 / 1500-B
+    ring and 300-B frames live pieces in runs of 32, 2-KiB slots live pieces in runs of 8. Every
+    batch's Rx flags and Tx bytes equal the oracle's on 2000 sampled frames of a 64 Ki-frame ring (Tx
+    in one and two passes), and every frame verifies after the Tx."""
+    n = 1 << 16
+    rng = np.random.default_rng(7)
+    if case == "template":
+        slot, lead, sizes, want_plan, v6 = 1520, 14, np.full(n, 1500), "8 bound=0", 0
+    elif case == "ring":
+        slot, lead, v6 = 1520, 14, 0
+        sizes = np.array([40, 576, 1500])[rng.choice(3, size=n, p=[7 / 12, 4 / 12, 1 / 12])]
+        want_plan = "32 bound=2"
+    elif case == "nb2k":
+        slot, lead, sizes, want_plan, v6 = 2048, 64, np.full(n, 1500), "8 bound=2", 0
+    elif case == "short":                           # 300-B datagrams in 1520-B slots: 10 KiB / 300 B
+        slot, lead, sizes, want_plan, v6 = 1520, 14, np.full(n, 300), "32 bound=2", 0
+    else:                                           # IPv4 / IPv6 full frames: RxValidateIP, form 0
+        slot, lead, sizes, want_plan, v6 = 1520, 14, np.full(n, 1500), "16 bound=0", 2
+    sizes = sizes.astype(np.int64)
+    buf = _np_ring(n, slot, lead, sizes, seed=zlib.crc32(case.encode()) & 0xFFFF, v6_every=v6)
+    present = slot - lead
+    ip = v6 != 0
+    rx_fn = netcsum.rx_validate_ip if ip else netcsum.rx_validate_ipv4
+    tx_fn = netcsum.tx_finalize_ip if ip else netcsum.tx_finalize_ipv4
+    o_rx = op.rx_validate_ip if ip else op.rx_validate
+    o_tx = op.tx_finalize_ip if ip else op.tx_finalize
+    sample = np.sort(rng.choice(n, size=2000, replace=False))
+    want_rx = {int(i): o_rx(bytes(buf[i * slot + lead:i * slot + lead + present])) for i in sample}
+    want_tx = {int(i): o_tx(bytes(buf[i * slot + lead:i * slot + lead + present]), True) for i in sample[:600]}
+    netcsum.tune(netcsum.TUNE_PKT_BOUND, 4)
+    b = torch.from_numpy(buf).to(DEV)
+    f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    launches = []
+    for call in range(3):                          # the first batch on the ring, then its plan
+        f.zero_()
+        rx_fn(b[lead:], n, f, stride=slot, pkt_len=present)
+        launches.append(netcsum.last_launch())
+        fl = f.cpu().numpy()                       # (synchronises: the plan word is written)
+        bad = [i for i, w in want_rx.items() if fl[i] != w]
+        assert not bad, (case, call, bad[:5])
+    # (the first batch runs in the host's default, or in the plan a previous buffer at the same address
+    # left: the plan lags one batch, harmless to the results)
+    assert launches[0].endswith("plan=first") or "plan=ring" in launches[0], launches[0]
+    for ln in launches[1:]:
+        assert "pkts_per_wave=" + want_plan in ln and "plan=ring" in ln, (case, ln)
+    ft = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    for passes in (1, 2):
+        netcsum.tune(netcsum.TUNE_TX_PASSES, passes)
+        bt = b.clone()                                            # (a new ring: its first batch,
+        tx_fn(bt[lead:], n, ft, stride=slot, pkt_len=present)     # then its plan; Tx is idempotent)
+        torch.cuda.synchronize()
+        tx_fn(bt[lead:], n, ft, stride=slot, pkt_len=present)
+        assert "pkts_per_wave=" + want_plan in netcsum.last_launch(), netcsum.last_launch()
+        got = bt.cpu().numpy()
+        ftn = ft.cpu().numpy()
+        for i, (q, qf) in want_tx.items():
+            o = i * slot + lead
+            assert bytes(got[o:o + present]) == q and ftn[i] == qf, (case, passes, i)
+        f.zero_()
+        rx_fn(bt[lead:], n, f, stride=slot, pkt_len=present)
+        assert bool(((f & 0x07) == 0x07).all().item()), (case, passes)

@@ -147,12 +147,28 @@ __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
-int main() {
+int main(int argc, char** argv) {
     struct Layout {
         const char* name;
         uint64_t stride;
         uint32_t lead, len;
-    } layouts[] = {{"packed", 1500, 0, 1500}, {"template", 1520, 14, 1500}, {"nb2k", 2048, 64, 1500}};
+    };
+    // default: the packet rows' rings; or layouts from the command line as NAME STRIDE LEAD LEN ...
+    // (round 5: TCP segments at TransportHdrIx of pool buffers, `seg1520 1520 34 1480`, `seg2k 2048 84
+    // 1480`, and the chain row's fragments, `frag2k 2048 42 1480`)
+    std::vector<Layout> layouts = {{"packed", 1500, 0, 1500}, {"template", 1520, 14, 1500}, {"nb2k", 2048, 64, 1500}};
+    if (argc > 1) {
+        layouts.clear();
+        for (int i = 1; i + 3 < argc; i += 4) {
+            const uint64_t st = std::strtoull(argv[i + 1], nullptr, 10);
+            const uint32_t ld = (uint32_t)std::strtoul(argv[i + 2], nullptr, 10), ln = (uint32_t)std::strtoul(argv[i + 3], nullptr, 10);
+            if (st == 0 || st > 2048u || ld + ln > st) {
+                std::fprintf(stderr, "layout %s: need stride <= 2048 and lead + len <= stride\n", argv[i]);
+                return 2;
+            }
+            layouts.push_back({argv[i], st, ld, ln});
+        }
+    }
     const uint32_t n = 1u << 20;
     const uint64_t ring_bytes = (uint64_t)n * 2048u + 4096u;
     uint8_t* ring = nullptr;

@@ -7,7 +7,9 @@ For 1 M datagrams per layout (tools/ring_layouts.py):
              Cfg/Template/net_dev_cfg.c:146-149), 1506 B present
   nb2k       1500-B datagrams in 2048-B slots at +64, 1984 B present
   ring       40 / 576 / 1500-B datagrams at 7 : 4 : 1 in 1520-B slots at +14, 1506 B present
-each as a strided batch (pkt_len = bytes present) under NETCSUM_TUNE_PKT_BOUND 0 / 1 / 2 / 3 (the
+each as a strided batch (pkt_len = bytes present) under NETCSUM_TUNE_PKT_BOUND 4 (ring plans: the form
+and run length the previous batch on the ring sampled on the device, "strided.plan", with the plan the
+timed calls ran) and 0 / 1 / 2 / 3 (the
 run-stream kernel reading whole spans / live pieces, the parse first / live pieces with piece 0,
 / with the first 4 pieces loaded during the parse; 3 only for dense layouts) at the default run
 length and at 8 / 32 datagrams per run, and as an
@@ -74,8 +76,16 @@ def main():
                         ("offlen.d8", -1, -1, desc, 8)]
         elif os.environ.get("RING_VARIANTS") == "runs":                 # run lengths of the default form
             variants = [("strided.b2.s%d" % s, 2, s, strided, 4) for s in (8, 12, 16, 20, 24, 28, 32)]
+        elif os.environ.get("RING_VARIANTS") == "offlen":               # offset/length forms only
+            variants = [("offlen", -1, -1, desc, 4), ("offlen.s32", -1, 32, desc, 4), ("offlen.s8", -1, 8, desc, 4)]
+        elif os.environ.get("RING_VARIANTS") == "plan":                 # the device plan against fixed forms
+            variants = [("strided.plan", 4, -1, strided, 4), ("strided.b0", 0, -1, strided, 4),
+                        ("strided.b2", 2, -1, strided, 4), ("strided.b2.s8", 2, 8, strided, 4),
+                        ("strided.b2.s32", 2, 32, strided, 4), ("offlen", -1, -1, desc, 4),
+                        ("offlen.b2.s32", 2, 32, desc, 4)]
         else:
-            variants = [("strided.b0", 0, -1, strided, 4), ("strided.b1", 1, -1, strided, 4),
+            variants = [("strided.plan", 4, -1, strided, 4),
+                        ("strided.b0", 0, -1, strided, 4), ("strided.b1", 1, -1, strided, 4),
                         ("strided.b2", 2, -1, strided, 4), ("strided.b3", 3, -1, strided, 4),
                         ("strided.b2.s8", 2, 8, strided, 4), ("strided.b3.s8", 3, 8, strided, 4),
                         ("strided.b2.s32", 2, 32, strided, 4), ("offlen", -1, -1, desc, 4),
@@ -97,6 +107,8 @@ def main():
                     ms = events_ms(fn, st)
                     d = res.setdefault((tag, op), {"ms": [], "kernel": netcsum.last_launch()})
                     d["ms"].append(ms)
+                    if bound == 4:                                         # the ring plan the timed calls ran
+                        d["plan"] = netcsum.last_launch().rsplit("pkts_per_wave=", 1)[-1]
                     if op == "rx":
                         d["all_valid"] = bool(((flags & 0x07) == 0x07).all().item())
                     else:

@@ -36,7 +36,7 @@ thread_local netcsum::TuneKnob g_tune_tile{-1};                 // -1: auto (4 s
 thread_local netcsum::TuneKnob g_tune_burst_zc{3};              // host bursts: pinned rings read in place by the resident server
 thread_local netcsum::TuneKnob g_tune_burst_idle{500};           // resident burst server: idle microseconds before it stops
 thread_local netcsum::TuneKnob g_tune_burst_life{1000};          // resident burst server: microseconds of residency per launch
-thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3
+thread_local netcsum::TuneKnob g_tune_pkt_bound{-1};            // run-stream packets: -1 auto, 0..3, 4 ring plans
 thread_local netcsum::TuneKnob g_tune_tx_passes{0};             // run-stream Tx: 0 auto (2 passes), 1, 2
 std::atomic<int> g_err_reports{0};
 
@@ -453,7 +453,7 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         ScratchLease word;
         NC_HIP(word.acquire(dev, s, 256u, false));
         uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
-        NC_HIP(netcsum::launch_varlen_runlen(a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
+        NC_HIP(netcsum::launch_varlen_runlen(a.seg_off, a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
                                              c.stream_spw, run, s));
         a.run_dev = run;
         NC_HIP(netcsum::launch_seg_batch(a, c, s));
@@ -905,6 +905,85 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
     return NET_UTIL_ERR_NONE;
 }
 
+// ---- ring plans (netcsum_pktstream.hip pkt_plan_block): the form and run length the last batch on a
+// ring sampled for the next one. The words live in one pinned, coherent, device-mapped allocation per
+// device that is never freed (a launch still in flight may store into its word after its thread has
+// gone); each thread keeps a small table of its rings, each with a word and a tag (a word reused for
+// another ring, or a late store of an evicted one, carries another tag and is ignored).
+constexpr uint32_t kPlanWords = 4096u;
+struct PlanPool {
+    std::once_flag once;
+    uint32_t* h = nullptr;
+    uint32_t* d = nullptr;
+};
+PlanPool g_plan_pool[kMaxDev];
+std::atomic<uint32_t> g_plan_next{0};
+struct RingPlan {
+    int dev = -1;
+    const void* base = nullptr;
+    uint64_t stride = 0;
+    uint32_t pkt_len = 0, n = 0, slot = 0, tag = 0, plan = 0, use = 0;
+    int ip_ver = -1;
+};
+constexpr int kRingPlans = 16;
+thread_local RingPlan tls_ring_plans[kRingPlans];
+thread_local uint32_t tls_ring_clock = 0;
+
+// The plan the ring's previous batch left (0: none yet), its word (host and device addresses) and tag
+// for this batch's plan block; *d_word = nullptr when no pool could be had (the batch then runs
+// without a plan block).
+static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t pkt_len, uint32_t n, int ip_ver,
+                          uint32_t** h_word, uint32_t** d_word, uint32_t* tag) {
+    *h_word = *d_word = nullptr;
+    if (dev < 0 || dev >= kMaxDev) return 0u;
+    PlanPool& pool = g_plan_pool[dev];
+    std::call_once(pool.once, [&]() {
+        void* h = nullptr;
+        void* dp = nullptr;
+        if (hipHostMalloc(&h, kPlanWords * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        std::memset(h, 0, kPlanWords * sizeof(uint32_t));
+        pool.h = static_cast<uint32_t*>(h);
+        pool.d = static_cast<uint32_t*>(dp);
+    });
+    if (pool.h == nullptr) return 0u;
+    RingPlan* e = nullptr;
+    RingPlan* lru = &tls_ring_plans[0];
+    for (RingPlan& r : tls_ring_plans) {
+        if (r.dev == dev && r.base == base && r.stride == stride && r.pkt_len == pkt_len && r.n == n && r.ip_ver == ip_ver) {
+            e = &r;
+            break;
+        }
+        if (r.use < lru->use) lru = &r;
+    }
+    if (e == nullptr) {                                     // a new ring: a fresh word and tag
+        e = lru;
+        const uint32_t k = g_plan_next.fetch_add(1u);
+        *e = RingPlan{};
+        e->dev = dev;
+        e->base = base;
+        e->stride = stride;
+        e->pkt_len = pkt_len;
+        e->n = n;
+        e->ip_ver = ip_ver;
+        e->slot = k % kPlanWords;
+        e->tag = (k / kPlanWords * 2654435761u + k) & 0x7FFFu;
+    }
+    e->use = ++tls_ring_clock;
+    const uint32_t w = *reinterpret_cast<volatile uint32_t*>(pool.h + e->slot);
+    if ((w >> 31) != 0u && ((w >> 16) & 0x7FFFu) == e->tag) e->plan = w & 0xFFFFu;
+    *h_word = pool.h + e->slot;
+    *d_word = pool.d + e->slot;
+    *tag = e->tag;
+    return e->plan;
+}
+
 // udp_mode: PktBatchArgs::udp_tx_csum (Tx); d_action / rx_cfg: the Rx burst actions (Rx, optional);
 // d_fieldpos: Tx, which fields each packet had written (the host-memory forms' records, optional).
 static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16_t* d_len, uint64_t stride,
@@ -985,12 +1064,14 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
     // r4f ring probe: 1 M x 1500 B Rx 0.2145 ms against 0.2188 in form 3)
     const bool dense = d_off == nullptr && stride <= (uint64_t)pkt_len + 64u;
     const bool packed = d_off == nullptr && stride == (uint64_t)pkt_len;
-    int bound = g_tune_pkt_bound.load() >= 0 ? g_tune_pkt_bound.load() : (packed ? 0 : 2);
-    if (bound_pref >= 0 && g_tune_pkt_bound.load() < 0) {   // the caller's preference, where it applies
+    const int tb0 = g_tune_pkt_bound.load();
+    const bool bound_default = tb0 < 0 || tb0 == 4;         // (4: ring plans, else as the default)
+    int bound = !bound_default ? tb0 : (packed ? 0 : 2);
+    if (bound_pref >= 0 && bound_default) {                 // the caller's preference, where it applies
         if (netcsum::pkt_stream_supported(a, ip_ver, bound_pref)) bound = bound_pref;
     }
     if (d == 8 && bound == 1) bound = 2;                    // (8 pieces in flight: forms 0, 2, 3)
-    if (!netcsum::pkt_stream_supported(a, ip_ver, bound) && bound >= 1 && dense && g_tune_pkt_bound.load() < 0) {
+    if (!netcsum::pkt_stream_supported(a, ip_ver, bound) && bound >= 1 && dense && bound_default) {
         bound = 0;                                          // datagrams > 64384 B: past the bitmap's reach
     }
     if (kern != 2 && netcsum::pkt_stream_supported(a, ip_ver, bound)) {
@@ -1012,6 +1093,47 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         if (!(tile > 0 && tile <= 64)) {
             while (spw > 1u && (uint64_t)n_pkt < 2048ull * spw) spw >>= 1;
         }
+        // The ring's plan (netcsum_pktstream.hip pkt_plan_block): for strided batches that are not
+        // packed — by default from 16 Ki datagrams (smaller ones are bursts, latency-bound, with the
+        // runs halved above), always with TUNE_PKT_BOUND 4 — the launch samples its datagrams in one
+        // extra block and leaves the form and run length for the next batch on the same ring (same
+        // base, stride, bytes present, count, IP version) in coherent host memory; a batch whose ring
+        // has a plan runs in it, the first one in the host's default above.
+        const bool plan_ring = d_off == nullptr && !packed && bound_pref < 0 && d == 4 && !(tile > 0 && tile <= 64) &&
+                               (tb0 == 4 || (tb0 < 0 && n_pkt >= 16384u)) && rec_only == nullptr &&
+                               netcsum::pkt_stream_supported(a, ip_ver, 2);
+        const char* plan_note = "";
+        if (plan_ring) {
+            uint32_t run0 = 0u;
+            if (netcsum::pkt_stream_supported(a, ip_ver, 0)) {
+                run0 = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
+                                   : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
+                while (run0 > 1u && (uint64_t)n_pkt < 2048ull * run0) run0 >>= 1;
+            }
+            uint64_t cap = (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+            cap = std::min<uint64_t>(cap, std::max<uint64_t>(8u, ((uint64_t)n_pkt / 2048u) & ~7ull));
+            cap = std::min<uint64_t>(cap, 64u);
+            uint32_t* h_word = nullptr;
+            uint32_t* d_word = nullptr;
+            uint32_t tag = 0u;
+            const uint32_t plan = ring_plan(dev, d_base, stride, pkt_len, n_pkt, ip_ver, &h_word, &d_word, &tag);
+            if (d_word != nullptr) {
+                a.plan = run0 | ((uint32_t)cap << 8) | (tag << 16);
+                a.plan_out = d_word;
+                const uint32_t form = plan & 0xFFu, prun = (plan >> 8) & 0xFFu;
+                if (plan != 0u && form == 0u && run0 != 0u && prun == run0) {
+                    bound = 0;
+                    spw = run0;
+                    plan_note = " plan=ring(form0)";
+                } else if (plan != 0u && form == 2u && prun >= 1u && prun <= cap) {
+                    bound = 2;
+                    spw = prun;
+                    plan_note = " plan=ring(live)";
+                } else {
+                    plan_note = " plan=first";
+                }
+            }
+        }
         const bool snt = nt >= 0 ? (nt != 0) : true;
         // Tx passes: auto = two (8-B records, then a scatter pass: 1 M x 1500 B 0.2918 against 0.2954
         // ms in one pass) from 64 Ki datagrams up, one below (a burst is then a single launch)
@@ -1019,30 +1141,37 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         const bool two = tx && (rec_only != nullptr || tp == 2 || (tp == 0 && n_pkt >= 65536u));
         // IPv6 / mixed: the Rx and one-pass Tx kernels, and two-pass Tx's scatter pass, finish their
         // deferred datagrams themselves (no deferral word, no walk launch, no flags in scratch)
-        if (bound >= 1 && d_off == nullptr) {
+        if (bound >= 1 && d_off == nullptr) {          // (the device plan sizes its own runs)
             const uint64_t cap = (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
-            if (spw > cap && tile > 0 && g_tune_pkt_bound.load() < 0 && dense) {
+            if (spw > cap && tile > 0 && bound_default && dense) {
                 bound = 0;                                // a run length asked for: the whole-span form
             } else {
                 spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
             }
         }
-        char desc[144];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s", d,
+        char desc[200];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s%s", d,
                  snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, bound,
-                 d_off ? " offlen" : "",
-                 two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "");
+                 d_off ? " offlen +pkt_vl_deferred_kernel" : "",
+                 two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "", plan_note);
         netcsum::set_last_launch(desc);
+        // scratch: the records of two-pass Tx; offset/length batches also the deferred-run list (its
+        // tagged count word, then one index per run the stream kernel could not stream in order)
+        const size_t rec_bytes = (two && rec_only == nullptr) ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
+        const size_t defer_bytes = d_off ? (8u + 4u * (((size_t)n_pkt + spw - 1u) / spw) + 15u) & ~(size_t)15u : 0u;
+        ScratchLease scratch;
+        if (rec_bytes + defer_bytes) NC_HIP(scratch.acquire(dev, hs, rec_bytes + defer_bytes));
+        if (d_off) {
+            a.vl_defer = reinterpret_cast<unsigned long long*>(static_cast<uint8_t*>(scratch.ptr()) + rec_bytes);
+            a.vl_tag = scratch.next_tag();
+        }
         if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
             NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs, rec_only,
                                               false));
-            return NET_UTIL_ERR_NONE;
+        } else {
+            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs,
+                                              two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         }
-        // scratch: the records of two-pass Tx
-        ScratchLease scratch;
-        if (two) NC_HIP(scratch.acquire(dev, hs, (size_t)n_pkt * sizeof(netcsum::PktTxRecord)));
-        NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs,
-                                          two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }
@@ -1629,7 +1758,7 @@ static NET_ERR tx_burst_zero_copy(HostCtx& c, void* h_base, const uint64_t* h_of
     // (the tuned bound, else the whole-span form 0 or the live-piece form 2), and the server's form
     // where the server serves it (server_form: strided dense, sparse and offset/length rings)
     const int tb = g_tune_pkt_bound.load();
-    if (!(tb >= 0 ? netcsum::pkt_stream_supported(a, 0, tb)
+    if (!((tb >= 0 && tb <= 3) ? netcsum::pkt_stream_supported(a, 0, tb)
                   : netcsum::pkt_stream_supported(a, 0, kBurstBound) || netcsum::pkt_stream_supported(a, 0, 2))) {
         return NET_UTIL_ERR_NONE;
     }
@@ -2014,7 +2143,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_burst_life.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
-        if (value < -1 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_pkt_bound.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_BLOCK_THREADS:

@@ -75,6 +75,16 @@ struct PktBatchArgs {
     uint32_t        xcd;           // run-stream form: XCD-aware block order (set by the launcher)
     uint32_t*       fieldpos_out;  // Tx (optional): per packet, which checksum fields were written —
                                    // kFieldIP | kFieldL4 | transport field offset (host-memory forms)
+    uint32_t        plan;          // run-stream strided form, the next batch's plan (pkt_plan_block):
+                                   // bits 0-7 the whole-span run (0: form 0 not allowed, gaps > 64 B),
+                                   // bits 8-15 the longest live-piece run allowed (the bitmap's reach,
+                                   // the batch size), bits 16-30 the host's tag for the ring
+    uint32_t*       plan_out;      // optional (strided): an extra block samples the batch and stores
+                                   // 1 << 31 | tag << 16 | run << 8 | form here (coherent host memory)
+    unsigned long long* vl_defer;  // offset/length runs not in address order within the reach: word 0 =
+                                   // vl_tag << 32 | count, then the run indices (u32) for the deferred
+                                   // pass (pkt_vl_deferred_kernel); nullptr: such runs are done inline
+    uint32_t        vl_tag;
 };
 constexpr uint32_t kFieldIP = 1u << 31;    // fieldpos_out: the IPv4 header checksum field (+10) written
 constexpr uint32_t kFieldL4 = 1u << 30;    // fieldpos_out: the transport field at (bits 0-15) written
@@ -151,8 +161,9 @@ uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
-// Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128).
-hipError_t launch_varlen_runlen(const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
+// Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128),
+// capped to 56 KiB / pitch and 64 for segments in increasing order with gaps (the live-sector runs).
+hipError_t launch_varlen_runlen(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
                                 uint32_t spw_min, uint32_t* out, hipStream_t s);
 void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
 uint32_t varlen_run_bytes();
