@@ -76,8 +76,12 @@ def main():
                         ("offlen.d8", -1, -1, desc, 8)]
         elif os.environ.get("RING_VARIANTS") == "runs":                 # run lengths of the default form
             variants = [("strided.b2.s%d" % s, 2, s, strided, 4) for s in (8, 12, 16, 20, 24, 28, 32)]
+        elif os.environ.get("RING_VARIANTS") == "offlengrid":           # offset/length runs x residency
+            variants = [("offlen.s%d.w%d" % (r, wv), -1, r, desc, 4) for r in (8, 16, 32) for wv in (5, 6, 7, 8)]
+            variants += [("strided.plan.w%d" % wv, 4, -1, strided, 4) for wv in (5, 6, 7, 8)]
         elif os.environ.get("RING_VARIANTS") == "offlen":               # offset/length forms only
-            variants = [("offlen", -1, -1, desc, 4), ("offlen.s32", -1, 32, desc, 4), ("offlen.s8", -1, 8, desc, 4)]
+            variants = [("offlen", -1, -1, desc, 4), ("offlen.s32", -1, 32, desc, 4), ("offlen.s8", -1, 8, desc, 4),
+                        ("offlen.w5", -1, -1, desc, 4), ("offlen.w6", -1, -1, desc, 4), ("offlen.s32.w6", -1, 32, desc, 4)]
         elif os.environ.get("RING_VARIANTS") == "plan":                 # the device plan against fixed forms
             variants = [("strided.plan", 4, -1, strided, 4), ("strided.b0", 0, -1, strided, 4),
                         ("strided.b2", 2, -1, strided, 4), ("strided.b2.s8", 2, 8, strided, 4),
@@ -97,6 +101,8 @@ def main():
                 netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
                 netcsum.tune(netcsum.TUNE_TILE, max(spw, -1))
                 netcsum.tune(netcsum.TUNE_KERNEL, 2 if spw == -2 else 0)   # the lane-group packet kernel
+                # ".wN": N waves per SIMD resident (TUNE_STREAM_WAVES; default: as many as fit)
+                netcsum.tune(netcsum.TUNE_STREAM_WAVES, int(tag.rsplit(".w", 1)[1]) if ".w" in tag else -1)
                 base = r["buf"] if kw is desc else r["base"]
                 for op in ("rx", "tx"):
                     if op == "rx":
@@ -117,6 +123,7 @@ def main():
         netcsum.tune(netcsum.TUNE_TILE, -1)
         netcsum.tune(netcsum.TUNE_KERNEL, 0)
         netcsum.tune(netcsum.TUNE_CHUNKS, 0)
+        netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
         for (tag, op), d in res.items():
             algo = r["datagram_bytes"] + n * (1 if op == "rx" else 4)
             ms = min(d["ms"])

@@ -359,6 +359,8 @@ thread_local ScratchCache tls_scratch;
 // contents any interleaving leaves correct (the varlen run word: any value is a valid run length):
 // it records no event (an event record costs ~3 us of GPU time per call, profiles/r3d_event_probe)
 // and its slot is freed after a device synchronisation instead.
+constexpr size_t kTailBytes = 64;
+
 class ScratchLease {
 public:
     hipError_t acquire(int dev, hipStream_t st, size_t bytes, bool ordered = true) {
@@ -387,16 +389,23 @@ public:
             hit->dev = dev;
             hit->stream = st;
         }
-        if (hit->cap < bytes) {
+        if (hit->cap < bytes + kTailBytes) {
             if (capturing_ || hit->pinned) return hipErrorStreamCaptureUnsupported;   // no allocation under capture
             hipError_t e = slot_wait(*hit);                // the stream's earlier launches may use it
             if (e != hipSuccess) return e;
             if (hit->p) (void)hipFree(hit->p);
             hit->p = nullptr;
             hit->cap = 0;
-            const size_t cap = std::max<size_t>(bytes, (size_t)1 << 20);
+            const size_t cap = std::max<size_t>(bytes + kTailBytes, (size_t)1 << 20);
             e = hipMalloc(&hit->p, cap);
             if (e != hipSuccess) {
+                hit->p = nullptr;
+                return e;
+            }
+            // the tail words start at zero (tail_words: counters that their users reset themselves)
+            e = hipMemsetAsync(static_cast<uint8_t*>(hit->p) + cap - kTailBytes, 0, kTailBytes, st);
+            if (e != hipSuccess) {
+                (void)hipFree(hit->p);
                 hit->p = nullptr;
                 return e;
             }
@@ -417,6 +426,11 @@ public:
         return hipSuccess;
     }
     void* ptr() const { return slot_ ? slot_->p : nullptr; }
+    // The slot's last kTailBytes, past every request (zeroed when the slot is allocated): words that
+    // outlive a call — the offset/length deferral counter, which the deferred pass resets to zero.
+    uint32_t* tail_words() const {
+        return slot_ ? reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot_->p) + slot_->cap - kTailBytes) : nullptr;
+    }
     // A tag no earlier call on this slot used (a deferral word holding it was written by this call;
     // after 2^32 calls a stale word may match once, which only repeats an idempotent pass).
     uint32_t next_tag() {
@@ -905,6 +919,11 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
     return NET_UTIL_ERR_NONE;
 }
 
+// (NETCSUM_TUNE_STREAM_WAVES set: measurements of fixed residencies take no plans)
+static bool g_tune_stream_waves_set() {
+    return netcsum::stream_waves_tuned();
+}
+
 // ---- ring plans (netcsum_pktstream.hip pkt_plan_block): the form and run length the last batch on a
 // ring sampled for the next one. The words live in one pinned, coherent, device-mapped allocation per
 // device that is never freed (a launch still in flight may store into its word after its thread has
@@ -1099,36 +1118,49 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         // extra block and leaves the form and run length for the next batch on the same ring (same
         // base, stride, bytes present, count, IP version) in coherent host memory; a batch whose ring
         // has a plan runs in it, the first one in the host's default above.
-        const bool plan_ring = d_off == nullptr && !packed && bound_pref < 0 && d == 4 && !(tile > 0 && tile <= 64) &&
+        // Offset/length batches take ring plans too, keyed on their descriptor arrays: the run length
+        // (by the streamed bytes, capped by the sampled pitch to the reach) and the residency.
+        const bool plan_ring = !packed && bound_pref < 0 && d == 4 && !(tile > 0 && tile <= 64) &&
                                (tb0 == 4 || (tb0 < 0 && n_pkt >= 16384u)) && rec_only == nullptr &&
-                               netcsum::pkt_stream_supported(a, ip_ver, 2);
+                               g_tune_stream_waves_set() == false && netcsum::pkt_stream_supported(a, ip_ver, 2);
         const char* plan_note = "";
-        if (plan_ring) {
+        bool vl_wide = true;                             // the deferred pass's grid: wide unless the plan
+        bool vl_inline = false;                          // found the ring's descriptors in order; a dense
+        if (plan_ring) {                                 // ring in order: the inline form (pkt_stream_kernel DEF)
             uint32_t run0 = 0u;
-            if (netcsum::pkt_stream_supported(a, ip_ver, 0)) {
+            if (d_off == nullptr && netcsum::pkt_stream_supported(a, ip_ver, 0)) {
                 run0 = ip_ver == 0 ? (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(16u, (40960u / per) & ~15ull))
                                    : (uint32_t)std::min<uint64_t>(64u, std::max<uint64_t>(8u, (20480u / per) & ~7ull));
                 while (run0 > 1u && (uint64_t)n_pkt < 2048ull * run0) run0 >>= 1;
             }
-            uint64_t cap = (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
+            uint64_t cap = d_off ? 64u : (netcsum::kLiveReach - 128u - (uint64_t)pkt_len) / std::max<uint64_t>(stride, 1u) + 1u;
             cap = std::min<uint64_t>(cap, std::max<uint64_t>(8u, ((uint64_t)n_pkt / 2048u) & ~7ull));
             cap = std::min<uint64_t>(cap, 64u);
             uint32_t* h_word = nullptr;
             uint32_t* d_word = nullptr;
             uint32_t tag = 0u;
-            const uint32_t plan = ring_plan(dev, d_base, stride, pkt_len, n_pkt, ip_ver, &h_word, &d_word, &tag);
+            const uint32_t plan = d_off ? ring_plan(dev, d_base, reinterpret_cast<uint64_t>(d_off), 0xFFFFFFFFu, n_pkt,
+                                                    ip_ver, &h_word, &d_word, &tag)
+                                        : ring_plan(dev, d_base, stride, pkt_len, n_pkt, ip_ver, &h_word, &d_word, &tag);
             if (d_word != nullptr) {
                 a.plan = run0 | ((uint32_t)cap << 8) | (tag << 16);
                 a.plan_out = d_word;
-                const uint32_t form = plan & 0xFFu, prun = (plan >> 8) & 0xFFu;
+                const uint32_t form = plan & 0x7u, pw = (plan >> 4) & 0xFu, prun = (plan >> 8) & 0xFFu;
+                if (plan != 0u && d_off != nullptr) {
+                    vl_wide = (plan & 8u) != 0u;
+                    vl_inline = !vl_wide && ((plan >> 4) & 0xFu) != 0u;   // (the plan's reduced residency)
+                }
                 if (plan != 0u && form == 0u && run0 != 0u && prun == run0) {
                     bound = 0;
                     spw = run0;
                     plan_note = " plan=ring(form0)";
-                } else if (plan != 0u && form == 2u && prun >= 1u && prun <= cap) {
+                } else if (plan != 0u && form == 2u && prun >= 1u && prun <= cap && (pw == 0u || (pw >= 3u && pw <= 8u))) {
                     bound = 2;
                     spw = prun;
-                    plan_note = " plan=ring(live)";
+                    a.res_waves = pw;
+                    plan_note = pw ? (pw == 5u ? " plan=ring(live,5 waves)" : pw == 6u ? " plan=ring(live,6 waves)"
+                                                                             : " plan=ring(live,waves)")
+                                   : " plan=ring(live)";
                 } else {
                     plan_note = " plan=first";
                 }
@@ -1152,18 +1184,20 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
         char desc[200];
         snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s%s", d,
                  snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, bound,
-                 d_off ? " offlen +pkt_vl_deferred_kernel" : "",
+                 d_off ? (vl_inline ? " offlen (inline fallback)" : " offlen +pkt_vl_deferred_kernel") : "",
                  two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "", plan_note);
         netcsum::set_last_launch(desc);
-        // scratch: the records of two-pass Tx; offset/length batches also the deferred-run list (its
-        // tagged count word, then one index per run the stream kernel could not stream in order)
+        // scratch: the records of two-pass Tx; offset/length batches also the deferred-run list (one
+        // index per run the stream kernel could not stream in order) and its counters in the slot's
+        // tail words (count, blocks done: the deferred pass leaves both zero)
         const size_t rec_bytes = (two && rec_only == nullptr) ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
-        const size_t defer_bytes = d_off ? (8u + 4u * (((size_t)n_pkt + spw - 1u) / spw) + 15u) & ~(size_t)15u : 0u;
+        const size_t defer_bytes = (d_off && !vl_inline) ? (4u * (((size_t)n_pkt + spw - 1u) / spw) + 15u) & ~(size_t)15u : 0u;
         ScratchLease scratch;
         if (rec_bytes + defer_bytes) NC_HIP(scratch.acquire(dev, hs, rec_bytes + defer_bytes));
-        if (d_off) {
-            a.vl_defer = reinterpret_cast<unsigned long long*>(static_cast<uint8_t*>(scratch.ptr()) + rec_bytes);
-            a.vl_tag = scratch.next_tag();
+        if (d_off && !vl_inline) {
+            a.vl_list = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch.ptr()) + rec_bytes);
+            a.vl_ctr = scratch.tail_words();
+            a.vl_wide = vl_wide ? 1u : 0u;
         }
         if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
             NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs, rec_only,

@@ -79,12 +79,15 @@ struct PktBatchArgs {
                                    // bits 0-7 the whole-span run (0: form 0 not allowed, gaps > 64 B),
                                    // bits 8-15 the longest live-piece run allowed (the bitmap's reach,
                                    // the batch size), bits 16-30 the host's tag for the ring
-    uint32_t*       plan_out;      // optional (strided): an extra block samples the batch and stores
-                                   // 1 << 31 | tag << 16 | run << 8 | form here (coherent host memory)
-    unsigned long long* vl_defer;  // offset/length runs not in address order within the reach: word 0 =
-                                   // vl_tag << 32 | count, then the run indices (u32) for the deferred
-                                   // pass (pkt_vl_deferred_kernel); nullptr: such runs are done inline
-    uint32_t        vl_tag;
+    uint32_t*       plan_out;      // optional: an extra block samples the batch and stores 1 << 31 |
+                                   // tag << 16 | run << 8 | waves << 4 | form here (coherent host
+                                   // memory); offset/length batches: bits 0-7 of `plan` unused
+    uint32_t        res_waves;     // launcher: waves per SIMD to keep resident (3..8; 0: as many as fit)
+    uint32_t*       vl_list;       // offset/length runs not in address order within the reach: the
+    uint32_t*       vl_ctr;        // stream kernel appends their indices (vl_ctr[0]: count, by atomic
+                                   // add) and the deferred pass (pkt_vl_deferred_kernel) does them, then
+                                   // leaves vl_ctr[0..1] zero; nullptr: done inline
+    uint32_t        vl_wide;       // launcher: the deferred pass's grid, wide (1) or 8 blocks (0)
 };
 constexpr uint32_t kFieldIP = 1u << 31;    // fieldpos_out: the IPv4 header checksum field (+10) written
 constexpr uint32_t kFieldL4 = 1u << 30;    // fieldpos_out: the transport field at (bits 0-15) written
@@ -248,6 +251,7 @@ hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, b
 // CU's 160 KiB; 0 = no cap.
 void set_stream_waves(int w);
 uint32_t stream_lds_bytes(int auto_waves);
+bool stream_waves_tuned();             // NETCSUM_TUNE_STREAM_WAVES set (>= 0)
 // Row-touch prologue of the run-stream kernels (NETCSUM_TUNE_STREAM_TOUCH: -1 each kernel's
 // default `auto_on`, 0 off, 1 on).
 void set_stream_touch(int t);

@@ -798,19 +798,14 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
                                                  len, span);
         } else if (DEFER) {
             // any other run (unordered, overlapping, far apart, or a datagram past the bitmap's reach)
-            // goes on the deferred list (pkt_vl_deferred_kernel): done here, one datagram at a time,
-            // its loop held the offset/length kernels at 91-93 VGPRs (4-5 waves per SIMD; VERDICT r4
-            // weak 4), for the sake of layouts a NIC ring does not have
+            // is flagged for the deferred pass (pkt_vl_deferred_kernel): done here, one datagram at a
+            // time, its loop held the offset/length kernels at 91-93 VGPRs (4-5 waves per SIMD;
+            // VERDICT r4 weak 4), for the sake of layouts a NIC ring does not have. (One atomic add per
+            // deferred run: appends by compare-and-swap on a tagged word took a batch of 32 768 deferred
+            // runs 289 ms.)
             if (lane == 0u) {
-                unsigned long long* word = A.vl_defer;
-                const unsigned long long tag = (unsigned long long)A.vl_tag << 32;
-                unsigned long long old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                unsigned long long nw;
-                do {
-                    nw = (old & ~0xFFFFFFFFull) == tag ? old + 1u : tag | 1u;
-                } while (!__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT));
-                reinterpret_cast<uint32_t*>(word + 1)[(uint32_t)nw - 1u] = (uint32_t)run;
+                const uint32_t k = __hip_atomic_fetch_add(A.vl_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                A.vl_list[k] = (uint32_t)run;
             }
         } else {
             // (the burst server, which has no deferred pass) one datagram per run (any order, overlap
@@ -827,33 +822,37 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
     }
 }
 
-// The deferred pass of an offset/length batch: the runs its stream kernel listed (A.vl_defer, tagged
-// with this batch's vl_tag: a stale count from an earlier batch reads as none), one datagram at a time
-// as a run of one. Waves take list entries round-robin; with nothing listed every wave returns after
-// one scalar load. Launched after the stream kernel in stream order (and before two-pass Tx's scatter).
+// The deferred pass of an offset/length batch: the runs its stream kernel listed (A.vl_list, count in
+// A.vl_ctr[0]), one datagram at a time as a run of one, waves taking list entries round-robin; the
+// last block to finish leaves the count and its own counter zero for the next batch on the stream.
+// Launched after the stream kernel in stream order (and before two-pass Tx's scatter): 8 blocks when
+// the ring's plan found its descriptors in order (a run listed anyway, e.g. where the ring wraps, is
+// still done), 256 otherwise (the ring's first batch, reordered rings).
 template <int D, bool NT, bool TX, bool REC, int VER, int BND>
 __global__ void __launch_bounds__(256) pkt_vl_deferred_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
+    __shared__ uint32_t s_last;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const unsigned long long word = *A.vl_defer;
     const uint32_t runs = (uint32_t)(((uint64_t)A.n + spw - 1u) / spw);
-    // (a fresh scratch word may hold anything: the count and every index are bounded by the batch, and
-    // a run done twice writes the same results)
-    const uint32_t count = (uint32_t)(word >> 32) == A.vl_tag ? min((uint32_t)word, runs) : 0u;
-    const uint32_t* list = reinterpret_cast<const uint32_t*>(A.vl_defer + 1);
+    const uint32_t count = min(*A.vl_ctr, runs);
     for (uint32_t i = blockIdx.x * 4u + w; i < count; i += gridDim.x * 4u) {
-        const uint32_t r = list[i];
-        if (r >= runs) {
-            continue;
-        }
+        const uint32_t r = A.vl_list[i];
         const uint32_t s_begin = r * spw;
-        const uint32_t nres = min(A.n - s_begin, spw);
+        const uint32_t nres = r < runs ? min(A.n - s_begin, spw) : 0u;
         for (uint32_t k = 0; k < nres; ++k) {
             const uint64_t ok_ = A.off[s_begin + k];
             const uint32_t lk = A.len[s_begin + k];
             const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
             const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
             pkt_run<D, NT, TX, REC, VER, BND, true>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        s_last = __hip_atomic_fetch_add(A.vl_ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+        if (s_last) {                                           // every block has read the count
+            __hip_atomic_store(A.vl_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.vl_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -877,14 +876,45 @@ __global__ void __launch_bounds__(256) pkt_vl_deferred_kernel(PktBatchArgs A, ui
 constexpr uint32_t kPlanLiveBytes = 10240u;
 constexpr uint32_t kPlanSamples = 1024u;
 
-template <int VER>
+// Offset/length rings (tools/ring_probe.py RING_VARIANTS=offlengrid, profiles/r5g_ring_probe_grid.jsonl:
+// runs of 8 / 16 / 32 at 5-8 waves per SIMD): short streamed datagrams (the 40 / 576 / 1500-B ring,
+// mean 317 B streamed) want runs of 32 at full residency (Rx 0.1063 ms; runs of 16: 0.1267), long ones
+// (1500-B frames, packed, in 1520-B or 2-KiB slots) runs of 16 at 6 waves per SIMD (2-KiB slots
+// 0.2581 against 0.2696 at 8 waves; template slots 0.2290, packed 0.2251): a stream of whole 1-KiB
+// pieces loses to DRAM contention at full residency, as C2 does (§5.2). Strided live runs keep full
+// residency (their best at 7-8 waves on every layout) and the run rule below.
+__device__ __forceinline__ void pkt_plan_vl(uint32_t mean, uint32_t& run, uint32_t& waves) {
+    run = mean * 45u < kPlanLiveBytes * 2u ? 32u : 16u;
+    waves = run == 32u ? 0u : 6u;
+}
+
+template <int VER, bool VL>
 __device__ void pkt_plan_block(const PktBatchArgs& A) {
-    __shared__ uint32_t part[4];
+    __shared__ uint32_t part[4][3];
     const uint32_t m = min(A.n, kPlanSamples);
-    uint32_t acc = 0u;
+    uint32_t acc = 0u, pit = 0u, npit = 0u;
     for (uint32_t j = threadIdx.x; j < m; j += 256u) {
         const uint64_t i = ((uint64_t)j * A.n) / m;
-        const uintptr_t a = (uintptr_t)A.base + i * A.stride;
+        uintptr_t a;
+        uint32_t avail;
+        if constexpr (VL) {                                   // the descriptors: start, length, pitch
+            const uint64_t o = A.off[i];
+            a = (uintptr_t)A.base + o;
+            avail = A.len[i];
+            if (i + 1u < A.n) {
+                const uint64_t o1 = A.off[i + 1u];
+                if (o1 >= o + avail && o1 - o < 65536u) {     // in order, no overlap, near: a pitch
+                    pit += (uint32_t)(o1 - o);
+                    npit += 1u;
+                }
+            }
+            if (avail < 12u) {                                 // (too short to hold a length: none)
+                continue;
+            }
+        } else {
+            a = (uintptr_t)A.base + i * A.stride;
+            avail = A.len_u;
+        }
         const uint32_t* p = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
         const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];      // the datagram's first 12 bytes (>= 64 present)
         const uint32_t sh = (uint32_t)(a & 3u);
@@ -894,28 +924,50 @@ __device__ void pkt_plan_block(const PktBatchArgs& A) {
         const uint32_t l6 = (((w1 & 0xFFu) << 8) | ((w1 >> 8) & 0xFFu)) + 40u;   // IPv6 payload length + 40
         const uint32_t ver = (w0 >> 4) & 0xFu;
         uint32_t L = VER == 4 ? l4 : VER == 6 ? l6 : (ver == 4u ? l4 : ver == 6u ? l6 : 0u);
-        L = min(L, A.len_u);
+        L = min(L, avail);
         acc += ((uint32_t)(a & 15u) + L <= 96u) ? 0u : L;                 // in-window datagrams stream nothing
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         acc += (uint32_t)__shfl_xor((int)acc, d, 64);
+        pit += (uint32_t)__shfl_xor((int)pit, d, 64);
+        npit += (uint32_t)__shfl_xor((int)npit, d, 64);
     }
     if ((threadIdx.x & 63u) == 0u) {
-        part[threadIdx.x >> 6] = acc;
+        part[threadIdx.x >> 6][0] = acc;
+        part[threadIdx.x >> 6][1] = pit;
+        part[threadIdx.x >> 6][2] = npit;
     }
     __syncthreads();
     if (threadIdx.x == 0u) {
-        const uint32_t tot = part[0] + part[1] + part[2] + part[3];
-        const uint32_t run0 = A.plan & 0xFFu, cap = max((A.plan >> 8) & 0xFFu, 1u);
+        const uint32_t tot = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+        const uint32_t run0 = A.plan & 0xFFu;
+        uint32_t cap = max((A.plan >> 8) & 0xFFu, 1u);
         uint32_t plan;
-        if (run0 != 0u && (uint64_t)tot * 8u >= 7ull * m * A.stride) {
+        const uint32_t mean = max(tot / max(m, 1u), 64u);
+        if (!VL && run0 != 0u && (uint64_t)tot * 8u >= 7ull * m * A.stride) {
             plan = run0 << 8;                                                // form 0
         } else {
-            // runs of 8, 16 or 32: the nearest on a log scale of kPlanLiveBytes / mean
-            const uint32_t mean = max(tot / max(m, 1u), 64u);
-            const uint32_t run = mean * 45u < kPlanLiveBytes * 2u ? 32u : mean * 45u < kPlanLiveBytes * 4u ? 16u : 8u;
-            plan = 2u | (min(run, cap) << 8);
+            if (VL) {                                         // a run within the reach by the sampled pitch
+                const uint32_t pn = part[0][2] + part[1][2] + part[2][2] + part[3][2];
+                const uint64_t pt = (uint64_t)part[0][1] + part[1][1] + part[2][1] + part[3][1];
+                if (pn != 0u) {
+                    cap = min(cap, max((kLiveReach - 8192u) / max((uint32_t)(pt / pn), 1u), 1u));
+                }
+            }
+            // runs of 8, 16 or 32: the nearest on a log scale of kPlanLiveBytes / mean (offset/length:
+            // pkt_plan_vl)
+            uint32_t run = mean * 45u < kPlanLiveBytes * 2u ? 32u : mean * 45u < kPlanLiveBytes * 4u ? 16u : 8u;
+            uint32_t waves = 0u;
+            if (VL) {
+                pkt_plan_vl(mean, run, waves);
+            }
+            plan = 2u | (min(run, cap) << 8) | (waves << 4);
+            if (VL) {                                         // out of order somewhere: a wide deferred pass
+                const uint32_t pn = part[0][2] + part[1][2] + part[2][2] + part[3][2];
+                const uint32_t pairs = m - (A.n <= m ? 1u : 0u);
+                plan |= (pn + pairs / 64u < pairs) ? 8u : 0u;
+            }
         }
         // valid bit, the host's tag for this ring (a slot reused for another ring is told apart)
         const uint32_t word = 0x80000000u | (((A.plan >> 16) & 0x7FFFu) << 16) | plan;
@@ -923,22 +975,24 @@ __device__ void pkt_plan_block(const PktBatchArgs& A) {
     }
 }
 
-template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL>
+// DEF (offset/length): runs not in order within the reach are listed for the deferred pass (true) or
+// done inline, one datagram at a time (false: the kernel then carries that loop, 79-93 VGPRs, 5-6 waves
+// per SIMD — the residency the dense offset/length rings want anyway, so their ring plan takes this
+// form and no deferred pass; profiles/r5g_ring_probe_grid.jsonl).
+template <int D, bool NT, bool TX, bool REC, int VER, int BND, bool VL, bool DEF = VL>
 __global__ void __launch_bounds__(256) pkt_stream_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t bid = blockIdx.x, nblk = gridDim.x;
-    if constexpr (!VL) {
-        if (A.plan_out != nullptr) {                          // block 0: the next batch's plan
-            if (bid == 0u) {
-                pkt_plan_block<VER>(A);
-                return;
-            }
-            bid -= 1u;
-            nblk -= 1u;
+    if (A.plan_out != nullptr) {                              // block 0: the next batch's plan
+        if (bid == 0u) {
+            pkt_plan_block<VER, VL>(A);
+            return;
         }
+        bid -= 1u;
+        nblk -= 1u;
     }
     const uint32_t blk = A.xcd ? xcd_block(bid, nblk) : bid;
-    pkt_stream_run<D, NT, TX, REC, VER, BND, VL, VL>(A, spw, rec, (uint64_t)blk * 4u + w, w, threadIdx.x & 63u);
+    pkt_stream_run<D, NT, TX, REC, VER, BND, VL, DEF>(A, spw, rec, (uint64_t)blk * 4u + w, w, threadIdx.x & 63u);
 }
 
 // Second pass of the two-pass Tx: one thread per packet writes its fields (and flags) from its record.
@@ -1233,14 +1287,19 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     a.touch = stream_touch(false) ? 1u : 0u;
     a.xcd = stream_xcd(false) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n + spw - 1u) / spw;
-    const int grid = (int)((waves + 3u) / 4u) + ((a.plan_out != nullptr && !VL) ? 1 : 0);   // (+ the plan block)
-    // offset/length: the deferred pass for the runs the stream kernel listed (at most one wave per run,
-    // at most 4 blocks per CU: a batch whose every run is listed is slow, but correct)
-    const int dgrid = (int)std::min<uint64_t>((waves + 3u) / 4u, 1024u);
+    const int grid = (int)((waves + 3u) / 4u) + (a.plan_out != nullptr ? 1 : 0);   // (+ the plan block)
+    const uint32_t lds = stream_lds_bytes((int)a.res_waves);
+    // offset/length: the deferred pass (8 blocks for a ring in order, else up to one per CU: a batch
+    // whose every run is listed is slow, but correct)
+    const int dgrid = a.vl_wide ? (int)std::min<uint64_t>((waves + 3u) / 4u, 256u) : (int)std::min<uint64_t>((waves + 3u) / 4u, 8u);
     if (TX && rec != nullptr) {
-        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND, VL>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+        if (VL && a.vl_ctr == nullptr) {                      // (offset/length, inline: no deferred pass)
+            hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND, VL, false>), dim3(grid), dim3(256), lds, s, a, spw, rec);
+        } else {
+            hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND, VL>), dim3(grid), dim3(256), lds, s, a, spw, rec);
+        }
         hipError_t e = hipGetLastError();
-        if (e == hipSuccess && VL && a.vl_defer != nullptr) {
+        if (e == hipSuccess && VL && a.vl_ctr != nullptr) {
             if constexpr (VL) {
                 hipLaunchKernelGGL((pkt_vl_deferred_kernel<D, NT, TX, TX, VER, BND>), dim3(dgrid), dim3(256), 0, s, a, spw, rec);
                 e = hipGetLastError();
@@ -1250,9 +1309,13 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         e = launch_scatter<VER != 4>(a, rec, s);
         return e != hipSuccess ? e : launch_tx_flush(s);
     }
-    hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND, VL>), dim3(grid), dim3(256), stream_lds_bytes(0), s, a, spw, rec);
+    if (VL && a.vl_ctr == nullptr) {
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND, VL, false>), dim3(grid), dim3(256), lds, s, a, spw, rec);
+    } else {
+        hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, false, VER, BND, VL>), dim3(grid), dim3(256), lds, s, a, spw, rec);
+    }
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && VL && a.vl_defer != nullptr) {
+    if (e == hipSuccess && VL && a.vl_ctr != nullptr) {
         if constexpr (VL) {
             hipLaunchKernelGGL((pkt_vl_deferred_kernel<D, NT, TX, false, VER, BND>), dim3(dgrid), dim3(256), 0, s, a, spw, rec);
             e = hipGetLastError();
@@ -1310,6 +1373,9 @@ hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint3
         return hipErrorInvalidValue;
     }
     // the plan block: its candidate runs must be legal for this layout (the next batch runs them)
+    if (a.res_waves > 8u) {
+        return hipErrorInvalidValue;
+    }
     if (a.plan_out != nullptr && a.off == nullptr) {
         const uint32_t run0 = a.plan & 0xFFu, cap = (a.plan >> 8) & 0xFFu;
         if (cap == 0u || cap > kMaxRunPkts || run0 > kMaxRunPkts || 128u + (uint64_t)(cap - 1u) * a.stride + a.len_u > kLiveReach ||

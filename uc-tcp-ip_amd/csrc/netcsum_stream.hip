@@ -737,6 +737,10 @@ void set_stream_waves(int w) {
     g_stream_waves.store(w);
 }
 
+bool stream_waves_tuned() {
+    return g_stream_waves.load(std::memory_order_relaxed) >= 0;
+}
+
 uint32_t stream_lds_bytes(int auto_waves) {
     const int g = g_stream_waves.load(std::memory_order_relaxed);
     const int w = g >= 0 ? g : auto_waves;
