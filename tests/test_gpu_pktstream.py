@@ -31,6 +31,7 @@ def _defaults():
         netcsum.tune(netcsum.TUNE_TX_PASSES, 0)
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
         netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
+        netcsum.tune(netcsum.TUNE_PKT_BOUND, -1)
         netcsum.tune(netcsum.TUNE_TX_FLUSH, -1)
     reset()
     yield
@@ -332,7 +333,11 @@ def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run, copies):
     """Default run: about 20 KB of datagrams per wave for packed batches (the whole-span form 0, r2zq sweep) and
     24 KB of slots for the live-piece form 2 of other layouts (r4m ring probe), in multiples of 8, 8..64, halved while
     the batch has fewer than 2048 runs (small bursts are latency-bound); results equal the lane-group kernel's.
-    copies: the 300-datagram batch repeated (300 000 datagrams keep the full run)."""
+    copies: the 300-datagram batch repeated (300 000 datagrams keep the full run). Layouts that are not
+    packed run with TUNE_PKT_BOUND 2 here: by default their batches of >= 16 Ki datagrams take ring plans
+    (the run the previous batch on the ring sampled; tests/test_gpu_ring_layouts.py)."""
+    if stride != pkt_len:
+        netcsum.tune(netcsum.TUNE_PKT_BOUND, 2)
     rng = random.Random(stride)
     n0 = 300
     buf0 = _batch(rng, n0, stride, pkt_len, 2)

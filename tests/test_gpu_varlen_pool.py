@@ -4,11 +4,12 @@ segment per NET_BUF pool buffer at DataPtr + TransportHdrIx (/root/reference/Sou
 mix of 40 / 576 / 1500-B datagrams, against the oracle's NetUtil_16BitOnesCplChkSumDataCalc /
 ...DataVerify per segment (oracle/net_util_oracle.c).
 
-Runs in increasing address order with gaps (the pool layouts) take the live-sector form of the varlen
-stream kernel (netcsum_stream.hip seg_live_totals): only the 64-B sectors holding segment bytes are
-read; the bytes between segments are random here, so a kernel that summed any of them would disagree
-with the oracle. Reversed, shuffled, duplicated and far-apart descriptors take the other forms; empty
-segments, odd offsets and odd pseudo-header lengths are mixed in; every run length from 1 to 128."""
+The bytes between segments are random here, so a kernel that summed any of them would disagree with
+the oracle. The batch's plan (varlen_runlen_kernel) sends segments of >= 1 KiB with gaps to the
+lane-group pipe form from the second batch on the same descriptors; the rest stay in the stream
+kernel (packed runs streamed, others by 16-lane groups). Reversed, shuffled, duplicated and far-apart
+descriptors, empty segments, odd offsets and odd pseudo-header lengths are mixed in; every run length
+from 1 to 128."""
 import zlib
 
 import numpy as np
@@ -57,8 +58,10 @@ def _pool(rng, n, slot, ix, mix, order):
 @pytest.mark.parametrize("slot,ix,mix", [(1520, 34, False), (1520, 34, True), (2048, 84, False), (2048, 84, True)])
 @pytest.mark.parametrize("plen", [0, 12, 11, 40])
 def test_pool_segments_vs_oracle(order, slot, ix, mix, plen):
-    rng = np.random.default_rng(zlib.crc32(f"{order}/{slot}/{mix}/{plen}".encode()))
-    n = 3000
+    key = zlib.crc32(f"{order}/{slot}/{mix}/{plen}".encode())
+    rng = np.random.default_rng(key)
+    n = 3000 + key % 10007      # (a batch size of its own: plans are keyed on the arrays' addresses and
+                                # the count, and torch hands the next test the same addresses)
     buf, offs, lens = _pool(rng, n, slot, ix, mix, order)
     ph = rng.integers(0, 256, size=n * max(plen, 1), dtype=np.uint8) if plen else None
     b = torch.from_numpy(buf).to(DEV)
@@ -73,15 +76,19 @@ def test_pool_segments_vs_oracle(order, slot, ix, mix, plen):
         got = out.cpu().numpy().view(np.uint16) if op_ == netcsum.OP_DATA_CALC else out.cpu().numpy()
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (op_, [(int(i), int(got[i]), int(want[i]), int(offs[i]), int(lens[i])) for i in bad[:6]])
-    assert netcsum.last_launch().startswith("seg_stream_varlen_kernel"), netcsum.last_launch()
+    # the batch's plan (the sampler of the first call): segments with gaps take the lane-group pipe form
+    # from the second call on the same descriptors (16 x 6 for 1480-B segments, 8 x 8 for the mix)
+    last = netcsum.last_launch()
+    assert last.startswith("seg_stream_varlen_kernel") or last.startswith("seg_pipe_kernel"), last
+    if order == "sorted":
+        assert "plan=pool(pipe)" in last and ("G=16,K=6" if not mix else "G=8,K=8") in last, last
 
 
 @pytest.mark.parametrize("spw", [1, 2, 7, 31, 64, 65, 128])
 @pytest.mark.parametrize("depth", [4, 8])
 def test_pool_segments_every_run_length(spw, depth):
-    """Fixed runs (TUNE_TILE) of 1..128 segments in 2-KiB buffers with the mix: runs of <= 27 fit the
-    live-sector reach and take that form, longer ones (and runs of > 64 segments) the 16-lane groups;
-    4 and 8 pieces in flight."""
+    """Fixed runs (TUNE_TILE) of 1..128 segments in 2-KiB buffers with the mix (the stream kernel's
+    16-lane groups for runs with gaps), 4 and 8 pieces in flight."""
     netcsum.tune(netcsum.TUNE_TILE, spw)
     netcsum.tune(netcsum.TUNE_CHUNKS, depth)
     rng = np.random.default_rng(spw * 10 + depth)

@@ -34,7 +34,12 @@ LAYOUTS = {"pool1520": (1520, 34, False), "pool1520mix": (1520, 34, True), "pool
            "pool2kmix": (2048, 84, True), "c4": (0, 0, False)}
 VARIANTS = [("default", {}), ("pipe16", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GROUP_LANES: 16, netcsum.TUNE_CHUNKS: 6}),
             ("runs8", {netcsum.TUNE_VARLEN_RUN_BYTES: 0})]
-RESET = {netcsum.TUNE_KERNEL: 0, netcsum.TUNE_GROUP_LANES: 0, netcsum.TUNE_CHUNKS: 0, netcsum.TUNE_VARLEN_RUN_BYTES: -1}
+if os.environ.get("POOL_PIPES"):                      # lane-group pipe geometries (kernel 2)
+    for g, k, t in ((16, 6, 2), (16, 6, 8), (16, 6, 16), (32, 4, 4), (8, 8, 4), (16, 8, 4)):
+        VARIANTS.append((f"pipe{g}k{k}t{t}", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GROUP_LANES: g,
+                                              netcsum.TUNE_CHUNKS: k, netcsum.TUNE_TILE: t}))
+RESET = {netcsum.TUNE_KERNEL: 0, netcsum.TUNE_GROUP_LANES: 0, netcsum.TUNE_CHUNKS: 0, netcsum.TUNE_VARLEN_RUN_BYTES: -1,
+         netcsum.TUNE_TILE: -1}
 
 
 def main():
@@ -73,6 +78,7 @@ def main():
                 ms = events_ms(lambda: netcsum.batch_varlen(base, off_d, len_d, ph, 12, 12, n, out, netcsum.OP_DATA_CALC,
                                                             stream=st), st)
                 d = res.setdefault(tag, {"ms": [], "kernel": netcsum.last_launch()})
+                d["kernel"] = netcsum.last_launch()                 # (the plan the timed calls ran)
                 d["ms"].append(ms)
                 if tag == "default" and p == 0:
                     torch.cuda.synchronize()

@@ -454,21 +454,132 @@ private:
     bool         ordered_ = true;
 };
 
+// (NETCSUM_TUNE_STREAM_WAVES set: measurements of fixed residencies take no plans)
+static bool g_tune_stream_waves_set() {
+    return netcsum::stream_waves_tuned();
+}
+
+// ---- ring plans (netcsum_pktstream.hip pkt_plan_block): the form and run length the last batch on a
+// ring sampled for the next one. The words live in one pinned, coherent, device-mapped allocation per
+// device that is never freed (a launch still in flight may store into its word after its thread has
+// gone); each thread keeps a small table of its rings, each with a word and a tag (a word reused for
+// another ring, or a late store of an evicted one, carries another tag and is ignored).
+constexpr uint32_t kPlanWords = 4096u;
+struct PlanPool {
+    std::once_flag once;
+    uint32_t* h = nullptr;
+    uint32_t* d = nullptr;
+};
+PlanPool g_plan_pool[kMaxDev];
+std::atomic<uint32_t> g_plan_next{0};
+struct RingPlan {
+    int dev = -1;
+    const void* base = nullptr;
+    uint64_t stride = 0;
+    uint32_t pkt_len = 0, n = 0, slot = 0, tag = 0, plan = 0, use = 0, calls = 0;
+    int ip_ver = -1;
+};
+constexpr int kRingPlans = 16;
+thread_local RingPlan tls_ring_plans[kRingPlans];
+thread_local uint32_t tls_ring_clock = 0;
+
+// The plan the ring's previous batch left (0: none yet), its word (host and device addresses) and tag
+// for this batch's plan block; *d_word = nullptr when no pool could be had (the batch then runs
+// without a plan block).
+static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t pkt_len, uint32_t n, int ip_ver,
+                          uint32_t** h_word, uint32_t** d_word, uint32_t* tag, uint32_t* calls = nullptr) {
+    *h_word = *d_word = nullptr;
+    if (dev < 0 || dev >= kMaxDev) return 0u;
+    PlanPool& pool = g_plan_pool[dev];
+    std::call_once(pool.once, [&]() {
+        void* h = nullptr;
+        void* dp = nullptr;
+        if (hipHostMalloc(&h, kPlanWords * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        std::memset(h, 0, kPlanWords * sizeof(uint32_t));
+        pool.h = static_cast<uint32_t*>(h);
+        pool.d = static_cast<uint32_t*>(dp);
+    });
+    if (pool.h == nullptr) return 0u;
+    RingPlan* e = nullptr;
+    RingPlan* lru = &tls_ring_plans[0];
+    for (RingPlan& r : tls_ring_plans) {
+        if (r.dev == dev && r.base == base && r.stride == stride && r.pkt_len == pkt_len && r.n == n && r.ip_ver == ip_ver) {
+            e = &r;
+            break;
+        }
+        if (r.use < lru->use) lru = &r;
+    }
+    if (e == nullptr) {                                     // a new ring: a fresh word and tag
+        e = lru;
+        const uint32_t k = g_plan_next.fetch_add(1u);
+        *e = RingPlan{};
+        e->dev = dev;
+        e->base = base;
+        e->stride = stride;
+        e->pkt_len = pkt_len;
+        e->n = n;
+        e->ip_ver = ip_ver;
+        e->slot = k % kPlanWords;
+        e->tag = (k / kPlanWords * 2654435761u + k) & 0x7FFFu;
+    }
+    e->use = ++tls_ring_clock;
+    if (calls != nullptr) *calls = e->calls++;
+    const uint32_t w = *reinterpret_cast<volatile uint32_t*>(pool.h + e->slot);
+    if ((w >> 31) != 0u && ((w >> 16) & 0x7FFFu) == e->tag) e->plan = w & 0xFFFFu;
+    *h_word = pool.h + e->slot;
+    *d_word = pool.d + e->slot;
+    *tag = e->tag;
+    return e->plan;
+}
+
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStream_t s) {
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
-    const netcsum::LaunchCfg c = choose_cfg(dev, a0, len_hint);
+    netcsum::LaunchCfg c = choose_cfg(dev, a0, len_hint);
     netcsum::SegBatchArgs a = a0;
     if (c.kernel == 6 && c.run_bytes != 0u && a.seg_off != nullptr) {
+        // The batch's plan (varlen_runlen_kernel, keyed on its descriptor arrays like the packet rings'
+        // plans): segments with gaps between them — one per pool buffer — take the lane-group pipe
+        // form (16 lanes x 6 chunks for >= 1 KiB segments, 8 x 8 for shorter ones); every 4th batch
+        // takes the stream form with the sampler again (a plan left by other descriptors at the same
+        // addresses lasts at most 3 batches; the sampler costs a 1-block launch, ≈ 5 µs)
+        uint32_t* h_word = nullptr;
+        uint32_t* d_word = nullptr;
+        uint32_t tag = 0u, calls = 0u;
+        const uint32_t plan = ring_plan(dev, a.base, reinterpret_cast<uint64_t>(a.seg_off), 0xFFFFFFFEu, a.n_seg, -2,
+                                        &h_word, &d_word, &tag, &calls);
+        if ((plan & 3u) != 0u && (calls & 3u) != 0u && g_tune_kernel.load() == 0 && g_tune_group.load() == 0 &&
+            g_tune_chunks.load() == 0) {                 // (any of those tuned: the form asked for)
+            const int k0 = g_tune_kernel.load();
+            g_tune_kernel.store(2);
+            g_tune_group.store((plan & 3u) == 1u ? 16 : 8);   // plan 1: >= 1 KiB segments, 2: shorter
+            g_tune_chunks.store((plan & 3u) == 1u ? 6 : 8);
+            const netcsum::LaunchCfg cp = choose_cfg(dev, a0, len_hint);
+            g_tune_kernel.store(k0);
+            g_tune_group.store(0);
+            g_tune_chunks.store(0);
+            NC_HIP(netcsum::launch_seg_batch(a, cp, s));
+            char d[192];
+            snprintf(d, sizeof d, "%s plan=pool(pipe)", NetUtil_MI355X_LastLaunch());
+            netcsum::set_last_launch(d);
+            return NET_UTIL_ERR_NONE;
+        }
         // adaptive varlen runs: a one-block kernel samples the lengths and leaves the run length in
         // this stream's scratch word, which the batch kernel reads (stream order; any value is safe:
-        // the kernel never runs shorter runs than its grid covers)
+        // the kernel never runs shorter runs than its grid covers), and the plan for the next batch
         // (at +128: the packet batches keep their deferral word at +0 of the same slot)
         ScratchLease word;
         NC_HIP(word.acquire(dev, s, 256u, false));
         uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
         NC_HIP(netcsum::launch_varlen_runlen(a.seg_off, a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
-                                             c.stream_spw, run, s));
+                                             c.stream_spw, run, d_word, tag, s));
         a.run_dev = run;
         NC_HIP(netcsum::launch_seg_batch(a, c, s));
         NC_HIP(word.end());
@@ -917,90 +1028,6 @@ NET_ERR NetUtil_MI355X_CRC32Host(const void* h_data, uint32_t len, uint32_t* p_c
     NC_HIP(hipStreamSynchronize(c.stream));
     *p_crc = *reinterpret_cast<volatile uint32_t*>(c.h_sum);
     return NET_UTIL_ERR_NONE;
-}
-
-// (NETCSUM_TUNE_STREAM_WAVES set: measurements of fixed residencies take no plans)
-static bool g_tune_stream_waves_set() {
-    return netcsum::stream_waves_tuned();
-}
-
-// ---- ring plans (netcsum_pktstream.hip pkt_plan_block): the form and run length the last batch on a
-// ring sampled for the next one. The words live in one pinned, coherent, device-mapped allocation per
-// device that is never freed (a launch still in flight may store into its word after its thread has
-// gone); each thread keeps a small table of its rings, each with a word and a tag (a word reused for
-// another ring, or a late store of an evicted one, carries another tag and is ignored).
-constexpr uint32_t kPlanWords = 4096u;
-struct PlanPool {
-    std::once_flag once;
-    uint32_t* h = nullptr;
-    uint32_t* d = nullptr;
-};
-PlanPool g_plan_pool[kMaxDev];
-std::atomic<uint32_t> g_plan_next{0};
-struct RingPlan {
-    int dev = -1;
-    const void* base = nullptr;
-    uint64_t stride = 0;
-    uint32_t pkt_len = 0, n = 0, slot = 0, tag = 0, plan = 0, use = 0;
-    int ip_ver = -1;
-};
-constexpr int kRingPlans = 16;
-thread_local RingPlan tls_ring_plans[kRingPlans];
-thread_local uint32_t tls_ring_clock = 0;
-
-// The plan the ring's previous batch left (0: none yet), its word (host and device addresses) and tag
-// for this batch's plan block; *d_word = nullptr when no pool could be had (the batch then runs
-// without a plan block).
-static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t pkt_len, uint32_t n, int ip_ver,
-                          uint32_t** h_word, uint32_t** d_word, uint32_t* tag) {
-    *h_word = *d_word = nullptr;
-    if (dev < 0 || dev >= kMaxDev) return 0u;
-    PlanPool& pool = g_plan_pool[dev];
-    std::call_once(pool.once, [&]() {
-        void* h = nullptr;
-        void* dp = nullptr;
-        if (hipHostMalloc(&h, kPlanWords * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        std::memset(h, 0, kPlanWords * sizeof(uint32_t));
-        pool.h = static_cast<uint32_t*>(h);
-        pool.d = static_cast<uint32_t*>(dp);
-    });
-    if (pool.h == nullptr) return 0u;
-    RingPlan* e = nullptr;
-    RingPlan* lru = &tls_ring_plans[0];
-    for (RingPlan& r : tls_ring_plans) {
-        if (r.dev == dev && r.base == base && r.stride == stride && r.pkt_len == pkt_len && r.n == n && r.ip_ver == ip_ver) {
-            e = &r;
-            break;
-        }
-        if (r.use < lru->use) lru = &r;
-    }
-    if (e == nullptr) {                                     // a new ring: a fresh word and tag
-        e = lru;
-        const uint32_t k = g_plan_next.fetch_add(1u);
-        *e = RingPlan{};
-        e->dev = dev;
-        e->base = base;
-        e->stride = stride;
-        e->pkt_len = pkt_len;
-        e->n = n;
-        e->ip_ver = ip_ver;
-        e->slot = k % kPlanWords;
-        e->tag = (k / kPlanWords * 2654435761u + k) & 0x7FFFu;
-    }
-    e->use = ++tls_ring_clock;
-    const uint32_t w = *reinterpret_cast<volatile uint32_t*>(pool.h + e->slot);
-    if ((w >> 31) != 0u && ((w >> 16) & 0x7FFFu) == e->tag) e->plan = w & 0xFFFFu;
-    *h_word = pool.h + e->slot;
-    *d_word = pool.d + e->slot;
-    *tag = e->tag;
-    return e->plan;
 }
 
 // udp_mode: PktBatchArgs::udp_tx_csum (Tx); d_action / rx_cfg: the Rx burst actions (Rx, optional);

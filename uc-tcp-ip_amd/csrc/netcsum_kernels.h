@@ -164,10 +164,10 @@ uint32_t hdr_pieces(const SegBatchArgs& a, int h);   // 1-KiB LDS-DMA pieces per
 int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
-// Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128),
-// capped to 56 KiB / pitch and 64 for segments in increasing order with gaps (the live-sector runs).
+// Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128);
+// with plan_out, also the batch's plan (1 << 31 | tag << 16 | 1 for the lane-group pipe form) there.
 hipError_t launch_varlen_runlen(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
-                                uint32_t spw_min, uint32_t* out, hipStream_t s);
+                                uint32_t spw_min, uint32_t* out, uint32_t* plan_out, uint32_t tag, hipStream_t s);
 void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
 uint32_t varlen_run_bytes();
 constexpr uint32_t kVarlenSpwMin = 3u;

@@ -256,123 +256,14 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     store_run_results(A, s_begin, nres, lane, res0, res1);
 }
 
-// Live-sector run (a run of <= 64 segments in increasing address order, each starting at or after the
-// previous one's end, spanning <= kLiveReach from its first 128-B line): the layout the stack holds
-// its segments in — one per NET_BUF pool buffer at DataPtr + TransportHdrIx (net_util.c:1627-1628,
-// 1649; net_tcp.c:1920), 1480 B of every 2-KiB buffer, or 40 / 576 / 1500-B datagrams in 1520-B
-// buffers. As the packet kernels' live-piece form (netcsum_pktstream.hip pkt_run, bounds 1-2): lane k
-// marks segment k's 64-B sectors in a per-wave bitmap in LDS, one ballot gives the run's live 1-KiB
-// pieces, the stream pops them in address order (piece 63, never live, is the sentinel) and lane l of
-// piece q loads its 16 B only if sector l / 4 of the piece is live; the walk takes one scalar event per
-// segment end. Before the bitmap, lane k touches its segment's first dword (plain policy: the live
-// read probe's best form on sparse layouts, tools/live_read_probe.hip). Returns segment k's exact
-// half-word sum (mod 2^32) in lane k; empty segments take no part (0).
-template <int D, bool NT>
-__device__ __forceinline__ uint32_t seg_live_totals(uintptr_t O, uint32_t span, uint32_t rel, uint32_t len, bool mine,
-                                                    uint32_t w, uint32_t lane) {
-    constexpr uint64_t kSent = 1ull << 63;
-    const uint32_t lane16 = 16u * lane;
-    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
-    const bool live = mine && len != 0u;
-    const uint32_t tch = __builtin_amdgcn_raw_buffer_load_b32(rd, (int)(live ? (rel & ~3u) : kOOB), 0, 0);
-    __shared__ uint32_t sect_all[4][32];                       // 1024 sectors of 64 B per wave
-    uint32_t* sect = sect_all[w];
-    if (lane < 32u) {
-        sect[lane] = 0u;
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (live) {
-        const uint32_t s0 = rel >> 6, s1 = (rel + len - 1u) >> 6;
-        for (uint32_t d = s0 >> 5; d <= (s1 >> 5); ++d) {
-            const uint32_t lo = max(s0, d << 5) - (d << 5), hi = min(s1, (d << 5) + 31u) - (d << 5);
-            atomicOr(&sect[d], (2u << hi) - (1u << lo));       // bits lo..hi (hi = 31: 2 << 31 wraps to 0)
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t pm0 = reinterpret_cast<const uint16_t*>(sect)[lane];   // sector mask of piece `lane`
-    const uint64_t lm = __builtin_amdgcn_ballot_w64(pm0 != 0u);
-    const uint32_t nlive = (uint32_t)__builtin_popcountll(lm);
-    uint64_t lm0 = lm | kSent;
-    const uint32_t lbit = 1u << (lane >> 2);
-    auto pop = [&]() -> uint32_t {
-        const uint32_t q = (uint32_t)__builtin_ctzll(lm0);
-        lm0 = (lm0 & (lm0 - 1u)) | kSent;
-        return q;
-    };
-    auto live_voff = [&](uint32_t q) -> uint32_t {
-        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
-        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
-    };
-    u32x4 dv[D];
-    uint32_t qd[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        qd[j] = pop();
-        dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
-    }
-    uint64_t srest = __builtin_amdgcn_ballot_w64(live);
-    const bool any = srest != 0u;
-    uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
-    srest &= srest - 1u;
-    uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)rel, (int)cur);
-    uint32_t ce = any ? cs + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)cur) : ~0u;
-    uint32_t acc = 0u, tot = 0u;
-    auto consume = [&](uint32_t q, u32x4 v) {
-        const uint32_t qb = q << 10;
-        const uint32_t pend = qb + 1024u;
-        const uint32_t full = sum4(v, 0u);
-        uint32_t u = cur, c = cs, e = ce, a = acc, t = tot;
-        uint64_t rs = srest;
-        if (e > pend) {                                        // no segment ends in this piece
-            a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
-        } else {
-            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
-#pragma clang loop vectorize(disable) unroll(disable)
-            do {
-                const uint32_t Pe = piece_prefix(v, full, lane16, e <= qb ? 0u : e - qb);
-                const uint32_t T = wave_total(a + (Pe - Ps));
-                t = (lane == u) ? T : t;
-                a = 0u;
-                const bool more = rs != 0u;
-                u = more ? (uint32_t)__builtin_ctzll(rs) : 63u;
-                rs &= rs - 1u;
-                c = (uint32_t)__builtin_amdgcn_readlane((int)rel, (int)u);
-                const bool adj = c == e;
-                e = more ? c + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)u) : ~0u;
-                Ps = adj ? Pe : piece_prefix(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
-            } while (e <= pend);
-            a = full - Ps;
-        }
-        cur = u;
-        srest = rs;
-        cs = c;
-        ce = e;
-        acc = a;
-        tot = t;
-    };
-    const uint32_t rounds = (nlive + (uint32_t)D - 1u) / (uint32_t)D;
-    for (uint32_t r = 0; r < rounds; ++r) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            consume(qd[j], opaque_tuple(dv[j]));
-            qd[j] = pop();                                     // none left: the sentinel, zeros
-            dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
-            asm volatile("" ::: "memory");
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("" ::"v"(tch));
-    return tot;
-}
-
 // Variable-length batches (offset/length descriptors, config C4). A wave takes a run of segments;
 // when they are PACKED (each starts where the previous one ends — the layout of back-to-back
 // datagrams) the run is one byte stream and the wave reads it exactly like seg_stream_kernel, with
 // the segment bounds taken from the run's descriptors (held in VGPRs: lane k % 64 of slot k / 64) by
-// v_readlane; gaps of up to kMaxGap bytes between segments are read and skipped. A run in increasing
-// address order with larger gaps (segments inside pool buffers) whose span fits the live-sector reach
-// reads only its segments' 64-B sectors (seg_live_totals). Any other run (reordering, overlap, a span
-// past the reach, > 64 segments) is summed four segments at a time by 16-lane groups — always correct.
+// v_readlane; gaps of up to kMaxGap bytes between segments are read and skipped. Any other run
+// (larger gaps, reordering, overlap, a span >= 2^31) is summed four segments at a time by 16-lane
+// groups — always correct; the packed layout is the fast path. (Segments in pool buffers with larger
+// gaps: the batch's plan may take the lane-group pipe form instead, launch_batch.)
 template <int D, int PH, bool NT>
 __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, uint32_t spw) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -407,6 +298,9 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
     const uint32_t len1 = v1 ? A.seg_len_v[s_begin + 64u + lane] : 0u;
 
     uint32_t ps0 = 0u, ps1 = 0u;
+    if constexpr (PH != 0) {
+        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
+    }
     uint32_t res0 = 0u, res1 = 0u;
 
     // Packed? Segment k starts where k - 1 ends, and the run spans < 2^31 bytes.
@@ -427,35 +321,6 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end1, (int)(kl & 63u));
     const uint64_t run_end = kl < 64u ? eA : eB;
     const bool packed = __all(ok0 && ok1) && run_end >= first && run_end - first < (1ull << 31) - 256u;
-
-    // in increasing order with gaps, within the reach: the live-sector run
-    const uint32_t lead_l = (uint32_t)((base + first) & 127u);
-    const bool live_ok = !packed && nres <= 64u && __all(!v0 || lane == 0u || off0 >= prev0) && run_end >= first &&
-                         run_end - first <= (uint64_t)(kLiveReach - 128u);
-    if (live_ok) {
-        const uintptr_t O = (base + first) & ~(uintptr_t)127;
-        const uint32_t rel = v0 ? lead_l + (uint32_t)(off0 - first) : 0u;
-        const uint32_t span = lead_l + (uint32_t)(run_end - first);
-        const uint32_t T = seg_live_totals<D, NT>(O, span, rel, len0, v0, w, lane);
-        // (the pseudo-header sums after the stream: held through it, they cost the kernel a wave per
-        // SIMD of residency, 64 -> 68 VGPRs with 12-B pseudo-headers)
-        if constexpr (PH != 0) {
-            run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
-        }
-        uint32_t t = fold16(T);
-        if (((rel & 1u) != 0u) != ph_odd) {
-            t = rot8(t);
-        }
-        if constexpr (PH != 0) {
-            t = fold16(t + ps0);
-        }
-        res0 = A.verify ? (t == 0xFFFFu ? 1u : 0u) : (~t & 0xFFFFu);
-        store_run_results(A, s_begin, nres, lane, res0, 0u);
-        return;
-    }
-    if constexpr (PH != 0) {
-        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
-    }
 
     if (!packed) {
         // Scattered run: four segments at a time, a 16-lane group each (the lane-group form of
@@ -575,13 +440,18 @@ hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStrea
 }
 
 // One block: the mean of up to 4096 evenly spaced lengths -> run length for about run_bytes per run.
-// Also the pitch: the distance from a sampled segment's start to the next one's. Where the segments
-// lie in pool buffers (pitch > length + kMaxGap: the live-sector runs) a run must span <= 56 KiB and
-// hold <= 64 segments, so the run is capped to that: 2-KiB buffers, 40 / 576 / 1500-B datagrams
-// (mean 320 B) get runs of 27 instead of 49.
+// Also the pitch — the distance from a sampled segment's start to the next one's — for the batch's
+// plan (plan_out, coherent host memory, with the host's tag): segments of >= 1 KiB on average with
+// gaps of >= 32 B between them (one per pool buffer, DataPtr + TransportHdrIx) read faster in the
+// lane-group pipe form (16 lanes x 6 chunks, two segments in flight per group) than in the stream
+// kernel, whose runs with gaps over kMaxGap take its 16-lane groups one segment at a time and whose
+// packed runs read the gaps (tools/varlen_pool_probe.py, profiles/r5h_varlen_pool_probe_*.jsonl,
+// r5j_*: 1480-B segments at +84 of 2-KiB buffers 0.2512 ms against 0.2817, at +34 of 1520-B buffers
+// 0.2418 against 0.2484); shorter ones with gaps the pipe form at 8 lanes x 8 chunks (plan 2: the
+// 40 / 576 / 1500-B mix in 1520-B buffers 0.1374 against 0.1577 in the stream kernel, r5k_*).
 __global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint64_t* offs, const uint16_t* lens, uint32_t n,
                                                              uint32_t extra, uint32_t run_bytes, uint32_t spw_min,
-                                                             uint32_t* out) {
+                                                             uint32_t* out, uint32_t* plan_out, uint32_t tag) {
     __shared__ uint32_t part[16][3];
     const uint32_t m = min(n, 4096u);
     uint32_t acc = 0u, pit = 0u, npit = 0u;
@@ -618,14 +488,12 @@ __global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint64_t* off
         }
         const uint32_t mlen = m ? tot / m : 0u;
         const uint32_t mean = mlen + extra;
-        uint32_t spw = min(max(run_bytes / max(mean, 1u), spw_min), kMaxRun);
-        if (pn * 2u >= (uint64_t)m) {                          // mostly in order
-            const uint32_t pitch = (uint32_t)(ptot / pn);
-            if (pitch > mlen + (uint32_t)kMaxGap) {            // gapped: the live-sector runs
-                spw = min(spw, max(min(57344u / max(pitch, 1u), 64u), spw_min));
-            }
+        *out = min(max(run_bytes / max(mean, 1u), spw_min), kMaxRun);
+        if (plan_out != nullptr) {
+            const bool gapped = pn * 2u >= (uint64_t)m && (uint32_t)(ptot / max(pn, 1ull)) >= mlen + 32u;
+            const uint32_t word = 0x80000000u | ((tag & 0x7FFFu) << 16) | (gapped ? (mlen >= 1024u ? 1u : 2u) : 0u);
+            __hip_atomic_store(plan_out, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        *out = spw;
     }
 }
 
@@ -643,8 +511,9 @@ uint32_t varlen_run_bytes() {
 }
 
 hipError_t launch_varlen_runlen(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
-                                uint32_t spw_min, uint32_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(varlen_runlen_kernel, dim3(1), dim3(1024), 0, s, offs, lens, n, extra, run_bytes, spw_min, out);
+                                uint32_t spw_min, uint32_t* out, uint32_t* plan_out, uint32_t tag, hipStream_t s) {
+    hipLaunchKernelGGL(varlen_runlen_kernel, dim3(1), dim3(1024), 0, s, offs, lens, n, extra, run_bytes, spw_min, out,
+                       plan_out, tag);
     return hipGetLastError();
 }
 
