@@ -3,7 +3,7 @@
 # configs record (tools/bench_configs.py). usage (on the box): bash tools/gpu_pmc_all.sh TAG [configs...]
 set -o pipefail
 T=${1:?tag}; shift
-CONFIGS=${*:-c3 c4 chains rx rx6 rxmix rxb txb tx tx_nb rx_nb tx_nb2k rx_nb2k rx_nb2kv tx_nb2kv rx_ring tx_ring rx_ringv tx_ringv}
+CONFIGS=${*:-c3 c4 pool1520 pool1520mix pool2k pool2kmix chains rx rx6 rxmix rxb txb tx tx_nb rx_nb tx_nb2k rx_nb2k rx_nb2kv tx_nb2kv rx_ring tx_ring rx_ringv tx_ringv}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 for c in $CONFIGS; do
   case $c in

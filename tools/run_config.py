@@ -20,6 +20,8 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
+  pool1520 / pool1520mix / pool2k / pool2kmix  ChkSumBatchVarLen over one segment per pool buffer
+       (tools/varlen_pool_probe.py)
 Prints the launch description and the mean ms per launch (HIP events), and the algorithmic bytes."""
 import os
 import sys
@@ -103,6 +105,24 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device=dev)
         fn = lambda: netcsum.batch_varlen(base, off_d, len_d, ph, 12, 12, n, out, 0, stream=st)  # noqa: E731
         algo = total + 12 * n + 2 * n
+    elif name.startswith("pool"):
+        # ChkSumBatchVarLen over one TCP segment per NET_BUF pool buffer (tools/varlen_pool_probe.py's
+        # layouts): 1480-B or 20/556/1480-B mix segments at +34 of 1520-B / +84 of 2048-B buffers
+        from varlen_pool_probe import LAYOUTS
+        slot, ix, mix = LAYOUTS[name]
+        n = 1 << 20
+        rng = np.random.default_rng(5)
+        lens = (np.array([20, 556, 1480])[rng.choice(3, size=n, p=[7 / 12, 4 / 12, 1 / 12])] if mix
+                else np.full(n, 1480)).astype(np.uint16)
+        offs = (np.arange(n, dtype=np.uint64) * np.uint64(slot) + np.uint64(ix)).astype(np.uint64)
+        base = torch.empty(n * slot + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(base, n * slot, SEED, 0)
+        ph = torch.from_numpy(rng.integers(0, 256, size=n * 12, dtype=np.uint8)).to(dev)
+        off_d = torch.from_numpy(offs.view(np.int64)).to(dev)
+        len_d = torch.from_numpy(lens.view(np.int16)).to(dev)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        fn = lambda: netcsum.batch_varlen(base, off_d, len_d, ph, 12, 12, n, out, 0, stream=st)  # noqa: E731
+        algo = int(lens.astype(np.int64).sum()) + 14 * n
     elif name == "chains":
         nc, per, B = 1 << 14, 45, 2048
         plen = np.full(per, 1480, np.uint16)
