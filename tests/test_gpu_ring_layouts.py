@@ -207,22 +207,28 @@ def test_bounded_stream_full_size_ring_properties():
     assert (np.delete(fl, k) & 0x07 == 0x07).all()
 
 
-@pytest.mark.parametrize("order", ["sorted", "reversed", "shuffled", "duplicates", "far", "packed"])
-@pytest.mark.parametrize("spw", [-1, 1, 7, 64])
+@pytest.mark.parametrize("order", ["sorted", "reversed", "shuffled", "duplicates", "far", "packed", "pairs"])
+@pytest.mark.parametrize("spw", [-1, 1, 7, 32, 64])
 @pytest.mark.parametrize("bound", [1, 2, 4])
 def test_offset_length_runs_every_order_vs_oracle(order, spw, bound):
     """Offset/length batches in the live-piece stream (netcsum_pktstream.hip, VL): a run of
     descriptors in increasing address order within the bitmap's reach streams; any other run (reversed
-    or shuffled rings, the same datagram listed twice, slots > 128 KiB apart) is listed for the deferred
-    pass, which does it datagram by datagram. Bound 4: ring plans (the plan block samples the
-    descriptors; run length and residency for the next batch). Mixed IPv4 / IPv6 (RxValidateIP,
-    TxFinalizeIP, RxBurst), results equal the oracle's; each batch twice (the second in the plan)."""
+    or shuffled rings, the same datagram listed twice, slots > 128 KiB apart, neighbours swapped, runs
+    of 32 / 64 slots that outgrow the 63-KiB reach) is listed for the deferred pass, which streams it in
+    ordered sub-runs inside the reach (a datagram out of order: a sub-run of one). Bound 4: ring plans
+    (the plan block samples the descriptors; run length and residency for the next batch). Mixed IPv4 /
+    IPv6 (RxValidateIP, TxFinalizeIP, RxBurst), 1520-B slots (2-KiB slots for runs of 32), results
+    equal the oracle's; each batch twice (the second in the plan)."""
     netcsum.tune(netcsum.TUNE_TILE, spw)
     netcsum.tune(netcsum.TUNE_PKT_BOUND, bound)
     rng = random.Random(zlib.crc32(f"{order}/{spw}".encode()))
-    n, slot, lead = 700, 1520, 14
+    n, slot, lead = 700, (2048 if spw == 32 else 1520), 14
     buf, lens = _ring(rng, n, slot, lead, v6mix=True)
     offs = np.arange(n, dtype=np.int64) * slot + lead
+    if order == "pairs":                                          # neighbours 3 <-> 4 of every 10 swapped
+        i = np.arange(3, n - 1, 10)
+        offs[i], offs[i + 1] = offs[i + 1].copy(), offs[i].copy()
+        lens[i], lens[i + 1] = lens[i + 1].copy(), lens[i].copy()
     if order == "reversed":
         offs, lens = offs[::-1].copy(), lens[::-1].copy()
     elif order == "shuffled":

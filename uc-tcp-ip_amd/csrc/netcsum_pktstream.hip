@@ -823,11 +823,12 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
 }
 
 // The deferred pass of an offset/length batch: the runs its stream kernel listed (A.vl_list, count in
-// A.vl_ctr[0]), one datagram at a time as a run of one, waves taking list entries round-robin; the
+// A.vl_ctr[0]), each in ordered sub-runs inside the reach, waves taking list entries round-robin; the
 // last block to finish leaves the count and its own counter zero for the next batch on the stream.
 // Launched after the stream kernel in stream order (and before two-pass Tx's scatter): 8 blocks when
 // the ring's plan found its descriptors in order (a run listed anyway, e.g. where the ring wraps, is
-// still done), 256 otherwise (the ring's first batch, reordered rings).
+// still done), one per 4 runs up to 2048 otherwise (the ring's first batch, reordered rings, runs
+// asked for that outgrow the reach).
 template <int D, bool NT, bool TX, bool REC, int VER, int BND>
 __global__ void __launch_bounds__(256) pkt_vl_deferred_kernel(PktBatchArgs A, uint32_t spw, PktTxRecord* rec) {
     __shared__ uint32_t s_last;
@@ -835,22 +836,47 @@ __global__ void __launch_bounds__(256) pkt_vl_deferred_kernel(PktBatchArgs A, ui
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t runs = (uint32_t)(((uint64_t)A.n + spw - 1u) / spw);
     const uint32_t count = min(*A.vl_ctr, runs);
-    for (uint32_t i = blockIdx.x * 4u + w; i < count; i += gridDim.x * 4u) {
+    // the blocks the list needs (4 entries each at first); the rest leave at once, touching nothing,
+    // so the grid can be sized for a whole batch deferred at the cost of one load per idle block (a
+    // block that reads the count after the reset below reads 0 and leaves too)
+    const uint32_t active = min(gridDim.x, (count + 3u) / 4u);
+    if (blockIdx.x >= active) {
+        return;
+    }
+    for (uint32_t i = blockIdx.x * 4u + w; i < count; i += active * 4u) {
         const uint32_t r = A.vl_list[i];
         const uint32_t s_begin = r * spw;
         const uint32_t nres = r < runs ? min(A.n - s_begin, spw) : 0u;
-        for (uint32_t k = 0; k < nres; ++k) {
-            const uint64_t ok_ = A.off[s_begin + k];
-            const uint32_t lk = A.len[s_begin + k];
-            const uintptr_t Ok = ((uintptr_t)A.base + ok_) & ~(uintptr_t)127;
-            const uint32_t pk = (uint32_t)((uintptr_t)A.base + ok_ - Ok);
-            pkt_run<D, NT, TX, REC, VER, BND, true>(A, rec, w, lane, s_begin + k, 1u, Ok, pk, lk, pk + lk);
+        // the run in sub-runs: from datagram k0, the longest prefix in order and inside the reach of
+        // k0's 128-B line streams as one wave run (a run that only outgrew the reach — runs of 32 in
+        // 2-KiB slots — costs two streamed sub-runs, not 32 prologues); a datagram out of order, or
+        // past the reach on its own, is a sub-run of one (`wide` in pkt_run)
+        for (uint32_t k0 = 0; k0 < nres;) {
+            const uint32_t idx = k0 + lane;
+            const bool mine = idx < nres;
+            const uint64_t off = A.off[s_begin + (mine ? idx : k0)];
+            const uint32_t len = mine ? (uint32_t)A.len[s_begin + idx] : 0u;
+            const uint64_t off0 = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(off >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off);
+            const uintptr_t O = ((uintptr_t)A.base + off0) & ~(uintptr_t)127;
+            const uint64_t rel = (uintptr_t)A.base + off - O;
+            const uint64_t end = rel + len;
+            const uint32_t prev_end_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
+            const bool ok = mine && rel < kLiveReach && end <= kLiveReach - 128u &&
+                            (lane == 0u || (uint64_t)prev_end_lo <= rel);
+            const uint64_t cut = ~__builtin_amdgcn_ballot_w64(ok);
+            const uint32_t m = max(cut ? (uint32_t)__builtin_ctzll(cut) : 64u, 1u);
+            const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(m - 1u));
+            const bool in = lane < m;
+            pkt_run<D, NT, TX, REC, VER, BND, true>(A, rec, w, lane, s_begin + k0, m, O, in ? (uint32_t)rel : 0u,
+                                                    in ? len : 0u, span);
+            k0 += m;
         }
     }
     __syncthreads();
     if (threadIdx.x == 0u) {
-        s_last = __hip_atomic_fetch_add(A.vl_ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
-        if (s_last) {                                           // every block has read the count
+        s_last = __hip_atomic_fetch_add(A.vl_ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == active - 1u;
+        if (s_last) {                                           // every active block has read the count
             __hip_atomic_store(A.vl_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(A.vl_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1291,7 +1317,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     const uint32_t lds = stream_lds_bytes((int)a.res_waves);
     // offset/length: the deferred pass (8 blocks for a ring in order, else up to one per CU: a batch
     // whose every run is listed is slow, but correct)
-    const int dgrid = a.vl_wide ? (int)std::min<uint64_t>((waves + 3u) / 4u, 256u) : (int)std::min<uint64_t>((waves + 3u) / 4u, 8u);
+    const int dgrid = a.vl_wide ? (int)std::min<uint64_t>((waves + 3u) / 4u, 2048u) : (int)std::min<uint64_t>((waves + 3u) / 4u, 8u);
     if (TX && rec != nullptr) {
         if (VL && a.vl_ctr == nullptr) {                      // (offset/length, inline: no deferred pass)
             hipLaunchKernelGGL((pkt_stream_kernel<D, NT, TX, TX, VER, BND, VL, false>), dim3(grid), dim3(256), lds, s, a, spw, rec);
