@@ -609,14 +609,17 @@ typedef enum netcsum_tune_key {
                                          auto: the most that fit 4 KiB from any 128-B lead, 192 for
                                          20-B headers). Chain batches: 1 = the wave-per-chain form
                                          (default: two passes, see (2c))                            */
-    NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8       */
+    NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8;
+                                         run-stream kernels: 1-KiB pieces in flight (4 / 8)        */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),
                                          2 run-stream form of the checksum kernels (24-KiB runs per
                                          wave, 4 nt pieces in flight, row touch, 5 waves per SIMD)  */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
     NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).
-                                         Kernel 6: J > 0 = segments per wave run (<= 128; auto 16).
+                                         Kernel 6: J > 0 = segments per wave run (<= 128; auto 16);
+                                         varlen batches whose plan is the live-sector stream (segments
+                                         one per pool buffer): its runs (<= 64; auto from the plan).
                                          Kernel 7: headers per lane, 1, 2 or 4 (auto 2).
                                          IPv4 packet batches: packets per wave run of the run-stream
                                          form (<= 64; auto 8); TUNE_KERNEL 2 forces the lane-group

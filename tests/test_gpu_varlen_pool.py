@@ -5,11 +5,12 @@ mix of 40 / 576 / 1500-B datagrams, against the oracle's NetUtil_16BitOnesCplChk
 ...DataVerify per segment (oracle/net_util_oracle.c).
 
 The bytes between segments are random here, so a kernel that summed any of them would disagree with
-the oracle. The batch's plan (varlen_runlen_kernel) sends segments of >= 1 KiB with gaps to the
-lane-group pipe form from the second batch on the same descriptors; the rest stay in the stream
-kernel (packed runs streamed, others by 16-lane groups). Reversed, shuffled, duplicated and far-apart
-descriptors, empty segments, odd offsets and odd pseudo-header lengths are mixed in; every run length
-from 1 to 128."""
+the oracle. The batch's plan (varlen_runlen_kernel) sends segments with gaps in address order to the
+live-sector stream (seg_live_varlen_kernel: only the 64-B sectors holding segment bytes are read)
+from the second batch on the same descriptors; its runs out of order or past the 63-KiB reach take
+16-lane groups. Other layouts stay in the stream kernel (packed runs streamed, others by 16-lane
+groups). Reversed, shuffled, duplicated and far-apart descriptors, empty segments, odd offsets and odd
+pseudo-header lengths are mixed in; every run length from 1 to 128."""
 import zlib
 
 import numpy as np
@@ -68,40 +69,58 @@ def test_pool_segments_vs_oracle(order, slot, ix, mix, plen):
     o = torch.from_numpy(offs.view(np.int64)).to(DEV)
     ln = torch.from_numpy(lens.view(np.int16)).to(DEV)
     p = torch.from_numpy(ph).to(DEV) if plen else None
-    for op_ in (netcsum.OP_DATA_CALC, netcsum.OP_DATA_VERIFY):
-        want = oracle.batch_varlen(buf, offs, lens, ph, plen, plen, op_)
+    want_c = oracle.batch_varlen(buf, offs, lens, ph, plen, plen, netcsum.OP_DATA_CALC)
+    want_v = oracle.batch_varlen(buf, offs, lens, ph, plen, plen, netcsum.OP_DATA_VERIFY)
+    launches = []
+    for op_ in (netcsum.OP_DATA_CALC, netcsum.OP_DATA_VERIFY, netcsum.OP_DATA_CALC):
+        want = want_c if op_ == netcsum.OP_DATA_CALC else want_v
         out = torch.zeros(n * (2 if op_ == netcsum.OP_DATA_CALC else 1), dtype=torch.uint8, device=DEV)
         netcsum.batch_varlen(b, o, ln, p, plen, plen, n, out, op_)
         torch.cuda.synchronize()
+        launches.append(netcsum.last_launch())
         got = out.cpu().numpy().view(np.uint16) if op_ == netcsum.OP_DATA_CALC else out.cpu().numpy()
         bad = np.nonzero(got != want)[0]
-        assert bad.size == 0, (op_, [(int(i), int(got[i]), int(want[i]), int(offs[i]), int(lens[i])) for i in bad[:6]])
-    # the batch's plan (the sampler of the first call): segments with gaps take the lane-group pipe form
-    # from the second call on the same descriptors (16 x 6 for 1480-B segments, 8 x 8 for the mix)
-    last = netcsum.last_launch()
-    assert last.startswith("seg_stream_varlen_kernel") or last.startswith("seg_pipe_kernel"), last
+        assert bad.size == 0, (op_, launches[-1], [(int(i), int(got[i]), int(want[i]), int(offs[i]), int(lens[i]))
+                                                   for i in bad[:6]])
+    # the batch's plan (the sampler of the first call): segments with gaps in address order take the
+    # live-sector stream from the second call on the same descriptors (runs of 16 at depth 8 for 1480-B
+    # segments, of 32 (30 in 2-KiB buffers) at depth 4 for the mix); its own sampler block keeps it
+    for last in launches:
+        assert last.split("<")[0] in ("seg_stream_varlen_kernel", "seg_live_varlen_kernel", "seg_pipe_kernel"), last
     if order == "sorted":
-        assert "plan=pool(pipe)" in last and ("G=16,K=6" if not mix else "G=8,K=8") in last, last
+        for last in launches[1:]:
+            run = 16 if not mix else (32 if slot == 1520 else 30)
+            assert "plan=pool(live)" in last and f"D={8 if not mix else 4}" in last, last
+            assert f"segs_per_wave={run}" in last, last
 
 
 @pytest.mark.parametrize("spw", [1, 2, 7, 31, 64, 65, 128])
 @pytest.mark.parametrize("depth", [4, 8])
-def test_pool_segments_every_run_length(spw, depth):
-    """Fixed runs (TUNE_TILE) of 1..128 segments in 2-KiB buffers with the mix (the stream kernel's
-    16-lane groups for runs with gaps), 4 and 8 pieces in flight."""
+@pytest.mark.parametrize("order", ["sorted", "duplicates"])
+def test_pool_segments_every_run_length(spw, depth, order):
+    """Fixed runs (TUNE_TILE) of 1..128 segments in 2-KiB buffers with the mix, 4 and 8 pieces in flight:
+    the first call in the stream kernel (its 16-lane groups for runs with gaps), the second in the
+    live-sector stream of the batch's plan at that run length (<= 64; past it the plan's) — with some
+    descriptors listed twice, its runs that hold them take the 16-lane groups."""
     netcsum.tune(netcsum.TUNE_TILE, spw)
     netcsum.tune(netcsum.TUNE_CHUNKS, depth)
     rng = np.random.default_rng(spw * 10 + depth)
-    n = 2000
-    buf, offs, lens = _pool(rng, n, 2048, 84, True, "sorted")
+    n = 2000 + spw * 3 + depth + (7 if order == "duplicates" else 0)
+    buf, offs, lens = _pool(rng, n, 2048, 84, True, order)
     ph = rng.integers(0, 256, size=n * 12, dtype=np.uint8)
     want = oracle.batch_varlen(buf, offs, lens, ph, 12, 12, netcsum.OP_DATA_CALC)
-    out = torch.zeros(n, dtype=torch.int16, device=DEV)
-    netcsum.batch_varlen(torch.from_numpy(buf).to(DEV), torch.from_numpy(offs.view(np.int64)).to(DEV),
-                         torch.from_numpy(lens.view(np.int16)).to(DEV), torch.from_numpy(ph).to(DEV), 12, 12, n, out,
-                         netcsum.OP_DATA_CALC)
-    torch.cuda.synchronize()
-    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    args = (torch.from_numpy(buf).to(DEV), torch.from_numpy(offs.view(np.int64)).to(DEV),
+            torch.from_numpy(lens.view(np.int16)).to(DEV), torch.from_numpy(ph).to(DEV))
+    for call in range(2):
+        out = torch.zeros(n, dtype=torch.int16, device=DEV)
+        netcsum.batch_varlen(*args, 12, 12, n, out, netcsum.OP_DATA_CALC)
+        torch.cuda.synchronize()
+        last = netcsum.last_launch()
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), want), (call, last)
+    if spw <= 64:
+        assert "plan=pool(live)" in last and f"D={depth}" in last and f"segs_per_wave={spw}" in last, last
+    else:                                                                # past the live form's runs
+        assert last.startswith("seg_stream_varlen_kernel"), last
 
 
 def test_pool_segments_full_size_properties():

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                             \
@@ -60,8 +61,10 @@ __global__ void fill_kernel(u32x4* p, uint64_t n16) {
     }
 }
 
-// bit s of bits: sector s (bytes [64 s, 64 s + 64) of the ring) holds datagram bytes
-__global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, uint32_t lead, uint32_t len) {
+// bit s of bits: sector s (bytes [64 s, 64 s + 64) of the ring) holds datagram bytes (slot i's length:
+// lens[i], or `len` for every slot when lens is null)
+__global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, uint32_t lead, uint32_t len,
+                               const uint16_t* lens, uint32_t n) {
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w * 32u >= nsect) return;
     uint32_t m = 0;
@@ -70,7 +73,7 @@ __global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, 
         const uint64_t a = s0 / stride;
         bool live = false;
         for (uint64_t i = a; i <= (s1 - 1u) / stride; ++i) {
-            const uint64_t d0 = i * stride + lead, d1 = d0 + len;
+            const uint64_t d0 = i * stride + lead, d1 = d0 + (lens ? (i < n ? lens[i] : 0u) : len);
             live = live || (s0 < d1 && d0 < s1);
         }
         m |= live ? (1u << b) : 0u;
@@ -152,27 +155,44 @@ int main(int argc, char** argv) {
         const char* name;
         uint64_t stride;
         uint32_t lead, len;
+        bool mix;
     };
     // default: the packet rows' rings; or layouts from the command line as NAME STRIDE LEAD LEN ...
     // (round 5: TCP segments at TransportHdrIx of pool buffers, `seg1520 1520 34 1480`, `seg2k 2048 84
-    // 1480`, and the chain row's fragments, `frag2k 2048 42 1480`)
-    std::vector<Layout> layouts = {{"packed", 1500, 0, 1500}, {"template", 1520, 14, 1500}, {"nb2k", 2048, 64, 1500}};
+    // 1480`, and the chain row's fragments, `frag2k 2048 42 1480`; LEN `mix`: segments of 20 / 556 /
+    // 1480 B at 7 : 4 : 1 — the 40 / 576 / 1500-B datagram mix — drawn per slot, `seg1520mix 1520 34 mix`)
+    std::vector<Layout> layouts = {{"packed", 1500, 0, 1500, false}, {"template", 1520, 14, 1500, false},
+                                   {"nb2k", 2048, 64, 1500, false}};
     if (argc > 1) {
         layouts.clear();
         for (int i = 1; i + 3 < argc; i += 4) {
             const uint64_t st = std::strtoull(argv[i + 1], nullptr, 10);
-            const uint32_t ld = (uint32_t)std::strtoul(argv[i + 2], nullptr, 10), ln = (uint32_t)std::strtoul(argv[i + 3], nullptr, 10);
+            const bool mix = std::string(argv[i + 3]) == "mix";
+            const uint32_t ld = (uint32_t)std::strtoul(argv[i + 2], nullptr, 10),
+                           ln = mix ? 1480u : (uint32_t)std::strtoul(argv[i + 3], nullptr, 10);
             if (st == 0 || st > 2048u || ld + ln > st) {
                 std::fprintf(stderr, "layout %s: need stride <= 2048 and lead + len <= stride\n", argv[i]);
                 return 2;
             }
-            layouts.push_back({argv[i], st, ld, ln});
+            layouts.push_back({argv[i], st, ld, ln, mix});
         }
     }
     const uint32_t n = 1u << 20;
     const uint64_t ring_bytes = (uint64_t)n * 2048u + 4096u;
     uint8_t* ring = nullptr;
     uint32_t *bits = nullptr, *sink = nullptr;
+    uint16_t* dlens = nullptr;
+    std::vector<uint16_t> hmix(n);
+    {
+        uint64_t x = 0x5EED0001ull;                                      // 20 / 556 / 1480 B at 7 : 4 : 1
+        for (uint32_t i = 0; i < n; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            const uint32_t r = (uint32_t)(x >> 33) % 12u;
+            hmix[i] = r < 7u ? 20u : r < 11u ? 556u : 1480u;
+        }
+    }
+    CK(hipMalloc(&dlens, (size_t)n * 2u));
+    CK(hipMemcpy(dlens, hmix.data(), (size_t)n * 2u, hipMemcpyHostToDevice));
     CK(hipMalloc(&ring, ring_bytes));
     CK(hipMalloc(&bits, ring_bytes / 64u / 8u + 1024u));
     CK(hipMemset(bits, 0, ring_bytes / 64u / 8u + 1024u));
@@ -185,7 +205,12 @@ int main(int argc, char** argv) {
         const uint64_t bytes = (uint64_t)n * L.stride + 4096u;
         const uint64_t nsect = bytes / 64u;
         hipLaunchKernelGGL(sectors_kernel, dim3((unsigned)((nsect / 32u + 256u) / 256u)), dim3(256), 0, 0, bits, nsect,
-                           L.stride, L.lead, L.len);
+                           L.stride, L.lead, L.len, L.mix ? dlens : nullptr, n);
+        uint64_t dbytes = (uint64_t)n * L.len;
+        if (L.mix) {
+            dbytes = 0;
+            for (uint16_t m : hmix) dbytes += m;
+        }
         CK(hipDeviceSynchronize());
         std::vector<uint32_t> hb(nsect / 32u);
         CK(hipMemcpy(hb.data(), bits, hb.size() * 4u, hipMemcpyDeviceToHost));
@@ -224,11 +249,11 @@ int main(int argc, char** argv) {
                     }
                     CK(hipGetLastError());
                     std::sort(t.begin(), t.end());
-                    const double ms = t[10], dgram = (double)n * L.len;
+                    const double ms = t[10], dgram = (double)dbytes;
                     std::printf("{\"layout\": \"%s\", \"stride\": %llu, \"lead\": %u, \"len\": %u, \"form\": \"%s\", \"run\": %u, "
                                 "\"pass\": %d, \"ms\": %.4f, \"datagram_GBps\": %.1f, \"frac_of_8TBps\": %.4f, "
                                 "\"sector_bytes\": %llu, \"sector_GBps\": %.1f}\n",
-                                L.name, (unsigned long long)L.stride, L.lead, L.len, v.tag, R, pass, ms,
+                                L.name, (unsigned long long)L.stride, L.lead, L.mix ? 0u : L.len, v.tag, R, pass, ms,
                                 dgram / ms / 1e6, dgram / ms / 1e6 / 8000.0, (unsigned long long)(live * 64u),
                                 (v.live ? (double)live * 64.0 : (double)n * L.stride) / ms / 1e6);
                     std::fflush(stdout);
@@ -239,5 +264,6 @@ int main(int argc, char** argv) {
     CK(hipFree(ring));
     CK(hipFree(bits));
     CK(hipFree(sink));
+    CK(hipFree(dlens));
     return 0;
 }

@@ -544,18 +544,37 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
     NC_HIP(hipGetDevice(&dev));
     netcsum::LaunchCfg c = choose_cfg(dev, a0, len_hint);
     netcsum::SegBatchArgs a = a0;
-    if (c.kernel == 6 && c.run_bytes != 0u && a.seg_off != nullptr) {
-        // The batch's plan (varlen_runlen_kernel, keyed on its descriptor arrays like the packet rings'
-        // plans): segments with gaps between them — one per pool buffer — take the lane-group pipe
-        // form (16 lanes x 6 chunks for >= 1 KiB segments, 8 x 8 for shorter ones); every 4th batch
-        // takes the stream form with the sampler again (a plan left by other descriptors at the same
-        // addresses lasts at most 3 batches; the sampler costs a 1-block launch, ≈ 5 µs)
+    const int tile_k = g_tune_tile.load();
+    const bool fixed = c.run_bytes == 0u && tile_k >= 1 && tile_k <= 64;    // TUNE_TILE: fixed runs, both forms
+    if (c.kernel == 6 && a.seg_off != nullptr && (c.run_bytes != 0u || fixed)) {
+        // The batch's plan (varlen_runlen_kernel / the live kernel's sampler block, keyed on its
+        // descriptor arrays like the packet rings' plans). Segments with gaps between them — one per
+        // pool buffer — in address order take the live-sector stream (plan 3: seg_live_varlen_kernel,
+        // the plan's run length and depth; TUNE_TILE 1..64 / TUNE_CHUNKS 4 or 8 override them), which
+        // samples the descriptors again in one extra block, so the plan follows the descriptors from
+        // batch to batch. Pools too sparse for it take the lane-group pipe form (16 lanes x 6 chunks
+        // for >= 1 KiB segments, 8 x 8 for shorter ones), every 4th batch the stream form with the
+        // sampler again (a plan left by other descriptors at the same addresses lasts at most 3
+        // batches; the sampler costs a 1-block launch, ≈ 5 µs).
         uint32_t* h_word = nullptr;
         uint32_t* d_word = nullptr;
         uint32_t tag = 0u, calls = 0u;
         const uint32_t plan = ring_plan(dev, a.base, reinterpret_cast<uint64_t>(a.seg_off), 0xFFFFFFFEu, a.n_seg, -2,
                                         &h_word, &d_word, &tag, &calls);
-        if ((plan & 3u) != 0u && (calls & 3u) != 0u && g_tune_kernel.load() == 0 && g_tune_group.load() == 0 &&
+        if ((plan & 3u) == 3u && d_word != nullptr && g_tune_kernel.load() == 0 && g_tune_group.load() == 0) {
+            const int ch = g_tune_chunks.load();
+            const uint32_t spw = fixed ? (uint32_t)tile_k : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (plan >> 8) & 0xFFu));
+            const int depth = (ch == 4 || ch == 8) ? ch : ((plan & 4u) ? 8 : 4);
+            a.plan_out = d_word;
+            a.plan_tag = tag;
+            NC_HIP(netcsum::launch_live_varlen(a, depth, spw, s));
+            char d[192];
+            snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d%s,nt> block=256 segs_per_wave=%u plan=pool(live)", depth,
+                     (a.pseudo && a.pseudo_len) ? ",pseudo" : "", spw);
+            netcsum::set_last_launch(d);
+            return NET_UTIL_ERR_NONE;
+        }
+        if (!fixed && (plan & 3u) != 0u && (plan & 3u) != 3u && (calls & 3u) != 0u && g_tune_kernel.load() == 0 && g_tune_group.load() == 0 &&
             g_tune_chunks.load() == 0) {                 // (any of those tuned: the form asked for)
             const int k0 = g_tune_kernel.load();
             g_tune_kernel.store(2);
@@ -580,7 +599,7 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
         NC_HIP(netcsum::launch_varlen_runlen(a.seg_off, a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
                                              c.stream_spw, run, d_word, tag, s));
-        a.run_dev = run;
+        a.run_dev = fixed ? nullptr : run;                 // (fixed runs: the sampler for the plan only)
         NC_HIP(netcsum::launch_seg_batch(a, c, s));
         NC_HIP(word.end());
         return NET_UTIL_ERR_NONE;

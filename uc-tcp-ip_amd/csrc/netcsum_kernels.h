@@ -32,6 +32,8 @@ struct SegBatchArgs {
     uint32_t        xcd;           // stream kernels: XCD-aware block order (set by the launcher)
     const uint32_t* run_dev;       // varlen stream kernel: run length chosen on the device (used when
                                    // larger than the launch's), nullptr = the launch's
+    uint32_t*       plan_out;      // varlen live kernel: the batch's plan for the next batch on the same
+    uint32_t        plan_tag;      // descriptors (an extra sampler block), nullptr = none
 };
 
 struct LaunchCfg {
@@ -165,9 +167,15 @@ int hdr_occupancy(const SegBatchArgs& a, int stages, int h);
 bool hdrstream_supported(const SegBatchArgs& a);                  // kernel 8: packed 16 / 20-B headers
 hipError_t launch_hdrstream(const SegBatchArgs& a, int depth, uint32_t spw, bool nt, hipStream_t s);
 // Varlen run length from sampled lengths: *out = clamp(run_bytes / (mean length + extra), spw_min, 128);
-// with plan_out, also the batch's plan (1 << 31 | tag << 16 | 1 for the lane-group pipe form) there.
+// with plan_out, also the batch's plan there: 1 << 31 | tag << 16 | form (0 the stream kernel; 1 / 2
+// the lane-group pipe at 16 x 6 / 8 x 8, for sparse pools; 3 the live-sector stream, run << 8, bit 2
+// depth 8).
 hipError_t launch_varlen_runlen(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t extra, uint32_t run_bytes,
                                 uint32_t spw_min, uint32_t* out, uint32_t* plan_out, uint32_t tag, hipStream_t s);
+// Segments one per pool buffer (plan 3): the live-sector stream (netcsum_stream.hip
+// seg_live_varlen_kernel), runs of spw <= 64 segments, depth 4 or 8 pieces in flight; a.plan_out:
+// one extra block samples the descriptors for the next batch's plan.
+hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hipStream_t s);
 void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
 uint32_t varlen_run_bytes();
 constexpr uint32_t kVarlenSpwMin = 3u;

@@ -423,6 +423,283 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
     store_run_results(A, s_begin, nres, lane, res0, res1);
 }
 
+// The plan word from the sampled mean length, mean pitch (of the pn in-order pairs of m samples):
+// segments with gaps of >= 32 B between them, mostly in order, take the live-sector stream
+// (seg_live_varlen_kernel): runs of 32 below a 455-B mean length, else 16, 8 pieces in flight from a
+// 910-B mean (tools/varlen_pool_probe.py POOL_LIVE over the pool layouts, profiles/r5s_*: 1480-B
+// segments fastest in runs of 16 at depth 8, the 20 / 556 / 1480-B mix in runs of 32 at depth 4),
+// capped so a run's slots span < 61 KiB; pools too sparse for runs of 4 take the lane-group pipe
+// form (1: 16 x 6 for >= 1 KiB segments, 2: 8 x 8).
+__device__ __forceinline__ uint32_t varlen_plan_word(uint32_t mlen, uint64_t ptot, uint64_t pn, uint32_t m, uint32_t tag) {
+    const uint32_t pitch = (uint32_t)(ptot / max(pn, 1ull));
+    const bool gapped = pn * 2u >= (uint64_t)m && pitch >= mlen + 32u;
+    uint32_t form = 0u;
+    if (gapped) {
+        const uint32_t cap = (kLiveReach - 2048u) / max(pitch, 1u);
+        const uint32_t run = min(mlen * 45u < 20480u ? 32u : 16u, cap);
+        form = run >= 4u ? (3u | (mlen * 45u >= 40960u ? 4u : 0u) | (run << 8)) : (mlen >= 1024u ? 1u : 2u);
+    }
+    return 0x80000000u | ((tag & 0x7FFFu) << 16) | form;
+}
+
+// Sampling by one block of NTH threads (NTH / 64 waves): the mean of up to 4096 evenly spaced
+// lengths and the mean in-order pitch; thread 0 returns the sums.
+template <int NTH>
+__device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t m,
+                                              uint32_t (&part)[NTH / 64][3], uint32_t& tot, uint64_t& ptot, uint64_t& pn) {
+    uint32_t acc = 0u, pit = 0u, npit = 0u;
+    for (uint32_t j = threadIdx.x; j < m; j += (uint32_t)NTH) {
+        const uint32_t i = (uint32_t)(((uint64_t)j * n) / m);
+        acc += lens[i];
+        if (i + 1u < n) {
+            const uint64_t a = offs[i], b = offs[i + 1u];
+            if (b > a && b - a < 65536u) {                     // in order and near: a pitch
+                pit += (uint32_t)(b - a);
+                npit += 1u;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        acc += (uint32_t)__shfl_xor((int)acc, d, 64);
+        pit += (uint32_t)__shfl_xor((int)pit, d, 64);
+        npit += (uint32_t)__shfl_xor((int)npit, d, 64);
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        part[threadIdx.x >> 6][0] = acc;
+        part[threadIdx.x >> 6][1] = pit;
+        part[threadIdx.x >> 6][2] = npit;
+    }
+    __syncthreads();
+    tot = 0u;
+    ptot = 0u;
+    pn = 0u;
+    if (threadIdx.x == 0u) {
+        for (int i = 0; i < NTH / 64; ++i) {
+            tot += part[i][0];
+            ptot += part[i][1];
+            pn += part[i][2];
+        }
+    }
+}
+
+// Segments one per pool buffer (DataPtr + TransportHdrIx of 1520-B or 2-KiB NET_BUFs, net_util.c:1627-1628,
+// 1649; net_tcp.c:1920): in address order, with gaps between them. The packed form above reads the
+// gaps (or, past kMaxGap, leaves the run to its 16-lane groups); here a wave reads only the 64-B
+// sectors that hold segment bytes, as the packet kernels' live pieces do (netcsum_pktstream.hip): each
+// lane marks its segment's sectors in a per-wave 1024-bit LDS bitmap (a run spans < 63 KiB from its
+// first 128-B line, kLiveReach), one ballot gives the run's live 1-KiB pieces, the stream pops them in
+// address order (bit 63 the never-live sentinel) and lane l loads its 16 B of piece q only when its
+// sector is live. Segment ends are the same scalar events as above, each leaving the segment's total
+// in its lane; a segment that ends within 48 B of its first 16-B chunk (the 20-B segment of a 40-B
+// ACK) is summed from that window instead, with no sectors and no event, and one vector epilogue
+// finishes every lane (an empty segment: its pseudo-header alone). Each lane's first chunk is loaded
+// with the plain policy before the bitmap (the live-read floor's touch, tools/live_read_probe.hip). A
+// run that is not in order or outgrows the reach takes the 16-lane groups. Run length and pieces in
+// flight come from the batch's plan (varlen_plan_word above; launch_batch).
+constexpr uint64_t kSentinelPiece = 1ull << 63;
+constexpr uint32_t kNoEnd = ~0u;
+
+template <int D, int PH, bool NT>
+__global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, uint32_t spw) {
+    __shared__ uint32_t sect_all[4][32];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t nwg = gridDim.x;
+    if (A.plan_out != nullptr) {                              // the last block: the next batch's plan
+        nwg -= 1u;
+        if (blockIdx.x == nwg) {
+            __shared__ uint32_t part[4][3];
+            const uint32_t m = min(A.n_seg, 4096u);
+            uint32_t tot = 0u;
+            uint64_t ptot = 0u, pn = 0u;
+            varlen_sample<256>(A.seg_off, A.seg_len_v, A.n_seg, m, part, tot, ptot, pn);
+            if (threadIdx.x == 0u) {
+                __hip_atomic_store(A.plan_out, varlen_plan_word(m ? tot / m : 0u, ptot, pn, m, A.plan_tag),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+    }
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg) : blockIdx.x;
+    const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
+    if (sb64 >= A.n_seg) {
+        return;
+    }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(A.n_seg - s_begin, spw);       // spw <= 64: segment k in lane k
+    const uint32_t lane16 = 16u * lane;
+    const bool ph_odd = PH != 0 && (A.pseudo_len & 1u) != 0u;
+    const uintptr_t base = (uintptr_t)A.base;
+    const bool mine = lane < nres;
+    const uint64_t off = A.seg_off[s_begin + (mine ? lane : 0u)];
+    const uint32_t len = mine ? (uint32_t)A.seg_len_v[s_begin + lane] : 0u;
+    const uint64_t off0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(off >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off);
+    const uintptr_t O = (base + off0) & ~(uintptr_t)127;
+    const uint64_t rel = base + off - O;                      // >= 0 when in order
+    const uint64_t end = rel + len;
+    const uint32_t prev_end = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
+    const bool ok = !mine || (rel < kLiveReach && end <= kLiveReach - 128u && (lane == 0u || (uint64_t)prev_end <= rel));
+    const bool stream = __builtin_amdgcn_ballot_w64(!ok) == 0u;
+    const uint32_t span = stream ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u)) : 0u;
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
+    // each lane's first 16 B (plain policy: the touch), and for a segment that ends within 48 B of its
+    // first chunk's start (a 20-B segment of a 40-B ACK) the next two: such a segment is summed here
+    // from its window, after the stream — no sectors, no event
+    const uint32_t wl = (uint32_t)rel & ~15u;
+    const bool inwin = stream && mine && len != 0u && ((uint32_t)rel & 15u) + len <= 48u;
+    const u32x4 w0 = buf_load16<false>(rd, (stream && mine && len != 0u) ? wl : kOOB);
+    const u32x4 w1 = buf_load16<false>(rd, inwin ? wl + 16u : kOOB);
+    const u32x4 w2 = buf_load16<false>(rd, inwin ? wl + 32u : kOOB);
+
+    uint32_t ps0 = 0u, ps1 = 0u;
+    if constexpr (PH != 0) {
+        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
+    }
+    uint32_t res0 = 0u, res1 = 0u;
+    if (!stream) {
+        // out of order, overlapping or past the reach: four segments at a time, a 16-lane group each
+        const uint32_t g = lane >> 4;
+        for (uint32_t k0 = 0; k0 < nres; k0 += 4u) {
+            const uint32_t k = k0 + g;
+            const uint64_t o = __shfl(off, (int)(k & 63u), 64);
+            const uint32_t l = (uint32_t)__shfl((int)len, (int)(k & 63u), 64);
+            const uintptr_t a = base + o;
+            const uint32_t tot = group_sum<16>(span_partial<16, 4, NT>(a, k < nres ? l : 0u, (int)(lane & 15u)));
+            const uint32_t odd = (uint32_t)(((a & 1u) != 0u) != ph_odd);
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+                if (k0 + i < nres) {
+                    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)(16u * i));
+                    const bool od = __builtin_amdgcn_readlane((int)odd, (int)(16u * i)) != 0;
+                    finish_segment<PH>(k0 + i, T, od, A.verify != 0u, lane, ps0, ps1, res0, res1);
+                }
+            }
+        }
+        asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
+        store_run_results(A, s_begin, nres, lane, res0, res1);
+        return;
+    }
+
+    // the run's live sectors, then its live pieces
+    uint32_t* sect = sect_all[w];
+    if (lane < 32u) {
+        sect[lane] = 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (mine && len != 0u && !inwin) {
+        const uint32_t s0 = (uint32_t)rel >> 6, s1 = ((uint32_t)end - 1u) >> 6;
+        for (uint32_t d = s0 >> 5; d <= (s1 >> 5); ++d) {
+            const uint32_t lo = max(s0, d << 5) - (d << 5), hi = min(s1, (d << 5) + 31u) - (d << 5);
+            atomicOr(&sect[d], (2u << hi) - (1u << lo));      // bits lo..hi (hi = 31: 2 << 31 wraps to 0)
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t pm0 = reinterpret_cast<const uint16_t*>(sect)[lane];
+    uint64_t lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
+    const uint32_t nlive = (uint32_t)__builtin_popcountll(lm0);
+    lm0 |= kSentinelPiece;
+    const uint32_t lbit = 1u << (lane >> 2);
+    auto pop = [&]() -> uint32_t {
+        const uint32_t q = (uint32_t)__builtin_ctzll(lm0);
+        lm0 = (lm0 & (lm0 - 1u)) | kSentinelPiece;
+        return q;
+    };
+    auto live_voff = [&](uint32_t q) -> uint32_t {
+        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
+        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+    };
+    u32x4 dv[D];
+    uint32_t qd[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        qd[j] = pop();
+        dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+    }
+
+    // the streamed segments, in address order (lane mask), and the next one's start / end; an event
+    // leaves the segment's total in its lane (tot), the epilogue below is one vector pass
+    uint32_t tot = 0u;
+    uint64_t srest = __builtin_amdgcn_ballot_w64(mine && len != 0u && !inwin);
+    const bool any = srest != 0u;
+    uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
+    srest &= srest - 1u;
+    uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)cur);
+    uint32_t ce = any ? cs + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)cur) : kNoEnd;
+    uint32_t acc = 0u;
+    auto consume = [&](uint32_t q, u32x4 v) {
+        const uint32_t qb = q << 10;
+        const uint32_t pend = qb + 1024u;
+        const uint32_t full = sum4(v, 0u);
+        uint32_t u = cur, c = cs, e = ce, a = acc, t = tot;
+        uint64_t rs = srest;
+        if (e > pend) {                                        // no segment ends in this piece
+            a += (c <= qb) ? full : full - piece_prefix(v, full, lane16, min(c - qb, 1024u));
+        } else {
+            uint32_t Ps = (c <= qb) ? 0u : piece_prefix(v, full, lane16, c - qb);
+#pragma clang loop vectorize(disable) unroll(disable)
+            do {
+                const uint32_t Pe = piece_prefix(v, full, lane16, e <= qb ? 0u : e - qb);
+                const uint32_t T = wave_total(a + (Pe - Ps));
+                t = (lane == u) ? T : t;
+                a = 0u;
+                const bool more = rs != 0u;
+                u = more ? (uint32_t)__builtin_ctzll(rs) : 63u;
+                rs &= rs - 1u;
+                const uint32_t pe = e;
+                c = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)u);
+                e = more ? c + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)u) : kNoEnd;
+                Ps = (c == pe) ? Pe : piece_prefix(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
+            } while (e <= pend);
+            a = full - Ps;
+        }
+        cur = u;
+        srest = rs;
+        cs = c;
+        ce = e;
+        acc = a;
+        tot = t;
+    };
+    const uint32_t rounds = (nlive + (uint32_t)D - 1u) / (uint32_t)D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            consume(qd[j], opaque_tuple(dv[j]));
+            qd[j] = pop();                                     // none left: the sentinel, no loads
+            dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
+            asm volatile("" ::: "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::"v"(w0));
+    if (inwin) {                                               // [lo, hi) of the 48-B window
+        const int lo = (int)((uint32_t)rel & 15u), hi = lo + (int)len;
+        tot = low_bytes(w0, min(hi, 16)) - low_bytes(w0, lo) + low_bytes(w1, min(max(hi - 16, 0), 16)) +
+              low_bytes(w2, max(hi - 32, 0));
+    }
+    // vector epilogue, lane k = segment k (an empty one: its pseudo-header alone)
+    uint32_t t = fold16(tot);
+    if ((((uint32_t)rel & 1u) != 0u) != ph_odd) {
+        t = rot8(t);
+    }
+    if constexpr (PH != 0) {
+        t = fold16(t + ps0);
+    }
+    res0 = A.verify ? (t == 0xFFFFu ? 1u : 0u) : (~t & 0xFFFFu);
+    store_run_results(A, s_begin, nres, lane, res0, res1);
+}
+
+template <int D, int PH, bool NT>
+hipError_t launch_live_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
+    SegBatchArgs a = a0;
+    a.xcd = stream_xcd(true) ? 1u : 0u;
+    const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
+    hipLaunchKernelGGL((seg_live_varlen_kernel<D, PH, NT>), dim3((unsigned)((waves + 3u) / 4u + (a.plan_out ? 1u : 0u))),
+                       dim3(256), stream_lds_bytes(0), s, a, spw);
+    return hipGetLastError();
+}
+
 template <int D, int PH, bool NT>
 hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
@@ -454,45 +731,15 @@ __global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint64_t* off
                                                              uint32_t* out, uint32_t* plan_out, uint32_t tag) {
     __shared__ uint32_t part[16][3];
     const uint32_t m = min(n, 4096u);
-    uint32_t acc = 0u, pit = 0u, npit = 0u;
-    for (uint32_t j = threadIdx.x; j < m; j += 1024u) {
-        const uint32_t i = (uint32_t)(((uint64_t)j * n) / m);
-        acc += lens[i];
-        if (i + 1u < n) {
-            const uint64_t a = offs[i], b = offs[i + 1u];
-            if (b > a && b - a < 65536u) {                     // in order and near: a pitch
-                pit += (uint32_t)(b - a);
-                npit += 1u;
-            }
-        }
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        acc += (uint32_t)__shfl_xor((int)acc, d, 64);
-        pit += (uint32_t)__shfl_xor((int)pit, d, 64);
-        npit += (uint32_t)__shfl_xor((int)npit, d, 64);
-    }
-    if ((threadIdx.x & 63u) == 0u) {
-        part[threadIdx.x >> 6][0] = acc;
-        part[threadIdx.x >> 6][1] = pit;
-        part[threadIdx.x >> 6][2] = npit;
-    }
-    __syncthreads();
+    uint32_t tot = 0u;
+    uint64_t ptot = 0u, pn = 0u;
+    varlen_sample<1024>(offs, lens, n, m, part, tot, ptot, pn);
     if (threadIdx.x == 0u) {
-        uint32_t tot = 0u;
-        uint64_t ptot = 0u, pn = 0u;
-        for (int i = 0; i < 16; ++i) {
-            tot += part[i][0];
-            ptot += part[i][1];
-            pn += part[i][2];
-        }
         const uint32_t mlen = m ? tot / m : 0u;
         const uint32_t mean = mlen + extra;
         *out = min(max(run_bytes / max(mean, 1u), spw_min), kMaxRun);
         if (plan_out != nullptr) {
-            const bool gapped = pn * 2u >= (uint64_t)m && (uint32_t)(ptot / max(pn, 1ull)) >= mlen + 32u;
-            const uint32_t word = 0x80000000u | ((tag & 0x7FFFu) << 16) | (gapped ? (mlen >= 1024u ? 1u : 2u) : 0u);
-            __hip_atomic_store(plan_out, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(plan_out, varlen_plan_word(mlen, ptot, pn, m, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -719,6 +966,16 @@ hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, b
     case 8: return launch_stream_d<8>(a, spw, nt, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hipStream_t s) {
+    if (a.seg_off == nullptr || spw == 0u || spw > 64u) return hipErrorInvalidValue;
+    const int ph = stream_ph(a);
+#define NETCSUM_LV(D_, PH_) \
+    if (depth == D_ && ph == PH_) return launch_live_varlen_t<D_, PH_, true>(a, spw, s);
+    NETCSUM_LV(4, 0) NETCSUM_LV(4, 1) NETCSUM_LV(4, 2) NETCSUM_LV(8, 0) NETCSUM_LV(8, 1) NETCSUM_LV(8, 2)
+#undef NETCSUM_LV
+    return hipErrorInvalidValue;
 }
 
 }  // namespace netcsum
