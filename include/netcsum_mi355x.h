@@ -608,7 +608,9 @@ typedef enum netcsum_tune_key {
                                          CHUNKS 4 / 8 = pieces in flight; TILE = headers per run,
                                          auto: the most that fit 4 KiB from any 128-B lead, 192 for
                                          20-B headers). Chain batches: 1 = the wave-per-chain form
-                                         (default: two passes, see (2c))                            */
+                                         (default: two passes, see (2c)), 3 = two passes with the
+                                         first in the live-sector stream (TILE = pieces per run,
+                                         CHUNKS 4 / 8 = pieces in flight)                          */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8;
                                          run-stream kernels: 1-KiB pieces in flight (4 / 8)        */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),

@@ -1,7 +1,8 @@
 """GPU parity of the batched NET_BUF chain checksums (NetUtil_MI355X_ChkSumBatchChains) against the C
 oracle walking the same pieces as NET_BUF chains (net_util.c:1545-1687), bit-exact, over every
 group width, scattered odd-offset pieces, empty pieces, NULL chains, odd pseudo-headers, u32 wrap,
-for the default two-pass form (per-piece sums, then a combine pass per chain), the wave-per-chain form
+for the default two-pass form (per-piece sums by tiled 16-lane groups — or in the live-sector stream
+with NETCSUM_TUNE_KERNEL 3 — then a combine pass per chain), the wave-per-chain form
 (NETCSUM_TUNE_KERNEL 1) and the two-pass form's fallback for batches with more pieces than its
 records hold."""
 import random
@@ -52,19 +53,19 @@ def _want(cb, op):
                                cb.pseudo_len, cb.n, op)
 
 
-@pytest.mark.parametrize("group", [0, 1, 16, 32, 64])           # 1: the wave-per-chain form (KERNEL 1)
+@pytest.mark.parametrize("group", [0, 1, 3, 16, 32, 64])        # 1 / 3: TUNE_KERNEL 1 (wave per chain) / 3
 @pytest.mark.parametrize("pseudo_len", [0, 12, 13, 40])
 @pytest.mark.parametrize("op", [0, 1])
 def test_chain_batch_matches_oracle(group, pseudo_len, op):
     rng = random.Random(group * 131 + pseudo_len * 3 + op)
     cb = make_chain_batch(rng, 1500, pseudo_len=pseudo_len, self_verify=0.5 if op else 0.0)
-    if group == 1:
-        netcsum.tune(netcsum.TUNE_KERNEL, 1)
+    if group in (1, 3):
+        netcsum.tune(netcsum.TUNE_KERNEL, group)
     else:
         netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     got, want = _gpu(cb, op), _want(cb, op)
-    assert netcsum.last_launch().startswith("chain_wave_kernel" if group == 1 else "chain_batch_kernel" if group
-                                            else "chain_piece_kernel"), netcsum.last_launch()
+    name = {0: "chain_piece_kernel", 1: "chain_wave_kernel", 3: "chain_live_piece_kernel"}.get(group, "chain_batch_kernel")
+    assert netcsum.last_launch().startswith(name), netcsum.last_launch()
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:5]]
     if op:
@@ -129,6 +130,56 @@ def test_chain_batch_more_pieces_than_records():
     want = oracle.batch_chains(base, offs, lens, first, ph, 13, 13, n, 0)
     assert netcsum.last_launch().startswith("chain_piece_kernel")
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+
+
+@pytest.mark.parametrize("order", ["sorted", "shuffled", "far", "odd"])
+@pytest.mark.parametrize("spw", [1, 7, 16, 45, 64])
+def test_chain_batch_fragments_live_runs(order, spw):
+    """Pass 1's live-sector stream (chain_live_piece_kernel, TUNE_KERNEL 3) on the chain row's layout:
+    datagrams' fragments, each in its own 2-KiB buffer at +42 (net_ipv4.c:3963 reassembly chains), 1-45
+    fragments per chain, the last one short, some empty; runs of 1..64 pieces (TUNE_TILE). Shuffled
+    fragments within a chain, every 5th buffer 200 KiB further on, or odd offsets and lengths: the runs
+    they break take the 16-lane groups."""
+    netcsum.tune(netcsum.TUNE_KERNEL, 3)
+    netcsum.tune(netcsum.TUNE_TILE, spw)
+    try:
+        rng = np.random.default_rng(spw * 7 + len(order))
+        per = rng.integers(1, 46, size=600)
+        npc = int(per.sum())
+        first = np.zeros(len(per) + 1, np.uint32)
+        first[1:] = np.cumsum(per)
+        lens = np.full(npc, 1480, np.uint16)
+        lens[first[1:] - 1] = rng.integers(1, 1481, size=len(per))        # each chain's last fragment
+        lens[rng.random(npc) < 0.02] = 0
+        offs = np.arange(npc, dtype=np.uint64) * np.uint64(2048) + np.uint64(42)
+        if order == "odd":
+            odd = rng.random(npc) < 0.3
+            offs = offs + odd.astype(np.uint64)
+            lens = np.where(rng.random(npc) < 0.3, lens - (lens > 0), lens).astype(np.uint16)
+        if order == "far":
+            offs = offs + (np.arange(npc, dtype=np.uint64) // 5) * np.uint64(200 * 1024)
+        if order == "shuffled":
+            for c in range(len(per)):
+                a, b = int(first[c]), int(first[c + 1])
+                p = rng.permutation(b - a) + a
+                offs[a:b], lens[a:b] = offs[p].copy(), lens[p].copy()
+        base = rng.integers(0, 256, size=int(offs.max()) + 2048 + 64, dtype=np.uint8)
+        ph = rng.integers(0, 256, size=12 * len(per), dtype=np.uint8)
+        n = len(per)
+        for op in (0, 1):
+            out = torch.zeros(n, dtype=torch.int16 if op == 0 else torch.uint8, device=DEV)
+            netcsum.batch_chains(_dev(base, np.uint8), _dev(offs, np.int64), _dev(lens, np.int16), _dev(first, np.int32),
+                                 _dev(ph, np.uint8), 12, 12, n, out, op=op, n_pieces=npc)
+            torch.cuda.synchronize()
+            assert netcsum.last_launch().startswith("chain_live_piece_kernel"), netcsum.last_launch()
+            assert f"pieces_per_wave={spw}" in netcsum.last_launch()
+            got = out.cpu().numpy()
+            want = oracle.batch_chains(base, offs, lens, first, ph, 12, 12, n, op)
+            got = got.view(np.uint16) if op == 0 else got
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (op, [(int(i), int(got[i]), int(want[i])) for i in bad[:5]])
+    finally:
+        netcsum.tune(netcsum.TUNE_TILE, -1)
 
 
 def test_chain_batch_matches_single_segment_batch():

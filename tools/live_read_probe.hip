@@ -225,7 +225,8 @@ int main(int argc, char** argv) {
                   {"live.d8.touch", 1, 8, 1}, {"whole.touch", 0, 4, 1}};
         for (int pass = 0; pass < 2; ++pass) {
             for (const V& v : vs) {
-                for (uint32_t R : {8u, 16u}) {
+                for (uint32_t R : {8u, 16u, 32u}) {
+                    if ((uint64_t)R * L.stride + 2048u > (63u << 10)) continue;   // a run within the bitmap's reach
                     const uint64_t waves = (n + R - 1u) / R;
                     const dim3 g((unsigned)((waves + 3u) / 4u)), b(256);
                     auto launch = [&]() {

@@ -16,7 +16,8 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   rx_ring / tx_ring  1 M mixed 40/576/1500-B datagrams (7:4:1) in 1520-B slots at +14, strided,
        pkt_len 1506; rx_ringv / tx_ringv the same ring by offset/length descriptors; rx_nb2kv /
        tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
-  suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N
+  suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
+  .kN = NETCSUM_TUNE_KERNEL N (chains.k3: pass 1 in the live-sector stream), .dN = NETCSUM_TUNE_CHUNKS N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -45,7 +46,11 @@ def main():
         if part.startswith("nt"):
             netcsum.tune(netcsum.TUNE_NT_LOADS, int(part[2:]))
             continue
-        if part[:1] == "b":
+        if part[:1] == "d":
+            netcsum.tune(netcsum.TUNE_CHUNKS, int(part[1:]))
+        elif part[:1] == "k":
+            netcsum.tune(netcsum.TUNE_KERNEL, int(part[1:]))
+        elif part[:1] == "b":
             netcsum.tune(netcsum.TUNE_PKT_BOUND, int(part[1:]))
         elif part[:1] == "s":
             netcsum.tune(netcsum.TUNE_TILE, int(part[1:]))

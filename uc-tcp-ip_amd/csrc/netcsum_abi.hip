@@ -1312,9 +1312,22 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
         const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 20, 128ull * n_chains), 1ull << 24);
         ScratchLease scratch;
         if (scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * 8u) == hipSuccess) {
-            netcsum::set_last_launch("chain_piece_kernel<G=16,K=6,tile=64,nt> +chain_combine_kernel");
+            // pass 1: tiled 16-lane groups, or with TUNE_KERNEL 3 the live-sector stream in runs of 16
+            // pieces (TUNE_TILE 1..64 sets the run, TUNE_CHUNKS 4 the depth) — 0.1993-0.2046 ms on the
+            // chain row against 0.1756-0.1803 for the groups (profiles/r5v_chains.log: two wave totals
+            // per piece end, the byte and the half-word sums, cost more than the sectors save there)
+            const int tk = g_tune_tile.load(), ch = g_tune_chunks.load();
+            const uint32_t live = g_tune_kernel.load() != 3 ? 0u : (tk >= 1 && tk <= 64) ? (uint32_t)tk : 16u;
+            const int depth = ch == 4 ? 4 : 8;
+            char d[128];
+            if (live) {
+                snprintf(d, sizeof d, "chain_live_piece_kernel<D=%d,nt> pieces_per_wave=%u +chain_combine_kernel", depth, live);
+            } else {
+                snprintf(d, sizeof d, "chain_piece_kernel<G=16,K=6,tile=64,nt> +chain_combine_kernel");
+            }
+            netcsum::set_last_launch(d);
             NC_HIP(netcsum::launch_chain_two_pass(a, static_cast<uint64_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
-                                                  static_cast<hipStream_t>(hip_stream)));
+                                                  static_cast<hipStream_t>(hip_stream), live, depth));
             NC_HIP(scratch.end());
             return NET_UTIL_ERR_NONE;
         }

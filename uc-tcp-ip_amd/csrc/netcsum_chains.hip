@@ -29,6 +29,7 @@
 
 #include "netcsum_device.h"
 #include "netcsum_kernels.h"
+#include "netcsum_stream.h"
 
 namespace netcsum {
 
@@ -386,12 +387,8 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
     const uint32_t g = threadIdx.x / kPG;
     const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
     const uint32_t ntiles = (np + tile - 1u) / tile;
-    if (np > cap) {                                               // no room for the records: this
-        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // pass does the batch
-        for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += gridDim.x * 4u) {   // in the wave-per-
-            wave_chain(A, ch);                                    // chain form, the combine pass
-        }                                                         // returns at once
-        return;
+    if (np > cap) {                                               // no room for the records: the
+        return;                                                   // combine pass does the batch
     }
     if (blockIdx.x >= ntiles) {
         return;
@@ -435,14 +432,198 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
     }
 }
 
+// Pass 1 in the live-sector stream (NETCSUM_TUNE_KERNEL 3; round 5): a wave takes a run of `spw` pieces
+// and, when they lie in address order within 63 KiB of the run's first 128-B line (a datagram's
+// fragments in their NET_BUFs, one per 2-KiB buffer at +42), reads only the 64-B sectors that hold
+// piece bytes, as seg_live_varlen_kernel (netcsum_stream.hip) does for segments: a per-wave LDS
+// bitmap of live sectors, the live 1-KiB pieces popped in address order, a lane loading its 16 B only
+// where its sector is live. Each piece end is one scalar event taking two wave totals, the byte sum b
+// and the half-word sum h of [start, end), into the piece's lane; a vector epilogue writes the records
+// (e | o << 32, o = (h - b) / 255). Runs out of order or past the reach take pass 1's 16-lane groups.
+// Measured on the chain row (16 Ki x 45 fragments): 0.1993-0.2046 ms in runs of 16-24 against
+// 0.1756-0.1803 ms for the tiled groups (profiles/r5v_chains.log) — two wave totals per piece end
+// cost more than the skipped sectors save — so the groups stay the default; the live-sector read
+// floor of the fragments is 0.1550 ms (tools/live_read_probe.hip frag2k, profiles/r5k_*).
+__device__ __forceinline__ uint32_t sum4b(u32x4 v) {
+    uint32_t b = __builtin_amdgcn_sad_u8(v.x, 0u, 0u);
+    b = __builtin_amdgcn_sad_u8(v.y, 0u, b);
+    b = __builtin_amdgcn_sad_u8(v.z, 0u, b);
+    return __builtin_amdgcn_sad_u8(v.w, 0u, b);
+}
+// piece_prefix (netcsum_stream.h) of the byte sum
+__device__ __forceinline__ uint32_t piece_prefix_b(u32x4 v, uint32_t s4, uint32_t lane16, uint32_t x) {
+    const uint32_t k = x & 15u;
+    const uint64_t m0 = k >= 8u ? ~0ull : (1ull << (8u * k)) - 1ull;
+    const uint64_t m1 = k <= 8u ? 0ull : (1ull << (8u * (k - 8u))) - 1ull;
+    uint32_t pv = __builtin_amdgcn_sad_u8(v.x & (uint32_t)m0, 0u, 0u);
+    pv = __builtin_amdgcn_sad_u8(v.y & (uint32_t)(m0 >> 32), 0u, pv);
+    pv = __builtin_amdgcn_sad_u8(v.z & (uint32_t)m1, 0u, pv);
+    pv = __builtin_amdgcn_sad_u8(v.w & (uint32_t)(m1 >> 32), 0u, pv);
+    return (lane16 + 16u <= x) ? s4 : ((lane16 < x) ? pv : 0u);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) chain_live_piece_kernel(ChainBatchArgs A, uint64_t* eo, uint32_t cap, uint32_t spw) {
+    using namespace sv;
+    __shared__ uint32_t sect_all[4][32];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
+    if (np > cap) {                                               // no room for the records: the
+        return;                                                   // combine pass does the batch
+    }
+    const uint64_t sb64 = ((uint64_t)blockIdx.x * 4u + w) * spw;
+    if (sb64 >= np) {
+        return;
+    }
+    const uint32_t s_begin = (uint32_t)sb64;
+    const uint32_t nres = min(np - s_begin, spw);                 // spw <= 64: piece k in lane k
+    const uint32_t lane16 = 16u * lane;
+    const uintptr_t base = (uintptr_t)A.base;
+    const bool mine = lane < nres;
+    const uint64_t off = A.off[s_begin + (mine ? lane : 0u)];
+    const uint32_t len = mine ? (uint32_t)A.len[s_begin + lane] : 0u;
+    const uint64_t off0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(off >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off);
+    const uintptr_t O = (base + off0) & ~(uintptr_t)127;
+    const uint64_t rel = base + off - O;
+    const uint64_t end = rel + len;
+    const uint32_t prev_end = (uint32_t)__shfl_up((int)(uint32_t)end, 1, 64);
+    const bool ok = !mine || (rel < kLiveReach && end <= kLiveReach - 128u && (lane == 0u || (uint64_t)prev_end <= rel));
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0u) {
+        // out of order, overlapping or past the reach: pass 1's 16-lane groups, four pieces at a time
+        const int gl = (int)(lane & 15u);
+        for (uint32_t k0 = 0; k0 < nres; k0 += 4u) {
+            const uint32_t k = k0 + (lane >> 4);
+            const uint64_t o = __shfl(off, (int)(k & 63u), 64);
+            const uint32_t l = (uint32_t)__shfl((int)len, (int)(k & 63u), 64);
+            PieceStage st;
+            piece_issue(st, base + o, k < nres ? l : 0u, gl);
+            uint32_t b, h;
+            piece_consume(st, gl, b, h);
+            piece_store(eo, s_begin + k, b, h, gl, k < nres);
+        }
+        return;
+    }
+    const uint32_t span = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)(nres - 1u));
+    const __amdgpu_buffer_rsrc_t rd = run_rsrc(O, (span + 15u) & ~15u);
+    const u32x4 w0 = buf_load16<false>(rd, (mine && len != 0u) ? ((uint32_t)rel & ~15u) : kOOB);   // touch
+    uint32_t* sect = sect_all[w];
+    if (lane < 32u) {
+        sect[lane] = 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (mine && len != 0u) {
+        const uint32_t s0 = (uint32_t)rel >> 6, s1 = ((uint32_t)end - 1u) >> 6;
+        for (uint32_t d = s0 >> 5; d <= (s1 >> 5); ++d) {
+            const uint32_t lo = max(s0, d << 5) - (d << 5), hi = min(s1, (d << 5) + 31u) - (d << 5);
+            atomicOr(&sect[d], (2u << hi) - (1u << lo));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t pm0 = reinterpret_cast<const uint16_t*>(sect)[lane];
+    uint64_t lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
+    const uint32_t nlive = (uint32_t)__builtin_popcountll(lm0);
+    constexpr uint64_t kSent = 1ull << 63;
+    lm0 |= kSent;
+    const uint32_t lbit = 1u << (lane >> 2);
+    auto pop = [&]() -> uint32_t {
+        const uint32_t q = (uint32_t)__builtin_ctzll(lm0);
+        lm0 = (lm0 & (lm0 - 1u)) | kSent;
+        return q;
+    };
+    auto live_voff = [&](uint32_t q) -> uint32_t {
+        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
+        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+    };
+    u32x4 dv[D];
+    uint32_t qd[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        qd[j] = pop();
+        dv[j] = buf_load16<true>(rd, live_voff(qd[j]));
+    }
+    uint64_t srest = __builtin_amdgcn_ballot_w64(mine && len != 0u);
+    const bool any = srest != 0u;
+    uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
+    srest &= srest - 1u;
+    uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)cur);
+    uint32_t ce = any ? cs + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)cur) : ~0u;
+    uint32_t ah = 0u, ab = 0u, th = 0u, tb = 0u;
+    auto consume = [&](uint32_t q, u32x4 v) {
+        const uint32_t qb = q << 10;
+        const uint32_t pend = qb + 1024u;
+        const uint32_t fh = sum4(v, 0u), fb = sum4b(v);
+        uint32_t u = cur, c = cs, e = ce, xh = ah, xb = ab, yh = th, yb = tb;
+        uint64_t rs = srest;
+        if (e > pend) {                                          // no piece ends in this 1 KiB
+            const uint32_t x = min(c - qb, 1024u);
+            xh += (c <= qb) ? fh : fh - piece_prefix(v, fh, lane16, x);
+            xb += (c <= qb) ? fb : fb - piece_prefix_b(v, fb, lane16, x);
+        } else {
+            uint32_t Ph = (c <= qb) ? 0u : piece_prefix(v, fh, lane16, c - qb);
+            uint32_t Pb = (c <= qb) ? 0u : piece_prefix_b(v, fb, lane16, c - qb);
+#pragma clang loop vectorize(disable) unroll(disable)
+            do {
+                const uint32_t xe = e <= qb ? 0u : e - qb;
+                const uint32_t Eh = piece_prefix(v, fh, lane16, xe), Eb = piece_prefix_b(v, fb, lane16, xe);
+                const uint32_t Th = wave_total(xh + (Eh - Ph)), Tb = wave_total(xb + (Eb - Pb));
+                yh = (lane == u) ? Th : yh;
+                yb = (lane == u) ? Tb : yb;
+                xh = 0u;
+                xb = 0u;
+                const bool more = rs != 0u;
+                u = more ? (uint32_t)__builtin_ctzll(rs) : 63u;
+                rs &= rs - 1u;
+                const uint32_t pe = e;
+                c = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)u);
+                e = more ? c + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)u) : ~0u;
+                const uint32_t xc = c <= qb ? 0u : min(c - qb, 1024u);
+                Ph = (c == pe) ? Eh : piece_prefix(v, fh, lane16, xc);
+                Pb = (c == pe) ? Eb : piece_prefix_b(v, fb, lane16, xc);
+            } while (e <= pend);
+            xh = fh - Ph;
+            xb = fb - Pb;
+        }
+        cur = u;
+        srest = rs;
+        cs = c;
+        ce = e;
+        ah = xh;
+        ab = xb;
+        th = yh;
+        tb = yb;
+    };
+    const uint32_t rounds = (nlive + (uint32_t)D - 1u) / (uint32_t)D;
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            consume(qd[j], opaque_tuple(dv[j]));
+            qd[j] = pop();
+            dv[j] = buf_load16<true>(rd, live_voff(qd[j]));
+            asm volatile("" ::: "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::"v"(w0));
+    if (mine) {                                                   // h - b = 255 o exactly (< 64 KiB)
+        const uint32_t o = (th - tb) * 0xFEFEFEFFu;
+        eo[s_begin + lane] = (uint64_t)(tb - o) | ((uint64_t)o << 32);
+    }
+}
+
 // A 16-lane group per chain (4 chains per wave, independent loads in flight for all four), 16
 // pieces per step.
 constexpr int kCG = 16;
 
 __global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, const uint64_t* eo, uint32_t cap) {
     const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
-    if (np > cap) {
-        return;                                                   // pass 1 did the batch
+    if (np > cap) {                                               // pass 1 had no room for the records:
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // the batch in the
+        for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += gridDim.x * 4u) {   // wave-per-chain
+            wave_chain(A, ch);                                    // form here (out of pass 1, whose
+        }                                                         // registers it set: 116 VGPRs)
+        return;
     }
     const int lane = (int)(threadIdx.x & (kCG - 1));
     const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(kCG - 1);          // the group's ballot bits
@@ -498,7 +679,23 @@ __global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, co
 
 }  // namespace
 
-hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s) {
+hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s, uint32_t live_spw,
+                                 int live_depth) {
+    if (live_spw != 0u) {                                          // pass 1 in the live-sector stream:
+        const uint64_t waves = ((uint64_t)cap + live_spw - 1u) / live_spw;   // a wave per run of the most
+        const dim3 g1((unsigned)((waves + 3u) / 4u));              // pieces the records hold; runs past
+        if (live_depth == 4) {                                     // the batch's return at once
+            hipLaunchKernelGGL(chain_live_piece_kernel<4>, g1, dim3(256), 0, s, a, eo, cap, live_spw);
+        } else {
+            hipLaunchKernelGGL(chain_live_piece_kernel<8>, g1, dim3(256), 0, s, a, eo, cap, live_spw);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;
+        const unsigned g2 = (unsigned)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 64u);
+        hipLaunchKernelGGL(chain_combine_kernel, dim3(g2), dim3(256), 0, s, a, (const uint64_t*)eo, cap);
+        return hipGetLastError();
+    }
     // pass 1: blocks take tiles of 64 consecutive pieces round-robin (the piece count lives on the
     // device; blocks past the last tile return). Grid: 2 blocks per chain, at least the resident
     // blocks, at most one per tile the scratch holds — so a batch of up to 32 pieces per chain gets

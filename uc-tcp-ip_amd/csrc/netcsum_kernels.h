@@ -128,7 +128,10 @@ struct ChainBatchArgs {
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
 // Two-pass form (default): per-piece even/odd sums into `eo` (cap records), then a combine pass per
 // chain; batches of more than `cap` pieces fall back to the wave-per-chain form inside pass 2.
-hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s);
+// live_spw != 0: pass 1 in the live-sector stream, runs of live_spw (<= 64) consecutive pieces,
+// live_depth (4 / 8) pieces in flight.
+hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s,
+                                 uint32_t live_spw = 0u, int live_depth = 8);
 
 // CRC-32 batches (netcsum_crc.hip; net_util.c:485-636).
 struct CrcBatchArgs {
