@@ -21,7 +21,7 @@ def rows(pattern):
 
 # the source file that defines each kernel (+ the shared headers): a summary is evidence for the
 # exact sources whose hash it records
-KERNEL_FILES = {"seg_stream": "netcsum_stream.hip", "seg_pipe": "netcsum_kernels.hip", "pkt_vl_deferred": "netcsum_pktstream.hip", "read_run": "netcsum_stream.hip", "varlen_runlen": "netcsum_stream.hip",
+KERNEL_FILES = {"seg_stream": "netcsum_stream.hip", "seg_live": "netcsum_stream.hip", "seg_pipe": "netcsum_kernels.hip", "pkt_vl_deferred": "netcsum_pktstream.hip", "read_run": "netcsum_stream.hip", "varlen_runlen": "netcsum_stream.hip",
                 "seg_hdrstream": "netcsum_hdrstream.hip", "seg_hdr_": "netcsum_hdr.hip", "pkt_stream": "netcsum_pktstream.hip",
                 "pkt_scatter": "netcsum_pktstream.hip", "pkt_batch": "netcsum_packets.hip", "pkt_v6_walk": "netcsum_v6walk.hip",
                 "chain_": "netcsum_chains.hip", "crc_": "netcsum_crc.hip", "seg_small": "netcsum_small.hip"}
