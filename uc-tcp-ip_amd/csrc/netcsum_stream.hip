@@ -442,19 +442,32 @@ __device__ __forceinline__ uint32_t varlen_plan_word(uint32_t mlen, uint64_t pto
     return 0x80000000u | ((tag & 0x7FFFu) << 16) | form;
 }
 
-// Sampling by one block of NTH threads (NTH / 64 waves): the mean of up to 4096 evenly spaced
-// lengths and the mean in-order pitch; thread 0 returns the sums.
+// Sampling by one block of NTH threads (NTH / 64 waves): the mean of up to kVarlenSamples evenly
+// spaced lengths and the mean in-order pitch; thread 0 returns the sums. (4096 samples took the
+// one-block kernel 18-20 µs ahead of every C4 batch — one CU's misses on 12 K scattered lines,
+// profiles/r5x_c4_pmc.json, r5z_*; 1024 estimate a mean length to ≈ 2 %.)
+constexpr uint32_t kVarlenSamples = 1024u;
 template <int NTH>
 __device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t m,
                                               uint32_t (&part)[NTH / 64][3], uint32_t& tot, uint64_t& ptot, uint64_t& pn) {
     uint32_t acc = 0u, pit = 0u, npit = 0u;
-    for (uint32_t j = threadIdx.x; j < m; j += (uint32_t)NTH) {
-        const uint32_t i = (uint32_t)(((uint64_t)j * n) / m);
-        acc += lens[i];
-        if (i + 1u < n) {
-            const uint64_t a = offs[i], b = offs[i + 1u];
-            if (b > a && b - a < 65536u) {                     // in order and near: a pitch
-                pit += (uint32_t)(b - a);
+    // four samples per thread at a time, every load issued before any is used
+    for (uint32_t j0 = threadIdx.x; j0 < m; j0 += 4u * (uint32_t)NTH) {
+        uint32_t l[4];
+        uint64_t a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t j = j0 + (uint32_t)u * (uint32_t)NTH;
+            const uint32_t i = j < m ? (uint32_t)(((uint64_t)j * n) / m) : 0u;
+            l[u] = j < m ? lens[i] : 0u;
+            a[u] = offs[i];
+            b[u] = (j < m && i + 1u < n) ? offs[i + 1u] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc += l[u];
+            if (b[u] > a[u] && b[u] - a[u] < 65536u) {          // in order and near: a pitch
+                pit += (uint32_t)(b[u] - a[u]);
                 npit += 1u;
             }
         }
@@ -510,7 +523,7 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         nwg -= 1u;
         if (blockIdx.x == nwg) {
             __shared__ uint32_t part[4][3];
-            const uint32_t m = min(A.n_seg, 4096u);
+            const uint32_t m = min(A.n_seg, kVarlenSamples);
             uint32_t tot = 0u;
             uint64_t ptot = 0u, pn = 0u;
             varlen_sample<256>(A.seg_off, A.seg_len_v, A.n_seg, m, part, tot, ptot, pn);
@@ -716,7 +729,7 @@ hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStrea
     return hipGetLastError();
 }
 
-// One block: the mean of up to 4096 evenly spaced lengths -> run length for about run_bytes per run.
+// One block: the mean of up to kVarlenSamples (1024) evenly spaced lengths -> run length for about run_bytes per run.
 // Also the pitch — the distance from a sampled segment's start to the next one's — for the batch's
 // plan (plan_out, coherent host memory, with the host's tag): segments of >= 1 KiB on average with
 // gaps of >= 32 B between them (one per pool buffer, DataPtr + TransportHdrIx) read faster in the
@@ -730,7 +743,7 @@ __global__ void __launch_bounds__(1024) varlen_runlen_kernel(const uint64_t* off
                                                              uint32_t extra, uint32_t run_bytes, uint32_t spw_min,
                                                              uint32_t* out, uint32_t* plan_out, uint32_t tag) {
     __shared__ uint32_t part[16][3];
-    const uint32_t m = min(n, 4096u);
+    const uint32_t m = min(n, kVarlenSamples);
     uint32_t tot = 0u;
     uint64_t ptot = 0u, pn = 0u;
     varlen_sample<1024>(offs, lens, n, m, part, tot, ptot, pn);
