@@ -83,14 +83,15 @@ def test_pool_segments_vs_oracle(order, slot, ix, mix, plen):
         assert bad.size == 0, (op_, launches[-1], [(int(i), int(got[i]), int(want[i]), int(offs[i]), int(lens[i]))
                                                    for i in bad[:6]])
     # the batch's plan (the sampler of the first call): segments with gaps in address order take the
-    # live-sector stream from the second call on the same descriptors (runs of 16 at depth 8 for 1480-B
-    # segments, of 32 (30 in 2-KiB buffers) at depth 4 for the mix); its own sampler block keeps it
+    # live-sector stream from the second call on the same descriptors (1480-B segments: runs of 8 at
+    # depth 4 in 1520-B buffers, 16 at depth 8 in 2-KiB ones; the mix: as long as the reach allows, 41 /
+    # 30 at depth 4); its own sampler block keeps it
     for last in launches:
         assert last.split("<")[0] in ("seg_stream_varlen_kernel", "seg_live_varlen_kernel", "seg_pipe_kernel"), last
     if order == "sorted":
         for last in launches[1:]:
-            run = 16 if not mix else (32 if slot == 1520 else 30)
-            assert "plan=pool(live)" in last and f"D={8 if not mix else 4}" in last, last
+            run, depth = ((8, 4) if slot == 1520 else (16, 8)) if not mix else ((41 if slot == 1520 else 30), 4)
+            assert "plan=pool(live)" in last and f"D={depth}" in last, last
             assert f"segs_per_wave={run}" in last, last
 
 

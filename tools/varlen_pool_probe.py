@@ -35,7 +35,7 @@ LAYOUTS = {"pool1520": (1520, 34, False), "pool1520mix": (1520, 34, True), "pool
 VARIANTS = [("default", {}), ("pipe16", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GROUP_LANES: 16, netcsum.TUNE_CHUNKS: 6}),
             ("runs8", {netcsum.TUNE_VARLEN_RUN_BYTES: 0})]
 if os.environ.get("POOL_LIVE"):                       # live-sector stream: run length x pieces in flight
-    for r, dd in ((8, 4), (8, 8), (16, 4), (16, 8), (32, 4), (32, 8)):
+    for r, dd in ((8, 4), (8, 8), (16, 4), (16, 8), (24, 4), (32, 4), (32, 8), (40, 4)):
         VARIANTS.append((f"live.s{r}.d{dd}", {netcsum.TUNE_TILE: r, netcsum.TUNE_CHUNKS: dd}))
 if os.environ.get("POOL_PIPES"):                      # lane-group pipe geometries (kernel 2)
     for g, k, t in ((16, 6, 2), (16, 6, 8), (16, 6, 16), (32, 4, 4), (8, 8, 4), (16, 8, 4)):

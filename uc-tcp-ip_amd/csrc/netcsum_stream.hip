@@ -425,19 +425,24 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
 
 // The plan word from the sampled mean length, mean pitch (of the pn in-order pairs of m samples):
 // segments with gaps of >= 32 B between them, mostly in order, take the live-sector stream
-// (seg_live_varlen_kernel): runs of 32 below a 455-B mean length, else 16, 8 pieces in flight from a
-// 910-B mean (tools/varlen_pool_probe.py POOL_LIVE over the pool layouts, profiles/r5s_*: 1480-B
-// segments fastest in runs of 16 at depth 8, the 20 / 556 / 1480-B mix in runs of 32 at depth 4),
-// capped so a run's slots span < 61 KiB; pools too sparse for runs of 4 take the lane-group pipe
-// form (1: 16 x 6 for >= 1 KiB segments, 2: 8 x 8).
+// (seg_live_varlen_kernel): below a 455-B mean length runs as long as the reach allows (a run's slots
+// span < 61 KiB: 41 1520-B buffers, 30 2-KiB ones), 16 below a 910-B mean, longer segments runs of 8
+// at depth 4 in nearly dense pools (pitch < 1800 B) and of 16 at depth 8 in sparser ones
+// (tools/varlen_pool_probe.py POOL_LIVE, profiles/r5t_*, r5y_*, r5ac_*: the 20 / 556 / 1480-B mix
+// 0.0975 ms in runs of 32 against 0.0953 in runs of 40 in 1520-B buffers; 1480-B segments there
+// 0.2211-0.2294 ms in runs of 8 at depth 4 against 0.2280-0.2305 in 16 at depth 8, in 2-KiB buffers
+// 0.2522-0.2567 against 0.2574-0.2585); pools too sparse for runs of 4 take the lane-group pipe form
+// (1: 16 x 6 for >= 1 KiB segments, 2: 8 x 8).
 __device__ __forceinline__ uint32_t varlen_plan_word(uint32_t mlen, uint64_t ptot, uint64_t pn, uint32_t m, uint32_t tag) {
     const uint32_t pitch = (uint32_t)(ptot / max(pn, 1ull));
     const bool gapped = pn * 2u >= (uint64_t)m && pitch >= mlen + 32u;
     uint32_t form = 0u;
     if (gapped) {
         const uint32_t cap = (kLiveReach - 2048u) / max(pitch, 1u);
-        const uint32_t run = min(mlen * 45u < 20480u ? 32u : 16u, cap);
-        form = run >= 4u ? (3u | (mlen * 45u >= 40960u ? 4u : 0u) | (run << 8)) : (mlen >= 1024u ? 1u : 2u);
+        const bool shrt = mlen * 45u < 20480u, lng = mlen * 45u >= 40960u;
+        const bool d8 = lng && pitch >= 1800u;                 // long segments with wide gaps
+        const uint32_t run = min(shrt ? 64u : (lng && !d8) ? 8u : 16u, cap);
+        form = run >= 4u ? (3u | (d8 ? 4u : 0u) | (run << 8)) : (mlen >= 1024u ? 1u : 2u);
     }
     return 0x80000000u | ((tag & 0x7FFFu) << 16) | form;
 }
@@ -545,6 +550,27 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
     const bool ph_odd = PH != 0 && (A.pseudo_len & 1u) != 0u;
     const uintptr_t base = (uintptr_t)A.base;
     const bool mine = lane < nres;
+    // lane k's pseudo-header chunks first: their addresses need no descriptor, so they travel with
+    // the descriptor loads below (one memory round trip for both, not two in a row)
+    constexpr int kPch = PH == 1 ? 2 : PH == 2 ? 5 : 1;
+    u32x4 pv[kPch];
+    uint32_t pa_lane = 0u;
+    if constexpr (PH != 0) {
+        const uint32_t plen = A.pseudo_len, pst = A.pseudo_stride;
+        const uintptr_t pfirst = (uintptr_t)A.pseudo + (uint64_t)s_begin * pst;
+        const uintptr_t PB = pfirst & ~(uintptr_t)15;
+        pa_lane = (uint32_t)(pfirst - PB) + lane * pst;
+        const uint32_t pspan = (uint32_t)(pfirst - PB) + (nres - 1u) * pst + plen;
+        const __amdgpu_buffer_rsrc_t rp = run_rsrc(PB, (pspan + 15u) & ~15u);
+        const uint32_t nchmax = (plen + 30u) >> 4;
+        const uint32_t hi = (pa_lane & 15u) + plen;
+#pragma unroll
+        for (int c = 0; c < kPch; ++c) {
+            pv[c] = (uint32_t)c < nchmax
+                        ? buf_load16<false>(rp, (mine && 16u * (uint32_t)c < hi) ? (pa_lane & ~15u) + 16u * (uint32_t)c : kOOB)
+                        : u32x4{0u, 0u, 0u, 0u};
+        }
+    }
     const uint64_t off = A.seg_off[s_begin + (mine ? lane : 0u)];
     const uint32_t len = mine ? (uint32_t)A.seg_len_v[s_begin + lane] : 0u;
     const uint64_t off0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(off >> 32)) << 32) |
@@ -566,9 +592,18 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
     const u32x4 w1 = buf_load16<false>(rd, inwin ? wl + 16u : kOOB);
     const u32x4 w2 = buf_load16<false>(rd, inwin ? wl + 32u : kOOB);
 
-    uint32_t ps0 = 0u, ps1 = 0u;
+    uint32_t ps0 = 0u, ps1 = 0u;                              // lane k: segment k's pseudo-header sum
     if constexpr (PH != 0) {
-        run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
+        const int lo = (int)(pa_lane & 15u), hi = lo + (int)A.pseudo_len;
+        uint32_t pacc = 0u;
+#pragma unroll
+        for (int c = 0; c < kPch; ++c) {
+            pacc += low_bytes(pv[c], min(max(hi - 16 * c, 0), 16)) - low_bytes(pv[c], min(max(lo - 16 * c, 0), 16));
+        }
+        ps0 = fold16(pacc);
+        if (pa_lane & 1u) {
+            ps0 = rot8(ps0);
+        }
     }
     uint32_t res0 = 0u, res1 = 0u;
     if (!stream) {
