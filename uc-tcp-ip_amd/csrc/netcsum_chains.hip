@@ -497,10 +497,26 @@ __global__ void __launch_bounds__(256) chain_live_piece_kernel(ChainBatchArgs A,
             const uint32_t k = k0 + (lane >> 4);
             const uint64_t o = __shfl(off, (int)(k & 63u), 64);
             const uint32_t l = (uint32_t)__shfl((int)len, (int)(k & 63u), 64);
-            PieceStage st;
-            piece_issue(st, base + o, k < nres ? l : 0u, gl);
-            uint32_t b, h;
-            piece_consume(st, gl, b, h);
+            // one 16-B chunk per lane at a time (this path is rare; pass 1's six-chunk stages set the
+            // kernel's VGPR count: 79 against 5x, 6 waves per SIMD against 8)
+            const uintptr_t a = base + o;
+            const uint32_t ln = k < nres ? l : 0u;
+            const uint32_t lead = (uint32_t)(a & 15u), rend = lead + ln;
+            const uint32_t nch = ln ? (rend + 15u) >> 4 : 0u;
+            const uintptr_t q0 = a & ~(uintptr_t)15;
+            uint32_t b = 0u, h = 0u;
+            uint32_t steps = (nch + 15u) >> 4;
+            steps = max(steps, (uint32_t)__shfl_xor((int)steps, 16, 64));
+            steps = max(steps, (uint32_t)__shfl_xor((int)steps, 32, 64));
+            for (uint32_t t = 0; t < steps; ++t) {
+                const uint32_t c = 16u * t + (uint32_t)gl;
+                u32x4 v = load16<true>(reinterpret_cast<gu32x4*>(c < nch ? q0 + 16u * (uintptr_t)c : zero_addr()));
+                if (c < nch) {
+                    v = edge_mask_rel(v, c, lead, rend);
+                }
+                b += sum4b(v);
+                h = sum4(v, h);
+            }
             piece_store(eo, s_begin + k, b, h, gl, k < nres);
         }
         return;

@@ -456,12 +456,14 @@ template <int NTH>
 __device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16_t* lens, uint32_t n, uint32_t m,
                                               uint32_t (&part)[NTH / 64][3], uint32_t& tot, uint64_t& ptot, uint64_t& pn) {
     uint32_t acc = 0u, pit = 0u, npit = 0u;
-    // four samples per thread at a time, every load issued before any is used
-    for (uint32_t j0 = threadIdx.x; j0 < m; j0 += 4u * (uint32_t)NTH) {
-        uint32_t l[4];
-        uint64_t a[4], b[4];
+    // U samples per thread at a time, every load issued before any is used (the live kernel's sampler
+    // block takes one at a time: its registers count toward the whole kernel's)
+    constexpr int U = NTH >= 1024 ? 4 : 1;
+    for (uint32_t j0 = threadIdx.x; j0 < m; j0 += (uint32_t)U * (uint32_t)NTH) {
+        uint32_t l[U];
+        uint64_t a[U], b[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const uint32_t j = j0 + (uint32_t)u * (uint32_t)NTH;
             const uint32_t i = j < m ? (uint32_t)(((uint64_t)j * n) / m) : 0u;
             l[u] = j < m ? lens[i] : 0u;
@@ -469,7 +471,7 @@ __device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16
             b[u] = (j < m && i + 1u < n) ? offs[i + 1u] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             acc += l[u];
             if (b[u] > a[u] && b[u] - a[u] < 65536u) {          // in order and near: a pitch
                 pit += (uint32_t)(b[u] - a[u]);
@@ -614,7 +616,9 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
             const uint64_t o = __shfl(off, (int)(k & 63u), 64);
             const uint32_t l = (uint32_t)__shfl((int)len, (int)(k & 63u), 64);
             const uintptr_t a = base + o;
-            const uint32_t tot = group_sum<16>(span_partial<16, 4, NT>(a, k < nres ? l : 0u, (int)(lane & 15u)));
+            // (one chunk per lane in flight: this path is rare here, and 4 set the kernel's VGPR count,
+            // 72 against 40-56 — 7 waves per SIMD against 8)
+            const uint32_t tot = group_sum<16>(span_partial<16, 1, NT>(a, k < nres ? l : 0u, (int)(lane & 15u)));
             const uint32_t odd = (uint32_t)(((a & 1u) != 0u) != ph_odd);
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) {
@@ -665,10 +669,19 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         qd[j] = pop();
         dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
     }
+    // the in-window segments' sums now, while the first pieces are in flight (the window loads were
+    // issued before them, so this waits for those alone), which frees the window's 12 VGPRs before the
+    // stream: 64 VGPRs, 8 waves per SIMD
+    uint32_t tot = 0u;
+    asm volatile("" ::"v"(w0));
+    if (inwin) {                                               // [lo, hi) of the 48-B window
+        const int lo = (int)((uint32_t)rel & 15u), hi = lo + (int)len;
+        tot = low_bytes(w0, min(hi, 16)) - low_bytes(w0, lo) + low_bytes(w1, min(max(hi - 16, 0), 16)) +
+              low_bytes(w2, max(hi - 32, 0));
+    }
 
     // the streamed segments, in address order (lane mask), and the next one's start / end; an event
     // leaves the segment's total in its lane (tot), the epilogue below is one vector pass
-    uint32_t tot = 0u;
     uint64_t srest = __builtin_amdgcn_ballot_w64(mine && len != 0u && !inwin);
     const bool any = srest != 0u;
     uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
@@ -720,12 +733,6 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("" ::"v"(w0));
-    if (inwin) {                                               // [lo, hi) of the 48-B window
-        const int lo = (int)((uint32_t)rel & 15u), hi = lo + (int)len;
-        tot = low_bytes(w0, min(hi, 16)) - low_bytes(w0, lo) + low_bytes(w1, min(max(hi - 16, 0), 16)) +
-              low_bytes(w2, max(hi - 32, 0));
-    }
     // vector epilogue, lane k = segment k (an empty one: its pseudo-header alone)
     uint32_t t = fold16(tot);
     if ((((uint32_t)rel & 1u) != 0u) != ph_odd) {
