@@ -693,10 +693,14 @@ typedef enum netcsum_tune_key {
     NETCSUM_TUNE_BURST_SERVER_IDLE_US = 23,/* mode 3: microseconds without a burst after which the server
                                          stops (the next burst relaunches it); a device-wide
                                          synchronisation waits up to this long. 1..1000000, default 500 */
-    NETCSUM_TUNE_BURST_SERVER_LIFE_US = 24 /* mode 3: microseconds one server launch stays resident even
+    NETCSUM_TUNE_BURST_SERVER_LIFE_US = 24,/* mode 3: microseconds one server launch stays resident even
                                          while bursts keep coming (kernels of other streams sharing its
                                          hardware queue wait behind it at most this long plus one
                                          burst); the next burst relaunches it. 1..1000000, default 1000 */
+    NETCSUM_TUNE_FAULT_INJECT  = 25   /* TEST ONLY. 1: the calling thread's next offset/length packet
+                                         batch that has a deferred pass enqueues its stream kernel,
+                                         skips the deferred pass and fails (NET_UTIL_ERR_MI355X_DEV):
+                                         the state a failed launch leaves; one-shot. 0: cleared      */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

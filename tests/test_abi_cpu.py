@@ -110,12 +110,14 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(25, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(26, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_ZERO_COPY, 4) == 219       # 0..3
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 0) == 219  # 1..10^6
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_IDLE_US, 500) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 0) == 219  # 1..10^6
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BURST_SERVER_LIFE_US, 1000) == 200
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_FAULT_INJECT, 2) == 219          # 0 or 1 (test only)
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_FAULT_INJECT, 0) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, 5) == 219             # -1..4
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PKT_BOUND, -1) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_VARLEN_RUN_BYTES, -2) == 219     # -1 .. 2^20

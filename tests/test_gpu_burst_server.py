@@ -10,9 +10,11 @@ thread's own burst server — waits behind it. Each server launch is therefore b
 Thread A posts 64-frame RxBurstHost bursts back to back for ~1.5 s with an idle limit of 100 ms, so
 its server never stops for lack of work; meanwhile thread B runs, on each of 12 streams (more than
 the 4 hardware queues, so several share A's queue), a device-resident ChkSumBatchStrided followed by
-a synchronisation of that stream, then an RxBurstHost of its own (B's own server). Every B call
-returns within 10 ms and every result of both threads equals the oracle's. With
-NETCSUM_BURST_SERVER_RECORD set, the latencies are written there as one JSON line.
+a synchronisation of that stream, then an RxBurstHost of its own (B's own server). B's calls are
+bounded by a multiple of the life limit, not by A's run: 99 % of them within 10 ms, every one within
+100 ms (round 4's server held one for 1 472 ms, until A stopped; the looser maximum leaves room for a
+host-side pause — GC, preemption, the GIL — on a shared box), and every result of both threads equals
+the oracle's. With NETCSUM_BURST_SERVER_RECORD set, the latencies are written there as one JSON line.
 """
 import json
 import os
@@ -33,7 +35,8 @@ from packets import KINDS, KINDS6, make_packet, make_packet_v6
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-B_BOUND_S = 0.010          # every one of B's calls, batch + stream sync or a burst
+B_P99_S = 0.010            # 99 % of B's calls, batch + stream sync or a burst (10 x the life limit)
+B_MAX_S = 0.100            # every one of them (100 x the life limit; round 4's library: 1.47 s)
 
 
 def _ring(seed, n, stride=1520, lead=14):
@@ -139,7 +142,8 @@ def test_busy_burst_server_does_not_starve_streams_sharing_its_queue():
            "b_burst_max_ms": round(max(b_burst) * 1e3, 3) if b_burst else None,
            "b_burst_median_us": round(statistics.median(b_burst) * 1e6, 2) if b_burst else None,
            "b_p99_ms": round(float(np.percentile(b_batch + b_burst, 99)) * 1e3, 3) if b_batch else None,
-           "b_over_bound": sum(x > B_BOUND_S for x in b_batch + b_burst), "bound_ms": B_BOUND_S * 1e3,
+           "b_over_p99_bound": sum(x > B_P99_S for x in b_batch + b_burst), "p99_bound_ms": B_P99_S * 1e3,
+           "max_bound_ms": B_MAX_S * 1e3,
            "a_paths": sorted(a_paths), "b_paths": sorted(b_paths), "lib": os.path.basename(netcsum.LIB_PATH)}
     print(json.dumps(rec))
     path = os.environ.get("NETCSUM_BURST_SERVER_RECORD")
@@ -151,4 +155,5 @@ def test_busy_burst_server_does_not_starve_streams_sharing_its_queue():
     assert a_alive_after_b, "thread A must keep its server busy for the whole of B's phase"
     assert not a_bad and not b_bad, (a_bad[:5], b_bad[:5])
     assert rounds >= 3, rec
-    assert rec["b_over_bound"] == 0, rec
+    assert rec["b_p99_ms"] <= B_P99_S * 1e3, rec
+    assert max(b_batch + b_burst) <= B_MAX_S, rec

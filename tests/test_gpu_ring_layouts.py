@@ -413,3 +413,57 @@ def test_ring_plan_per_layout_vs_oracle(case):
         f.zero_()
         rx_fn(bt[lead:], n, f, stride=slot, pkt_len=present)
         assert bool(((f & 0x07) == 0x07).all().item()), (case, passes)
+
+
+@pytest.mark.parametrize("kind", ["rx", "tx1", "tx2"])
+def test_deferred_counters_reset_after_a_failed_call(kind):
+    """an offset/length batch counts its out-of-order runs in the scratch slot's
+    tail words and its deferred pass resets them. A call that fails between the two (here: the
+    test-only NETCSUM_TUNE_FAULT_INJECT 1, which enqueues the stream kernel and fails instead of
+    launching the deferred pass) leaves them non-zero; the next call on the slot must zero them first,
+    or it would re-run the stale list entries (Tx: the same runs twice, concurrently). Shuffled
+    descriptors, so every run is listed; the calls after each failure equal the oracle."""
+    rng = random.Random(606)
+    n, slot, lead = 700, 1520, 14
+    buf, lens = _ring(rng, n, slot, lead, v6mix=True)
+    perm = np.random.default_rng(9).permutation(n)
+    offs = (np.arange(n, dtype=np.int64) * slot + lead)[perm].copy()
+    lens = lens[perm].copy()
+    o_d = torch.from_numpy(offs).to(DEV)
+    l_d = torch.from_numpy(lens.view(np.int16)).to(DEV)
+    frames = [bytes(buf[o:o + int(m)]) for o, m in zip(offs.tolist(), lens.tolist())]
+    if kind == "rx":
+        want = np.array([op.rx_validate_ip(f) for f in frames], np.uint8)
+    else:
+        netcsum.tune(netcsum.TUNE_TX_PASSES, 1 if kind == "tx1" else 2)
+        want = buf.copy()
+        want_f = np.zeros(n, np.uint8)
+        for i, (o, m) in enumerate(zip(offs.tolist(), lens.tolist())):
+            q, want_f[i] = op.tx_finalize_ip(bytes(buf[o:o + int(m)]), True)
+            want[o:o + int(m)] = np.frombuffer(q, np.uint8)
+
+    def call(check=True):
+        f = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        if kind == "rx":
+            err = netcsum.rx_validate_ip(torch.from_numpy(buf).to(DEV), n, f, off=o_d, lens=l_d, check=check)
+            torch.cuda.synchronize()
+            return err, f.cpu().numpy(), None
+        bt = torch.from_numpy(buf).to(DEV)
+        err = netcsum.tx_finalize_ip(bt, n, f, off=o_d, lens=l_d, check=check)
+        torch.cuda.synchronize()
+        return err, bt.cpu().numpy(), f.cpu().numpy()
+
+    try:
+        for rep in range(3):
+            netcsum.tune(netcsum.TUNE_FAULT_INJECT, 1)
+            err, _, _ = call(check=False)
+            assert err == netcsum.NET_UTIL_ERR_MI355X_DEV, err
+            assert "offlen +pkt_vl_deferred_kernel" in netcsum.last_launch(), netcsum.last_launch()
+            for _ in range(2):
+                err, got, got_f = call()
+                assert err == 0
+                _check(got, want, f"{kind} after failed call {rep}")
+                if got_f is not None:
+                    _check(got_f, want_f, f"{kind} flags after failed call {rep}")
+    finally:
+        netcsum.tune(netcsum.TUNE_FAULT_INJECT, 0)

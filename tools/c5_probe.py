@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Round 6, verdict r5 item 1: where does the C5 shard (16 M x 1500 B + 12 B, 25.4 GB) lose its
+per-GPU rate against C2 (1 M, 1.6 GB) on some boxes? Interleaves, in one process, on the C5 shard
+and on a C2 batch allocated beside it (GPU box only; JSON lines):
+  kernel            the library's default launch (bench.py's step)
+  nopseudo          the same segments without pseudo-headers (no second address stream)
+  chunk1M           the 16 M segments as 16 back-to-back launches of 1 M (C2-sized footprints)
+  run_probe         read_run_kernel: the kernel's access pattern, nothing computed (TUNE_PROBE 2)
+  lds_probe         the LDS-DMA grid-stride read probe (TUNE_PROBE 1)
+  touch0 / xcd0     the kernel without the row touch / in the plain block order
+Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("uc-tcp-ip_amd", "tools", ""):
+    sys.path.insert(0, os.path.join(REPO, sub))
+import torch  # noqa: E402
+
+import netcsum  # noqa: E402
+from bench import SEED, c2_pseudo_headers  # noqa: E402
+from sweep import timeit  # noqa: E402
+
+
+def main():
+    rounds = int(os.environ.get("C5P_ROUNDS", "3"))
+    reps = int(os.environ.get("C5P_REPS", "20"))
+    only = os.environ.get("C5P_VARIANTS")
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    L, P = 1500, 12
+    sizes = {"c5": 1 << 24, "c2": 1 << 20}
+    bufs = {}
+    for name, n in sizes.items():
+        seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(seg, n * L, SEED, 0)
+        ph = torch.from_numpy(c2_pseudo_headers(0, n, L, P)).to(dev)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        bufs[name] = (n, seg, ph, out)
+    sink = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def tune(probe=1, touch=-1, xcd=-1):
+        netcsum.tune(netcsum.TUNE_PROBE, probe)
+        netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
+        netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
+
+    variants = []
+    for name, (n, seg, ph, out) in bufs.items():
+        n16 = n * L // 16 * 16
+        algo = n * (L + P + 2)
+
+        def k(seg=seg, ph=ph, out=out, n=n):
+            return lambda: netcsum.batch_strided(seg, L, L, ph, P, P, n, out, netcsum.OP_DATA_CALC, stream=st)
+
+        def nop(seg=seg, out=out, n=n):
+            return lambda: netcsum.batch_strided(seg, L, L, None, 0, 0, n, out, netcsum.OP_DATA_CALC, stream=st)
+
+        def chunked(seg=seg, ph=ph, out=out, n=n):
+            m = 1 << 20
+            parts = [(seg[i * m * L:], ph[i * m * P:], out[i * m:]) for i in range(n // m)]
+
+            def f():
+                for s, p, o in parts:
+                    netcsum.batch_strided(s, L, L, p, P, P, m, o, netcsum.OP_DATA_CALC, stream=st)
+            return f
+
+        def rd(seg=seg, n16=n16):
+            return lambda: netcsum.read_stream(seg, n16, sink, stream=st)
+        variants += [(f"{name}_kernel", {}, k(), algo), (f"{name}_nopseudo", {}, nop(), n * (L + 2)),
+                     (f"{name}_run_probe", {"probe": 2}, rd(), n16), (f"{name}_lds_probe", {"probe": 1}, rd(), n16),
+                     (f"{name}_touch0", {"touch": 0}, k(), algo), (f"{name}_xcd0", {"xcd": 0}, k(), algo)]
+        if n > (1 << 20):
+            variants.append((f"{name}_chunk1M", {}, chunked(), algo))
+    if only:
+        keep = only.split(",")
+        variants = [v for v in variants if any(v[0].endswith(x) for x in keep)]
+    res = {}
+    for _ in range(rounds):
+        for name, kw, fn, byts in variants:
+            tune(**kw)
+            med, mn = timeit(fn, st, reps=reps, warm_s=0.3)
+            res.setdefault(name, []).append((med, mn, byts, netcsum.last_launch()))
+    tune()
+    for name, r in res.items():
+        med = statistics.median(x[0] for x in r)
+        print(json.dumps({"variant": name, "kernel": r[0][3], "ms_med": round(med, 4),
+                          "ms_min": round(min(x[1] for x in r), 4), "GBps_med": round(r[0][2] / med / 1e6, 1),
+                          "frac_of_8TBps": round(r[0][2] / med / 1e6 / 8000.0, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/netcsum_mi355x.h"
@@ -315,6 +316,8 @@ struct ScratchSlot {
     bool               ev_live = false;
     bool               pinned = false;  // used under stream capture: never freed while the thread runs
     bool               unordered = false;  // used by a lease with no event since the last record
+    bool               tail_dirty = false; // tail words handed out by a call that did not confirm the
+                                           // launch of the pass that resets them (ScratchLease::tail_words)
     uint32_t           seq = 0;         // last tag handed out (ScratchLease::next_tag)
 };
 
@@ -410,6 +413,15 @@ public:
                 return e;
             }
             hit->cap = cap;
+            hit->tail_dirty = false;
+        }
+        if (hit->tail_dirty) {
+            // the last call that used the tail words (the offset/length deferral counters) failed
+            // between the kernel that counts up and the pass that resets them: zero them in stream
+            // order before this call's launches (a stale count re-ran stale list entries)
+            hipError_t e = hipMemsetAsync(static_cast<uint8_t*>(hit->p) + hit->cap - kTailBytes, 0, kTailBytes, st);
+            if (e != hipSuccess) return e;
+            hit->tail_dirty = false;
         }
         if (ordered && hit->ev_live && !capturing_ && hipEventQuery(hit->ev) == hipErrorNotReady) {
             hipError_t e = hipStreamWaitEvent(st, hit->ev, 0);
@@ -428,8 +440,15 @@ public:
     void* ptr() const { return slot_ ? slot_->p : nullptr; }
     // The slot's last kTailBytes, past every request (zeroed when the slot is allocated): words that
     // outlive a call — the offset/length deferral counter, which the deferred pass resets to zero.
+    // Handing them out marks the slot dirty until tail_reset_enqueued(): a call that fails before its
+    // resetting pass is enqueued leaves them to be zeroed by the next acquire() of the slot.
     uint32_t* tail_words() const {
-        return slot_ ? reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot_->p) + slot_->cap - kTailBytes) : nullptr;
+        if (slot_ == nullptr) return nullptr;
+        slot_->tail_dirty = true;
+        return reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot_->p) + slot_->cap - kTailBytes);
+    }
+    void tail_reset_enqueued() {
+        if (slot_) slot_->tail_dirty = false;
     }
     // A tag no earlier call on this slot used (a deferral word holding it was written by this call;
     // after 2^32 calls a stale word may match once, which only repeats an idempotent pass).
@@ -593,7 +612,8 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         // adaptive varlen runs: a one-block kernel samples the lengths and leaves the run length in
         // this stream's scratch word, which the batch kernel reads (stream order; any value is safe:
         // the kernel never runs shorter runs than its grid covers), and the plan for the next batch
-        // (at +128: the packet batches keep their deferral word at +0 of the same slot)
+        // (at +128 of the slot's reserved 256-B header: the lane-group walk pass keeps its deferral word
+        // at +0; the packet stream's Tx records and deferred-run list start at +256)
         ScratchLease word;
         NC_HIP(word.acquire(dev, s, 256u, false));
         uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
@@ -1233,25 +1253,31 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
                  d_off ? (vl_inline ? " offlen (inline fallback)" : " offlen +pkt_vl_deferred_kernel") : "",
                  two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "", plan_note);
         netcsum::set_last_launch(desc);
-        // scratch: the records of two-pass Tx; offset/length batches also the deferred-run list (one
-        // index per run the stream kernel could not stream in order) and its counters in the slot's
-        // tail words (count, blocks done: the deferred pass leaves both zero)
+        // scratch slot layout (one slot per (thread, device, stream), shared by every batch kind on the
+        // stream, which stream order keeps apart): [0, 256) the words that must survive other calls'
+        // data — +0 the lane-group walk pass's deferral word (tagged), +128 the varlen run word — then,
+        // from +256, the records of two-pass Tx and, after them, offset/length batches' deferred-run list
+        // (one index per run the stream kernel could not stream in order); the list's counters (count,
+        // blocks done) are the slot's tail words, which the deferred pass leaves zero
         const size_t rec_bytes = (two && rec_only == nullptr) ? (size_t)n_pkt * sizeof(netcsum::PktTxRecord) : 0u;
         const size_t defer_bytes = (d_off && !vl_inline) ? (4u * (((size_t)n_pkt + spw - 1u) / spw) + 15u) & ~(size_t)15u : 0u;
+        constexpr size_t kHdr = 256u;
         ScratchLease scratch;
-        if (rec_bytes + defer_bytes) NC_HIP(scratch.acquire(dev, hs, rec_bytes + defer_bytes));
+        if (rec_bytes + defer_bytes) NC_HIP(scratch.acquire(dev, hs, kHdr + rec_bytes + defer_bytes));
         if (d_off && !vl_inline) {
-            a.vl_list = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch.ptr()) + rec_bytes);
+            a.vl_list = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch.ptr()) + kHdr + rec_bytes);
             a.vl_ctr = scratch.tail_words();
             a.vl_wide = vl_wide ? 1u : 0u;
         }
+        netcsum::PktTxRecord* recs = rec_bytes ? reinterpret_cast<netcsum::PktTxRecord*>(static_cast<uint8_t*>(scratch.ptr()) + kHdr)
+                                               : nullptr;
         if (rec_only != nullptr) {                        // zero-copy Tx burst: records only, no scatter
             NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs, rec_only,
                                               false));
         } else {
-            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs,
-                                              two ? static_cast<netcsum::PktTxRecord*>(scratch.ptr()) : nullptr));
+            NC_HIP(netcsum::launch_pkt_stream(a, ip_ver, d, spw, snt, tx, bound, hs, two ? recs : nullptr));
         }
+        if (a.vl_ctr != nullptr) scratch.tail_reset_enqueued();   // (launch_pkt_stream enqueued the deferred pass)
         NC_HIP(scratch.end());
         return NET_UTIL_ERR_NONE;
     }
@@ -1618,14 +1644,19 @@ static NET_ERR launch_server(HostCtx& c, uint64_t seq0) {
 // Waits for the server's stream for at most limit_ms (a stream query loop, never a blocking
 // synchronisation): a server launch queued behind other work on its hardware queue still ends, since
 // every launch of every server is bounded by its residency limit, but the caller's wait must not
-// depend on that. hipErrorNotReady when the stream is still busy at the deadline.
+// depend on that. hipErrorNotReady when the stream is still busy at the deadline: a burst whose server
+// is still queued 2 s after its post (burst_server_run's wait_out) fails with NET_UTIL_ERR_MI355X_DEV,
+// and the server stays marked live (it still serves or stops). The first 20 us poll back to back (a
+// server leaves within one burst of its stop), after that each poll yields the host core.
 static hipError_t server_stream_wait(hipStream_t s, int limit_ms) {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
-        if (e != hipErrorNotReady || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
+        const auto el = std::chrono::steady_clock::now() - t0;
+        if (e != hipErrorNotReady || el > std::chrono::milliseconds(limit_ms)) {
             return e;
         }
+        if (el > std::chrono::microseconds(20)) std::this_thread::yield();
     }
 }
 
@@ -2234,6 +2265,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_BURST_SERVER_LIFE_US:
         if (value < 1 || value > 1000000) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_burst_life.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_FAULT_INJECT:
+        if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_fault_skip_deferred(value == 1);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PKT_BOUND:
         if (value < -1 || value > 4) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

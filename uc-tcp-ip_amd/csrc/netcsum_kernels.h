@@ -195,6 +195,10 @@ void set_tx_flush(int mode);
 // host applies them)
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec = nullptr, bool scatter = true);
+// Test-only fault (NETCSUM_TUNE_FAULT_INJECT 1): the calling thread's next offset/length packet batch
+// with a deferred pass enqueues its stream kernel, skips the deferred pass and fails with
+// hipErrorLaunchFailure — the state a failed deferred launch leaves (the list counters not reset).
+void set_fault_skip_deferred(bool on);
 // Zero-copy host bursts: one wave copies n result bytes (flags, and actions if act != nullptr) from
 // device memory into coherent pinned host memory, then stores `tag` into *word (system scope).
 hipError_t launch_burst_done(const uint8_t* fl, const uint8_t* act, uint32_t n, uint8_t* h_fl, uint8_t* h_act,

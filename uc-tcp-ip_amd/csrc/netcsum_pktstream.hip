@@ -805,7 +805,10 @@ __device__ __forceinline__ void pkt_stream_run(const PktBatchArgs& A, uint32_t s
             // runs 289 ms.)
             if (lane == 0u) {
                 const uint32_t k = __hip_atomic_fetch_add(A.vl_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                A.vl_list[k] = (uint32_t)run;
+                // the list holds one entry per run of this batch; a count left over by a failed call
+                // is zeroed by the host before the next one (ScratchLease), so k stays below it —
+                // checked anyway, since an entry past it would land outside the lease
+                if ((uint64_t)k < ((uint64_t)A.n + spw - 1u) / spw) A.vl_list[k] = (uint32_t)run;
             }
         } else {
             // (the burst server, which has no deferred pass) one datagram per run (any order, overlap
@@ -1305,6 +1308,19 @@ hipError_t launch_tx_flush(hipStream_t s) {
     return hipSuccess;
 }
 
+thread_local bool tls_fault_skip_deferred = false;
+
+// the deferred pass, unless a test asked for its launch to fail (set_fault_skip_deferred)
+template <int D, bool NT, bool TX, bool REC, int VER, int BND>
+hipError_t launch_vl_deferred(const PktBatchArgs& a, int dgrid, uint32_t spw, PktTxRecord* rec, hipStream_t s) {
+    if (tls_fault_skip_deferred) {
+        tls_fault_skip_deferred = false;
+        return hipErrorLaunchFailure;
+    }
+    hipLaunchKernelGGL((pkt_vl_deferred_kernel<D, NT, TX, REC, VER, BND>), dim3(dgrid), dim3(256), 0, s, a, spw, rec);
+    return hipGetLastError();
+}
+
 template <int D, bool NT, bool TX, int VER, int BND, bool VL>
 hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t s, PktTxRecord* rec, bool scatter) {
     PktBatchArgs a = a0;
@@ -1327,8 +1343,7 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
         hipError_t e = hipGetLastError();
         if (e == hipSuccess && VL && a.vl_ctr != nullptr) {
             if constexpr (VL) {
-                hipLaunchKernelGGL((pkt_vl_deferred_kernel<D, NT, TX, TX, VER, BND>), dim3(dgrid), dim3(256), 0, s, a, spw, rec);
-                e = hipGetLastError();
+                e = launch_vl_deferred<D, NT, TX, TX, VER, BND>(a, dgrid, spw, rec, s);
             }
         }
         if (e != hipSuccess || !scatter) return e;
@@ -1343,14 +1358,17 @@ hipError_t launch_pkt_stream_t(const PktBatchArgs& a0, uint32_t spw, hipStream_t
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && VL && a.vl_ctr != nullptr) {
         if constexpr (VL) {
-            hipLaunchKernelGGL((pkt_vl_deferred_kernel<D, NT, TX, false, VER, BND>), dim3(dgrid), dim3(256), 0, s, a, spw, rec);
-            e = hipGetLastError();
+            e = launch_vl_deferred<D, NT, TX, false, VER, BND>(a, dgrid, spw, rec, s);
         }
     }
     return (e != hipSuccess || !TX) ? e : launch_tx_flush(s);
 }
 
 }  // namespace
+
+void set_fault_skip_deferred(bool on) {
+    tls_fault_skip_deferred = on;
+}
 
 hipError_t launch_pkt_field_gather(const PktBatchArgs& a, uint64_t* rec_out, hipStream_t s) {
     if (a.n == 0u) return hipSuccess;

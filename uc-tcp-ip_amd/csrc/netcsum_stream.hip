@@ -1025,6 +1025,9 @@ hipError_t launch_stream_batch(const SegBatchArgs& a, int depth, uint32_t spw, b
 
 hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hipStream_t s) {
     if (a.seg_off == nullptr || spw == 0u || spw > 64u) return hipErrorInvalidValue;
+    // PH 2 loads 5 aligned 16-B chunks of each pseudo-header: <= 64 B from any start (stream_supported's
+    // limit, checked here too so that no caller can reach the kernel with a longer one)
+    if (a.pseudo != nullptr && a.pseudo_len > 64u) return hipErrorInvalidValue;
     const int ph = stream_ph(a);
 #define NETCSUM_LV(D_, PH_) \
     if (depth == D_ && ph == PH_) return launch_live_varlen_t<D_, PH_, true>(a, spw, s);

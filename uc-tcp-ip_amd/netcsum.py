@@ -72,6 +72,7 @@ TUNE_PKT_BOUND = 21
 TUNE_BURST_ZERO_COPY = 22
 TUNE_BURST_SERVER_IDLE_US = 23
 TUNE_BURST_SERVER_LIFE_US = 24
+TUNE_FAULT_INJECT = 25          # test only: the next offset/length packet batch skips its deferred pass and fails
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
