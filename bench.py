@@ -301,6 +301,64 @@ def host_c2_shard(oracle, start, n, L, plen):
 C5_SHARD = 1 << 24                  # BASELINE configs[4]: 128 M segments over 8 GPUs = 16 M per GPU
 
 
+def read_probes(torch, netcsum, seg, n16, stream, reps=20):
+    """Measured read ceilings over the first n16 bytes of `seg` (HIP events on `stream`, mean of reps
+    launches after reps untimed): the LDS-DMA grid-stride probe (TUNE_PROBE 1) and read_run_kernel, the
+    checksum kernel's own access pattern with no arithmetic (TUNE_PROBE 2). Returns (lds, run) GB/s."""
+    sink = torch.zeros(1, dtype=torch.int64, device=seg.device)
+    ms = {}
+    for probe in (1, 2):
+        netcsum.tune(netcsum.TUNE_PROBE, probe)
+        for _ in range(reps):
+            netcsum.read_stream(seg, n16, sink, stream=stream)
+        rs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in rs:
+            a.record(stream)
+            netcsum.read_stream(seg, n16, sink, stream=stream)
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms[probe] = sum(a.elapsed_time(b) for a, b in rs) / len(rs)
+    netcsum.tune(netcsum.TUNE_PROBE, 1)
+    return n16 / (ms[1] * 1e-3) / 1e9, n16 / (ms[2] * 1e-3) / 1e9
+
+
+# One rank's own measurements at N > 1, all-gathered in this field order (float64 tensor).
+RANK_FIELDS = ("rank", "local_rank", "device", "wall_s", "kernel_ms", "per_gpu_GiBps", "run_stream_read_probe_GBps",
+               "read_stream_probe_GBps", "frac_of_run_stream_read_probe", "parity_sample_ok")
+
+
+def rank_records(dist, tensor_dev, own, world):
+    """All-gather every rank's `own` record (RANK_FIELDS) over the process group; list in rank order.
+    tensor_dev: "cpu" for gloo, the rank's GPU for RCCL."""
+    import torch
+    t = torch.tensor([float(own[k]) for k in RANK_FIELDS], dtype=torch.float64, device=tensor_dev)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(got, t)
+    return [dict(zip(RANK_FIELDS, x.cpu().tolist())) for x in got]
+
+
+def rank_summary(recs):
+    """The N > 1 line's self-explaining part: each rank's per-GPU rate (its own
+    wall time over the K timed launches), event-timed kernel ms and read ceilings over its own shard,
+    the slowest and fastest rank, and the spread. The aggregate `value` is set by the slowest rank (max
+    over ranks of the wall time), so a slow device is named here by its LOCAL_RANK."""
+    per = []
+    for r in recs:
+        per.append({"rank": int(r["rank"]), "local_rank": int(r["local_rank"]), "device": int(r["device"]),
+                    "per_gpu_GiBps": round(r["per_gpu_GiBps"], 2), "wall_s": round(r["wall_s"], 6),
+                    "kernel_ms": round(r["kernel_ms"], 5),
+                    "run_stream_read_probe_GBps": round(r["run_stream_read_probe_GBps"], 1),
+                    "read_stream_probe_GBps": round(r["read_stream_probe_GBps"], 1),
+                    "frac_of_run_stream_read_probe": round(r["frac_of_run_stream_read_probe"], 4),
+                    "parity_sample_ok": bool(r["parity_sample_ok"])})
+    slow = min(per, key=lambda x: x["per_gpu_GiBps"])
+    fast = max(per, key=lambda x: x["per_gpu_GiBps"])
+    return {"per_rank": per, "min_per_gpu": slow["per_gpu_GiBps"], "max_per_gpu": fast["per_gpu_GiBps"],
+            "slowest_rank": slow["rank"], "slowest_local_rank": slow["local_rank"],
+            "fastest_rank": fast["rank"], "spread_max_over_min": round(fast["per_gpu_GiBps"] / slow["per_gpu_GiBps"], 4),
+            "min_frac_of_run_stream_read_probe": min(x["frac_of_run_stream_read_probe"] for x in per)}
+
+
 def c5_point(torch, netcsum, args, dev, stream):
     """Same-workload retention denominator, measured at N = 1 OUTSIDE the timed region: the per-GPU
     rate of one C5 shard (16 M x 1500 B + 12 B, rank 0's slice of the global batch) on this GPU, by
@@ -344,14 +402,21 @@ def c5_point(torch, netcsum, args, dev, stream):
     except Exception as e:                        # noqa: BLE001
         parity = f"unchecked: {e}"
     desc = "netcsum::" + netcsum.last_launch()
+    # the read ceilings over the same 25 GB (a box whose C5 rate falls while these
+    # hold loses it in the kernel, one whose probes fall with it loses it in the access pattern)
+    n16 = (n * L) // 16 * 16
+    lds_gbps, run_gbps = read_probes(torch, netcsum, seg, n16, stream)
     del seg, ph, out
     torch.cuda.empty_cache()
     algo = n * (L + plen + 2)
+    ach = algo / (kern_ms * 1e-3) / 1e9
     return {"workload": f"C5 shard: {n} x {L} B TCP segments + {plen} B pseudo-header on one GPU "
                         "(rank 0's slice of the 128 M global batch)",
             "value_per_gpu": round(n * (L + plen) * k / wall / 2 ** 30, 2), "unit": "GiB/s",
             "ms_per_step": round(wall / k * 1e3, 4), "steps": k, "kernel": desc,
-            "kernel_ms": round(kern_ms, 4), "roofline_frac": round(algo / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "kernel_ms": round(kern_ms, 4), "roofline_frac": round(ach / HBM_PEAK_GBPS, 4),
+            "run_stream_read_probe_GBps": round(run_gbps, 1), "frac_of_run_stream_read_probe": round(ach / run_gbps, 4),
+            "read_stream_probe_GBps": round(lds_gbps, 1), "frac_of_read_stream_probe": round(ach / lds_gbps, 4),
             "parity_sample_ok": parity,
             "use": "retention denominator for the driver's N > 1 runs (same workload per GPU)"}
 
@@ -606,6 +671,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_env = local                              # (the device index may be folded below: gloo rehearsal)
     # RCCL ("nccl") carries the barrier and the two reductions; NETCSUM_BENCH_DIST_BACKEND=gloo (host
     # tensors) lets several ranks share one GPU to rehearse the N > 1 path (RCCL refuses duplicate GPUs)
     backend = os.environ.get("NETCSUM_BENCH_DIST_BACKEND", "nccl")
@@ -685,6 +751,7 @@ def main():
     kern_ms = sum(kern) / len(kern)
     kern_med_ms = kern[len(kern) // 2]
 
+    wall_own = wall
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -709,26 +776,22 @@ def main():
     # LDS-DMA grid-stride probe (TUNE_PROBE 1) and the run-stream form of the checksum kernel with no
     # arithmetic (TUNE_PROBE 2, netcsum_stream.hip read_run_kernel)
     n16 = (n * L) // 16 * 16
-    sink = torch.zeros(1, dtype=torch.int64, device=dev)
-    probe_ms = {}
-    for probe in (1, 2):
-        netcsum.tune(netcsum.TUNE_PROBE, probe)
-        for _ in range(20):
-            netcsum.read_stream(seg, n16, sink, stream=stream)
-        rs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
-        for a, b in rs:
-            a.record(stream)
-            netcsum.read_stream(seg, n16, sink, stream=stream)
-            b.record(stream)
-        torch.cuda.synchronize()
-        probe_ms[probe] = sum(a.elapsed_time(b) for a, b in rs) / len(rs)
-    netcsum.tune(netcsum.TUNE_PROBE, 1)
-    rs_ms = probe_ms[1]
-    run_probe_gbps = n16 / (probe_ms[2] * 1e-3) / 1e9
+    lds_probe_gbps, run_probe_gbps = read_probes(torch, netcsum, seg, n16, stream)
+    achieved = n * (L + plen + 2) / (kern_ms * 1e-3) / 1e9
+
+    # N > 1: every rank's own numbers, gathered (rank order), so that the record names a slow device
+    ranks = None
+    if world > 1:
+        own = {"rank": rank, "local_rank": local_env, "device": local, "wall_s": wall_own, "kernel_ms": kern_ms,
+               "per_gpu_GiBps": n * (L + plen) * args.steps / wall_own / 2 ** 30,
+               "run_stream_read_probe_GBps": run_probe_gbps, "read_stream_probe_GBps": lds_probe_gbps,
+               "frac_of_run_stream_read_probe": achieved / run_probe_gbps,
+               "parity_sample_ok": 1.0 if parity_ok is True else 0.0}
+        ranks = rank_summary(rank_records(dist, dev if backend == "nccl" else "cpu", own, world))
 
     c5 = None
     if world == 1 and not args.no_c5_point and n != C5_SHARD:
-        del seg, ph, out, sink
+        del seg, ph, out
         torch.cuda.empty_cache()
         try:
             c5 = c5_point(torch, netcsum, args, dev, stream)
@@ -745,7 +808,6 @@ def main():
         total_bytes = world * n * (L + plen) * args.steps
         value = total_bytes / wall / 2 ** 30
         algo_bytes = n * (L + plen + 2)
-        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
         traffic_err = "--pmc off" if args.pmc == "off" else None
         live_err = None
@@ -786,14 +848,16 @@ def main():
                          "traffic_source": traffic_src,
                          "traffic_error": traffic_err,
                          "kernel_src_sha": kernel_src_sha(kernel_desc.split("::")[-1].split("<")[0]),
-                         "read_stream_probe_GBps": round(n16 / (rs_ms * 1e-3) / 1e9, 1),
-                         "frac_of_read_stream_probe": round(achieved / (n16 / (rs_ms * 1e-3) / 1e9), 4),
+                         "read_stream_probe_GBps": round(lds_probe_gbps, 1),
+                         "frac_of_read_stream_probe": round(achieved / lds_probe_gbps, 4),
                          "run_stream_read_probe_GBps": round(run_probe_gbps, 1),
                          "frac_of_run_stream_read_probe": round(achieved / run_probe_gbps, 4)},
             "parity_sample_ok": parity_all,
         }
         if c5 is not None:
             line["c5_shard_point"] = c5
+        if ranks is not None:
+            line["ranks"] = ranks
         if world == 1:
             line["config"]["dist"] = "single rank"
         else:

@@ -143,3 +143,41 @@ def test_varlen_shard_boundaries():
         assert max(b) - min(b) <= 2 * (9000 + 12), (world, b)
     assert list(netcsum.shard_varlen(np.zeros(0, np.uint16), 12, 4)) == [0, 0, 0, 0, 0]
     assert list(netcsum.shard_varlen(np.array([100], np.uint16), 0, 3)) == [0, 1, 1, 1]
+
+
+def _rank_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 1 is the slow device: a longer wall time, a lower fraction of its own read ceiling
+    own = {"rank": rank, "local_rank": rank, "device": rank, "wall_s": 0.10 + 0.02 * rank, "kernel_ms": 3.5 + 0.3 * rank,
+           "per_gpu_GiBps": 6700.0 - 500.0 * rank, "run_stream_read_probe_GBps": 7300.0,
+           "read_stream_probe_GBps": 6990.0, "frac_of_run_stream_read_probe": 0.98 - 0.07 * rank,
+           "parity_sample_ok": 1.0}
+    recs = bench.rank_records(dist, "cpu", own, world)
+    if rank == 0:
+        q.put(bench.rank_summary(recs))
+    dist.destroy_process_group()
+
+
+def test_rank_records_name_the_slowest_device():
+    """bench.py at N > 1: every rank's own per-GPU rate, kernel time and read
+    ceilings are all-gathered, and rank 0's line names the slowest rank and its LOCAL_RANK."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    summ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r["rank"] for r in summ["per_rank"]] == [0, 1]
+    assert summ["slowest_rank"] == 1 and summ["slowest_local_rank"] == 1 and summ["fastest_rank"] == 0
+    assert summ["min_per_gpu"] == 6200.0 and summ["max_per_gpu"] == 6700.0
+    assert summ["spread_max_over_min"] == round(6700.0 / 6200.0, 4)
+    assert summ["min_frac_of_run_stream_read_probe"] == 0.91
+    assert summ["per_rank"][1]["kernel_ms"] == 3.8 and all(r["parity_sample_ok"] for r in summ["per_rank"])
+    assert set(summ["per_rank"][0]) >= {"per_gpu_GiBps", "wall_s", "run_stream_read_probe_GBps", "local_rank"}
