@@ -697,13 +697,32 @@ typedef enum netcsum_tune_key {
                                          while bursts keep coming (kernels of other streams sharing its
                                          hardware queue wait behind it at most this long plus one
                                          burst); the next burst relaunches it. 1..1000000, default 1000 */
-    NETCSUM_TUNE_FAULT_INJECT  = 25   /* TEST ONLY. 1: the calling thread's next offset/length packet
+    NETCSUM_TUNE_FAULT_INJECT  = 25,  /* TEST ONLY. 1: the calling thread's next offset/length packet
                                          batch that has a deferred pass enqueues its stream kernel,
                                          skips the deferred pass and fails (NET_UTIL_ERR_MI355X_DEV):
                                          the state a failed launch leaves; one-shot. 0: cleared      */
+    NETCSUM_TUNE_PLAN_AHEAD    = 26   /* planned batches (NIC rings, offset/length rings, segments one
+                                         per pool buffer) whose plan has no sample yet — the first batch
+                                         on a layout (NetUtil_MI355X_PlanBind) — : 1 = sample the layout
+                                         first (a one-block launch on the same stream; the call waits
+                                         for its plan word, i.e. for the stream's earlier work too) and
+                                         run this batch in its plan; 0 = run the first batch unplanned
+                                         (its own sampler block leaves the plan for the next batch);
+                                         -1 (default) = 1 from 1 Mi frames (rings) / 256 Ki segments
+                                         (pools), else 0. Never under stream capture.                 */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);
+
+/* Plan identity. The planned batch kinds — strided and offset/length NIC rings
+ * (RxValidate / TxFinalize / bursts) and offset/length segment batches one per pool buffer — choose
+ * their form from a plan the previous batch on the same layout sampled on the device, keyed on the
+ * batch's addresses (base, descriptor arrays / stride, count, IP version). A caller that places a
+ * DIFFERENT layout at the same addresses binds each layout to an id of its own: the calling thread's
+ * later batches key their plans on (addresses, plan_id) until it binds another id, so each layout keeps
+ * its plan and never runs one batch in the other's form. 0 (the default) = addresses only. Host-only;
+ * never fails. */
+NET_ERR  NetUtil_MI355X_PlanBind           (uint32_t plan_id);
 
 /* The calling thread's last batch launch: kernel form and geometry (for profiling / logs). */
 const char *NetUtil_MI355X_LastLaunch      (void);

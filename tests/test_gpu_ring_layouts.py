@@ -461,7 +461,7 @@ def test_deferred_counters_reset_after_a_failed_call(kind):
             assert "offlen +pkt_vl_deferred_kernel" in netcsum.last_launch(), netcsum.last_launch()
             for _ in range(2):
                 err, got, got_f = call()
-                assert err == 0
+                assert err == netcsum.NET_UTIL_ERR_NONE, err
                 _check(got, want, f"{kind} after failed call {rep}")
                 if got_f is not None:
                     _check(got_f, want_f, f"{kind} flags after failed call {rep}")

@@ -497,10 +497,21 @@ struct RingPlan {
     uint64_t stride = 0;
     uint32_t pkt_len = 0, n = 0, slot = 0, tag = 0, plan = 0, use = 0, calls = 0;
     int ip_ver = -1;
+    uint32_t plan_id = 0;
 };
 constexpr int kRingPlans = 16;
 thread_local RingPlan tls_ring_plans[kRingPlans];
 thread_local uint32_t tls_ring_clock = 0;
+// NetUtil_MI355X_PlanBind: the caller's identity for the layout its next batches carry (0: none, the
+// plans are keyed on the batch's addresses alone). Part of every plan key, so two layouts placed at the
+// same addresses under different ids keep a plan each and never run in the other's form.
+thread_local uint32_t tls_plan_id = 0;
+// NETCSUM_TUNE_PLAN_AHEAD: -1 auto (a batch whose plan has no word yet samples its layout first, in a
+// one-block launch the host waits for, from kPlanAheadRing frames / kPlanAheadPool segments), 0 never
+// (the first batch runs unplanned and leaves the plan for the next), 1 always.
+thread_local netcsum::TuneKnob g_tune_plan_ahead{-1};
+constexpr uint32_t kPlanAheadRing = 1u << 20;
+constexpr uint32_t kPlanAheadPool = 1u << 18;
 
 // The plan the ring's previous batch left (0: none yet), its word (host and device addresses) and tag
 // for this batch's plan block; *d_word = nullptr when no pool could be had (the batch then runs
@@ -529,7 +540,8 @@ static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t p
     RingPlan* e = nullptr;
     RingPlan* lru = &tls_ring_plans[0];
     for (RingPlan& r : tls_ring_plans) {
-        if (r.dev == dev && r.base == base && r.stride == stride && r.pkt_len == pkt_len && r.n == n && r.ip_ver == ip_ver) {
+        if (r.dev == dev && r.base == base && r.stride == stride && r.pkt_len == pkt_len && r.n == n && r.ip_ver == ip_ver &&
+            r.plan_id == tls_plan_id) {
             e = &r;
             break;
         }
@@ -545,6 +557,7 @@ static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t p
         e->pkt_len = pkt_len;
         e->n = n;
         e->ip_ver = ip_ver;
+        e->plan_id = tls_plan_id;
         e->slot = k % kPlanWords;
         e->tag = (k / kPlanWords * 2654435761u + k) & 0x7FFFu;
     }
@@ -556,6 +569,29 @@ static uint32_t ring_plan(int dev, const void* base, uint64_t stride, uint32_t p
     *d_word = pool.d + e->slot;
     *tag = e->tag;
     return e->plan;
+}
+
+// Sample a plan ahead of this batch (NETCSUM_TUNE_PLAN_AHEAD): for a plan entry that has never had a
+// word (its first batch), of at least `nmin` items, on a stream that is not being captured.
+static bool plan_ahead(hipStream_t s, uint32_t n, uint32_t nmin) {
+    const int v = g_tune_plan_ahead.load();
+    if (v == 0 || (v < 0 && n < nmin)) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (s != nullptr && hipStreamIsCapturing(s, &cs) != hipSuccess) return false;
+    return cs == hipStreamCaptureStatusNone;
+}
+
+// The plan word a sampler launch stores for `tag` (coherent host memory, system-scope store), polled:
+// the plan (bits 0-15), or 0 when none arrived within limit_ms (the batch then runs unplanned).
+static uint32_t wait_plan_word(uint32_t* h_word, uint32_t tag, int limit_ms = 2000) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const uint32_t w = *reinterpret_cast<volatile uint32_t*>(h_word);
+        if ((w >> 31) != 0u && ((w >> 16) & 0x7FFFu) == tag) return w & 0xFFFFu;
+        const auto el = std::chrono::steady_clock::now() - t0;
+        if (el > std::chrono::milliseconds(limit_ms)) return 0u;
+        if (el > std::chrono::microseconds(20)) std::this_thread::yield();
+    }
 }
 
 NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStream_t s) {
@@ -578,8 +614,23 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
         uint32_t* h_word = nullptr;
         uint32_t* d_word = nullptr;
         uint32_t tag = 0u, calls = 0u;
-        const uint32_t plan = ring_plan(dev, a.base, reinterpret_cast<uint64_t>(a.seg_off), 0xFFFFFFFEu, a.n_seg, -2,
-                                        &h_word, &d_word, &tag, &calls);
+        uint32_t plan = ring_plan(dev, a.base, reinterpret_cast<uint64_t>(a.seg_off), 0xFFFFFFFEu, a.n_seg, -2,
+                                  &h_word, &d_word, &tag, &calls);
+        const char* ahead = "";
+        if (plan == 0u && calls == 0u && d_word != nullptr && !fixed && plan_ahead(s, a.n_seg, kPlanAheadPool)) {
+            // the first batch on these descriptors: the sampler alone, waited for, so that this batch
+            // already runs in its plan (a one-block launch and a poll of the word)
+            ScratchLease word;
+            NC_HIP(word.acquire(dev, s, 256u, false));
+            uint32_t* run = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(word.ptr()) + 128);
+            *reinterpret_cast<volatile uint32_t*>(h_word) = 0u;
+            NC_HIP(netcsum::launch_varlen_runlen(a.seg_off, a.seg_len_v, a.n_seg, a.pseudo ? a.pseudo_len : 0u, c.run_bytes,
+                                                 c.stream_spw, run, d_word, tag, s));
+            NC_HIP(word.end());
+            plan = wait_plan_word(h_word, tag);
+            ahead = " ahead";
+            calls = 1u;                                   // (the pipe form below may use its plan at once)
+        }
         if ((plan & 3u) == 3u && d_word != nullptr && g_tune_kernel.load() == 0 && g_tune_group.load() == 0) {
             const int ch = g_tune_chunks.load();
             const uint32_t spw = fixed ? (uint32_t)tile_k : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (plan >> 8) & 0xFFu));
@@ -588,8 +639,8 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
             a.plan_tag = tag;
             NC_HIP(netcsum::launch_live_varlen(a, depth, spw, s));
             char d[192];
-            snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d%s,nt> block=256 segs_per_wave=%u plan=pool(live)", depth,
-                     (a.pseudo && a.pseudo_len) ? ",pseudo" : "", spw);
+            snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d%s,nt> block=256 segs_per_wave=%u plan=pool(live)%s", depth,
+                     (a.pseudo && a.pseudo_len) ? ",pseudo" : "", spw, ahead);
             netcsum::set_last_launch(d);
             return NET_UTIL_ERR_NONE;
         }
@@ -605,7 +656,7 @@ NET_ERR launch_batch(const netcsum::SegBatchArgs& a0, uint32_t len_hint, hipStre
             g_tune_chunks.store(0);
             NC_HIP(netcsum::launch_seg_batch(a, cp, s));
             char d[192];
-            snprintf(d, sizeof d, "%s plan=pool(pipe)", NetUtil_MI355X_LastLaunch());
+            snprintf(d, sizeof d, "%s plan=pool(pipe)%s", NetUtil_MI355X_LastLaunch(), ahead);
             netcsum::set_last_launch(d);
             return NET_UTIL_ERR_NONE;
         }
@@ -1190,6 +1241,7 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
                                (tb0 == 4 || (tb0 < 0 && n_pkt >= 16384u)) && rec_only == nullptr &&
                                g_tune_stream_waves_set() == false && netcsum::pkt_stream_supported(a, ip_ver, 2);
         const char* plan_note = "";
+        const char* ahead_note = "";
         bool vl_wide = true;                             // the deferred pass's grid: wide unless the plan
         bool vl_inline = false;                          // found the ring's descriptors in order; a dense
         if (plan_ring) {                                 // ring in order: the inline form (pkt_stream_kernel DEF)
@@ -1204,13 +1256,20 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
             cap = std::min<uint64_t>(cap, 64u);
             uint32_t* h_word = nullptr;
             uint32_t* d_word = nullptr;
-            uint32_t tag = 0u;
-            const uint32_t plan = d_off ? ring_plan(dev, d_base, reinterpret_cast<uint64_t>(d_off), 0xFFFFFFFFu, n_pkt,
-                                                    ip_ver, &h_word, &d_word, &tag)
-                                        : ring_plan(dev, d_base, stride, pkt_len, n_pkt, ip_ver, &h_word, &d_word, &tag);
+            uint32_t tag = 0u, calls = 0u;
+            uint32_t plan = d_off ? ring_plan(dev, d_base, reinterpret_cast<uint64_t>(d_off), 0xFFFFFFFFu, n_pkt,
+                                              ip_ver, &h_word, &d_word, &tag, &calls)
+                                  : ring_plan(dev, d_base, stride, pkt_len, n_pkt, ip_ver, &h_word, &d_word, &tag, &calls);
             if (d_word != nullptr) {
                 a.plan = run0 | ((uint32_t)cap << 8) | (tag << 16);
                 a.plan_out = d_word;
+                if (plan == 0u && calls == 0u && plan_ahead(hs, n_pkt, kPlanAheadRing)) {
+                    // the ring's first batch: its sampler alone, waited for
+                    *reinterpret_cast<volatile uint32_t*>(h_word) = 0u;
+                    NC_HIP(netcsum::launch_pkt_plan(a, ip_ver, hs));
+                    plan = wait_plan_word(h_word, tag);
+                    ahead_note = " ahead";
+                }
                 const uint32_t form = plan & 0x7u, pw = (plan >> 4) & 0xFu, prun = (plan >> 8) & 0xFFu;
                 if (plan != 0u && d_off != nullptr) {
                     vl_wide = (plan & 8u) != 0u;
@@ -1247,11 +1306,11 @@ static NET_ERR pkt_batch(const void* d_base, const uint64_t* d_off, const uint16
                 spw = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(spw, cap));
             }
         }
-        char desc[200];
-        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s%s", d,
+        char desc[208];
+        snprintf(desc, sizeof desc, "pkt_stream_kernel<D=%d%s,%s,%s> block=256 pkts_per_wave=%u bound=%d%s%s%s%s%s", d,
                  snt ? ",nt" : "", tx ? "tx" : "rx", ip_ver == 4 ? "v4" : ip_ver == 6 ? "v6" : "mixed", spw, bound,
                  d_off ? (vl_inline ? " offlen (inline fallback)" : " offlen +pkt_vl_deferred_kernel") : "",
-                 two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "", plan_note);
+                 two ? " +pkt_scatter_kernel" : "", walk ? " +inline_v6_walk" : "", plan_note, ahead_note);
         netcsum::set_last_launch(desc);
         // scratch slot layout (one slot per (thread, device, stream), shared by every batch kind on the
         // stream, which stream order keeps apart): [0, 256) the words that must survive other calls'
@@ -2171,6 +2230,11 @@ NET_ERR NetUtil_MI355X_ReadStream(const void* d_buf, uint64_t n_bytes, uint64_t*
     return NET_UTIL_ERR_NONE;
 }
 
+NET_ERR NetUtil_MI355X_PlanBind(uint32_t plan_id) {
+    tls_plan_id = plan_id;
+    return NET_UTIL_ERR_NONE;
+}
+
 NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     switch (key) {
     case NETCSUM_TUNE_GRID_BLOCKS:
@@ -2265,6 +2329,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_BURST_SERVER_LIFE_US:
         if (value < 1 || value > 1000000) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_burst_life.store(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_PLAN_AHEAD:
+        if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_plan_ahead.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_FAULT_INJECT:
         if (value < 0 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

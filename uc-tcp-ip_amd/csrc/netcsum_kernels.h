@@ -195,6 +195,9 @@ void set_tx_flush(int mode);
 // host applies them)
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,
                              hipStream_t s, PktTxRecord* rec = nullptr, bool scatter = true);
+// The ring plan's sampler alone (one block; a.plan, a.plan_out and the batch's descriptors / stride as
+// for the batch): the plan word for the batch about to be launched, which the host waits for.
+hipError_t launch_pkt_plan(const PktBatchArgs& a, int ip_ver, hipStream_t s);
 // Test-only fault (NETCSUM_TUNE_FAULT_INJECT 1): the calling thread's next offset/length packet batch
 // with a deferred pass enqueues its stream kernel, skips the deferred pass and fails with
 // hipErrorLaunchFailure — the state a failed deferred launch leaves (the list counters not reset).

@@ -1004,6 +1004,13 @@ __device__ void pkt_plan_block(const PktBatchArgs& A) {
     }
 }
 
+// The same sampler as a launch of its own (one block), ahead of a ring's FIRST batch when the host
+// waits for the plan instead of letting the first batch run unplanned (launch_pkt_plan, abi ring_plan).
+template <int VER, bool VL>
+__global__ void __launch_bounds__(256) pkt_plan_kernel(PktBatchArgs A) {
+    pkt_plan_block<VER, VL>(A);
+}
+
 // DEF (offset/length): runs not in order within the reach are listed for the deferred pass (true) or
 // done inline, one datagram at a time (false: the kernel then carries that loop, 79-93 VGPRs, 5-6 waves
 // per SIMD — the residency the dense offset/length rings want anyway, so their ring plan takes this
@@ -1404,6 +1411,16 @@ bool pkt_stream_supported(const PktBatchArgs& a, int ip_ver, int bound) {
     if (bound >= 1 && a.len_u + 128u > kLiveReach) return false;        // a run of one spans <= 63 KiB
     return a.len_u >= 64u && a.stride >= a.len_u && ((bound == 1 || bound == 2) || a.stride <= a.len_u + 64u) &&
            (uint64_t)kMaxRunPkts * a.stride < (1ull << 31);
+}
+
+hipError_t launch_pkt_plan(const PktBatchArgs& a, int ip_ver, hipStream_t s) {
+    if (a.plan_out == nullptr || a.n == 0u) return hipErrorInvalidValue;
+    const bool vl = a.off != nullptr;
+#define NETCSUM_PP(V_, VL_) \
+    if (ip_ver == V_ && vl == VL_) { hipLaunchKernelGGL((pkt_plan_kernel<V_, VL_>), dim3(1), dim3(256), 0, s, a); return hipGetLastError(); }
+    NETCSUM_PP(4, false) NETCSUM_PP(4, true) NETCSUM_PP(6, false) NETCSUM_PP(6, true) NETCSUM_PP(0, false) NETCSUM_PP(0, true)
+#undef NETCSUM_PP
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_pkt_stream(const PktBatchArgs& a, int ip_ver, int depth, uint32_t spw, bool nt, bool tx, int bound,

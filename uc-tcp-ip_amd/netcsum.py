@@ -73,6 +73,7 @@ TUNE_BURST_ZERO_COPY = 22
 TUNE_BURST_SERVER_IDLE_US = 23
 TUNE_BURST_SERVER_LIFE_US = 24
 TUNE_FAULT_INJECT = 25          # test only: the next offset/length packet batch skips its deferred pass and fails
+TUNE_PLAN_AHEAD = 26            # first batch on a layout: sample it first and run in its plan (-1 auto, 0, 1)
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
@@ -262,6 +263,8 @@ def lib() -> ctypes.CDLL:
     L.NetUtil_MI355X_ReadStream.restype = i32
     L.NetUtil_MI355X_Tune.argtypes = [i32, i32]
     L.NetUtil_MI355X_Tune.restype = i32
+    L.NetUtil_MI355X_PlanBind.argtypes = [u32]
+    L.NetUtil_MI355X_PlanBind.restype = i32
     L.NetUtil_MI355X_LastLaunch.argtypes = []
     L.NetUtil_MI355X_LastLaunch.restype = ctypes.c_char_p
     L.NetUtil_MI355X_Version.argtypes = []
@@ -669,6 +672,11 @@ def read_stream(buf, n_bytes, sink, stream=None):
 
 def tune(key, value):
     _check(lib().NetUtil_MI355X_Tune(key, value), "NetUtil_MI355X_Tune")
+
+
+def plan_bind(plan_id):
+    """NetUtil_MI355X_PlanBind: this thread's later planned batches key their plans on plan_id too."""
+    _check(lib().NetUtil_MI355X_PlanBind(plan_id), "NetUtil_MI355X_PlanBind")
 
 
 def last_launch() -> str:
