@@ -390,6 +390,13 @@ def c5_point(torch, netcsum, args, dev, stream):
         b.record(stream)
     torch.cuda.synchronize()
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / k
+    # diagnostic: the same launches without the pseudo-header stream (a second address stream)
+    for a, b in evs:
+        a.record(stream)
+        netcsum.batch_strided(seg, L, L, None, 0, 0, n, out, netcsum.OP_DATA_CALC, stream=stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    nop_ms = sum(a.elapsed_time(b) for a, b in evs) / k
     parity = None
     try:
         import oracle
@@ -417,6 +424,7 @@ def c5_point(torch, netcsum, args, dev, stream):
             "kernel_ms": round(kern_ms, 4), "roofline_frac": round(ach / HBM_PEAK_GBPS, 4),
             "run_stream_read_probe_GBps": round(run_gbps, 1), "frac_of_run_stream_read_probe": round(ach / run_gbps, 4),
             "read_stream_probe_GBps": round(lds_gbps, 1), "frac_of_read_stream_probe": round(ach / lds_gbps, 4),
+            "kernel_ms_no_pseudo_headers": round(nop_ms, 4),
             "parity_sample_ok": parity,
             "use": "retention denominator for the driver's N > 1 runs (same workload per GPU)"}
 
@@ -625,6 +633,51 @@ def live_traffic(args, n, kernel_desc):
     b = vals["FETCH_SIZE"] * 1024 * 2 + vals["WRITE_SIZE"] * 1024
     return b, (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 3-launch child run "
                f"(median per launch: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KB x2, WRITE_SIZE {vals['WRITE_SIZE']:.0f} KB)"), None
+
+
+C5_COUNTERS = ("TCP_UTCL1_TRANSLATION_MISS_sum", "TCP_UTCL1_REQUEST_sum", "TCP_UTCL1_STALL_INFLIGHT_MAX_sum",
+               "TCP_TCC_READ_REQ_LATENCY_sum", "GRBM_UTCL2_BUSY", "GRBM_GUI_ACTIVE", "TCC_EA0_RDREQ_sum", "TCC_TAG_STALL_sum")
+
+
+def live_c5_counters(args):
+    """VERDICT r5 next #1, on whatever box runs the bench: one rocprofv3 --pmc pass (4 TCP, 2 GRBM, 2 TCC
+    counters: within one pass's limits) over a child run of the C5 shard (3 launches, then the bench's
+    two read probes over the same 25 GB), so that the record says, for the checksum kernel and for
+    read_run_kernel (its access pattern, no arithmetic), how many address translations missed the
+    UTCL1, how busy the UTCL2 was and the L2's HBM read requests — a box where the kernel falls behind
+    the probe shows there which of them differs. Returns {kernel short name: {counter: median}}."""
+    import csv
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return {"error": "rocprofv3 not on PATH"}
+    tmp = tempfile.mkdtemp(prefix="bench_c5pmc_", dir="/tmp")
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1", "--ramp-seconds", "0",
+             "--no-cpu-baseline", "--no-c5-point", "--pmc", "off", "--segments", str(C5_SHARD), "--seg-len",
+             str(args.seg_len), "--pseudo-len", str(args.pseudo_len)]
+    cmd = ["timeout", "-s", "KILL", "180", exe, "--pmc", *C5_COUNTERS, "-d", tmp, "-o", "c5", "--output-format", "csv",
+           "--"] + child
+    r = subprocess.run(cmd, cwd="/tmp", env={**os.environ, "TMPDIR": "/tmp"}, capture_output=True, text=True)
+    if r.returncode != 0:
+        shutil.rmtree(tmp, ignore_errors=True)
+        return {"error": f"rocprofv3 exited {r.returncode}: {r.stderr.strip()[-300:]}"}
+    vals = {}
+    for f in glob.glob(os.path.join(tmp, "**", "c5_counter_collection.csv"), recursive=True):
+        for x in csv.DictReader(open(f)):
+            k = next((n for n in ("seg_stream_kernel", "read_run_kernel", "read_stream_lds_kernel") if n in x["Kernel_Name"]), None)
+            if k:
+                vals.setdefault(k, {}).setdefault(x["Counter_Name"], []).append(float(x["Counter_Value"]))
+    shutil.rmtree(tmp, ignore_errors=True)
+    out = {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in vals.items()}
+    for k, d in out.items():
+        if d.get("TCP_UTCL1_REQUEST_sum"):
+            d["utcl1_miss_per_request"] = round(d.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0) / d["TCP_UTCL1_REQUEST_sum"], 7)
+        if d.get("GRBM_GUI_ACTIVE"):
+            d["utcl2_busy_frac"] = round(d.get("GRBM_UTCL2_BUSY", 0.0) / d["GRBM_GUI_ACTIVE"], 5)
+    return out or {"error": "no counter rows for the C5 kernels"}
 
 
 def load_traffic(path, n_seg, kernel_desc):
@@ -855,6 +908,8 @@ def main():
             "parity_sample_ok": parity_all,
         }
         if c5 is not None:
+            if args.pmc == "live" and "error" not in c5:
+                c5["pmc_live"] = live_c5_counters(args)
             line["c5_shard_point"] = c5
         if ranks is not None:
             line["ranks"] = ranks

@@ -701,7 +701,7 @@ typedef enum netcsum_tune_key {
                                          batch that has a deferred pass enqueues its stream kernel,
                                          skips the deferred pass and fails (NET_UTIL_ERR_MI355X_DEV):
                                          the state a failed launch leaves; one-shot. 0: cleared      */
-    NETCSUM_TUNE_PLAN_AHEAD    = 26   /* planned batches (NIC rings, offset/length rings, segments one
+    NETCSUM_TUNE_PLAN_AHEAD    = 26,  /* planned batches (NIC rings, offset/length rings, segments one
                                          per pool buffer) whose plan has no sample yet — the first batch
                                          on a layout (NetUtil_MI355X_PlanBind) — : 1 = sample the layout
                                          first (a one-block launch on the same stream; the call waits
@@ -710,6 +710,10 @@ typedef enum netcsum_tune_key {
                                          (its own sampler block leaves the plan for the next batch);
                                          -1 (default) = 1 from 1 Mi frames (rings) / 256 Ki segments
                                          (pools), else 0. Never under stream capture.                 */
+    NETCSUM_TUNE_LIVE_COMPACT  = 27   /* live-sector streams (segments one per pool buffer): 1 / -1
+                                         (default) the run's live 64-B sectors read compacted, 16 per
+                                         wave-instruction; 0 the live 1-KiB pieces of the run's span,
+                                         each lane loading its 16 B where its sector is live          */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -62,9 +62,10 @@ __global__ void fill_kernel(u32x4* p, uint64_t n16) {
 }
 
 // bit s of bits: sector s (bytes [64 s, 64 s + 64) of the ring) holds datagram bytes (slot i's length:
-// lens[i], or `len` for every slot when lens is null)
+// lens[i], or `len` for every slot when lens is null); win > 0: a datagram that ends within win bytes of
+// its first 16-B chunk holds none (the kernels sum it from the window loaded at its start)
 __global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, uint32_t lead, uint32_t len,
-                               const uint16_t* lens, uint32_t n) {
+                               const uint16_t* lens, uint32_t n, uint32_t win) {
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w * 32u >= nsect) return;
     uint32_t m = 0;
@@ -73,18 +74,36 @@ __global__ void sectors_kernel(uint32_t* bits, uint64_t nsect, uint64_t stride, 
         const uint64_t a = s0 / stride;
         bool live = false;
         for (uint64_t i = a; i <= (s1 - 1u) / stride; ++i) {
-            const uint64_t d0 = i * stride + lead, d1 = d0 + (lens ? (i < n ? lens[i] : 0u) : len);
-            live = live || (s0 < d1 && d0 < s1);
+            const uint32_t l = lens ? (i < n ? lens[i] : 0u) : len;
+            const uint64_t d0 = i * stride + lead, d1 = d0 + l;
+            const bool inwin = win != 0u && (uint32_t)(d0 & 15u) + l <= win;
+            live = live || (!inwin && s0 < d1 && d0 < s1);
         }
         m |= live ? (1u << b) : 0u;
     }
     bits[w] = m;
 }
 
-template <bool LIVE, int D, bool TOUCH>
+__device__ __forceinline__ uint32_t incl_scan64(uint32_t v, uint32_t lane) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    return v + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
+}
+
+// LIVE: 0 every piece of the span, 1 the live pieces (lanes load their live sectors), 2 the live
+// sectors compacted (16 per wave-instruction, in address order: lane l the 16 B at (l & 3) 16 of live
+// sector 16 q + l / 4). TOUCH: 0 none, 1 lane k loads the 16 B at datagram k's start (plain), 2 the six
+// 16-B chunks from there (the packet kernels' 96-B header window).
+template <int LIVE, int D, int TOUCH>
 __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_t ring_bytes, uint32_t n, uint64_t stride,
                                                     uint32_t lead, uint32_t len, uint32_t R, const uint32_t* bits,
                                                     uint32_t* sink) {
+    __shared__ uint16_t lst_all[4][1024];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t s_begin = ((uint64_t)blockIdx.x * 4u + w) * R;
@@ -98,7 +117,7 @@ __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_
     const uint32_t lane16 = 16u * lane;
     uint64_t lm = 0;                                                     // live pieces (bit 63: sentinel)
     uint32_t pm = 0;                                                     // sector mask of piece `lane`
-    if constexpr (LIVE) {
+    if constexpr (LIVE != 0) {
         // piece `lane`: its 16 sectors start at sector O / 64 + 16 lane (O is 128-B aligned)
         const uint64_t s = O / 64u + 16u * lane;
         if (lane < npieces) {                                            // (words inside the bitmap)
@@ -108,26 +127,46 @@ __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_
         lm = __builtin_amdgcn_ballot_w64(pm != 0u) | (1ull << 63);
     }
     const uint32_t lbit = 1u << (lane >> 2);
+    uint32_t nsect = 0;
+    uint16_t* lst = lst_all[w];
+    if constexpr (LIVE == 2) {
+        const uint32_t cnt = (uint32_t)__builtin_popcount(pm);
+        const uint32_t incl = incl_scan64(cnt, lane);
+        nsect = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        for (uint32_t m = pm, pos = incl - cnt; m != 0u; m &= m - 1u) lst[pos++] = (uint16_t)((lane << 4) | (uint32_t)__builtin_ctz(m));
+        __builtin_amdgcn_wave_barrier();
+    }
     auto pop = [&]() -> uint32_t {
         const uint32_t q = (uint32_t)__builtin_ctzll(lm);
         lm = (lm & (lm - 1u)) | (1ull << 63);
         return q;
     };
     auto voff = [&](uint32_t q) -> uint32_t {
-        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm, (int)q);
-        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+        if constexpr (LIVE == 2) {
+            const uint32_t i = (q << 4) + (lane >> 2);
+            return i < nsect ? ((uint32_t)lst[i < 1023u ? i : 1023u] << 6) + ((lane & 3u) << 4) : kOOB;
+        } else {
+            const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm, (int)q);
+            return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+        }
     };
-    const uint32_t nlive = LIVE ? (uint32_t)__builtin_popcountll(lm) - 1u : npieces;
-    // touch: lane k loads the 16 B at datagram k's start (plain policy), as the kernel's parse does
+    const uint32_t nlive = LIVE == 2 ? (nsect + 15u) >> 4 : LIVE ? (uint32_t)__builtin_popcountll(lm) - 1u : npieces;
+    // touch: lane k loads the 16 B at datagram k's start (plain policy), as the kernel's parse does; TOUCH
+    // 2: the 96-B header window (six chunks)
     u32x4 tv = {0u, 0u, 0u, 0u};
-    if constexpr (TOUCH) {
-        tv = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(lane < nres ? ((uint32_t)(a0 - O) + lane * (uint32_t)stride) & ~15u : kOOB), 0, 0);
+    if constexpr (TOUCH != 0) {
+        const uint32_t t0 = lane < nres ? ((uint32_t)(a0 - O) + lane * (uint32_t)stride) & ~15u : kOOB;
+#pragma unroll
+        for (int c = 0; c < (TOUCH == 2 ? 6 : 1); ++c) {
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(t0 == kOOB ? kOOB : t0 + 16u * (uint32_t)c), 0, 0);
+            tv = u32x4{tv.x ^ x.x, tv.y ^ x.y, tv.z ^ x.z, tv.w ^ x.w};
+        }
     }
     u32x4 dv[D];
     uint32_t qd[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        qd[j] = LIVE ? pop() : (uint32_t)j;
+        qd[j] = LIVE == 1 ? pop() : (uint32_t)j;
         dv[j] = ld16(rd, LIVE ? voff(qd[j]) : ((uint32_t)j << 10) + lane16);
     }
     uint32_t acc = 0;
@@ -136,8 +175,11 @@ __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* ring, uint64_
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             acc = add4(opaque(dv[j]), acc);
-            if constexpr (LIVE) {
+            if constexpr (LIVE == 1) {
                 qd[j] = pop();
+                dv[j] = ld16(rd, voff(qd[j]));
+            } else if constexpr (LIVE == 2) {
+                qd[j] += (uint32_t)D;
                 dv[j] = ld16(rd, voff(qd[j]));
             } else {
                 dv[j] = ld16(rd, ((r * D + (uint32_t)j + D) << 10) + lane16);
@@ -155,26 +197,32 @@ int main(int argc, char** argv) {
         const char* name;
         uint64_t stride;
         uint32_t lead, len;
-        bool mix;
+        int mix;           // 0 uniform `len`; 1 segments 20 / 556 / 1480 B; 2 datagrams 40 / 576 / 1500 B (7 : 4 : 1)
+        uint32_t win;      // sectors of datagrams ending within `win` B of their first chunk are not live
     };
     // default: the packet rows' rings; or layouts from the command line as NAME STRIDE LEAD LEN ...
     // (round 5: TCP segments at TransportHdrIx of pool buffers, `seg1520 1520 34 1480`, `seg2k 2048 84
     // 1480`, and the chain row's fragments, `frag2k 2048 42 1480`; LEN `mix`: segments of 20 / 556 /
     // 1480 B at 7 : 4 : 1 — the 40 / 576 / 1500-B datagram mix — drawn per slot, `seg1520mix 1520 34 mix`)
-    std::vector<Layout> layouts = {{"packed", 1500, 0, 1500, false}, {"template", 1520, 14, 1500, false},
-                                   {"nb2k", 2048, 64, 1500, false}};
+    // (round 6: LEN `mixwin`: the segment mix with the pool kernel's in-window rule — a segment ending
+    // within 48 B of its first chunk is read by that lane's window loads, not as sectors; `ringmix`: the
+    // 40 / 576 / 1500-B datagram mix with the packet kernel's 96-B header window, `ring 1520 14 ringmix`)
+    std::vector<Layout> layouts = {{"packed", 1500, 0, 1500, 0, 0}, {"template", 1520, 14, 1500, 0, 0},
+                                   {"nb2k", 2048, 64, 1500, 0, 0}};
     if (argc > 1) {
         layouts.clear();
         for (int i = 1; i + 3 < argc; i += 4) {
             const uint64_t st = std::strtoull(argv[i + 1], nullptr, 10);
-            const bool mix = std::string(argv[i + 3]) == "mix";
+            const std::string lt = argv[i + 3];
+            const int mix = (lt == "mix" || lt == "mixwin") ? 1 : lt == "ringmix" ? 2 : 0;
+            const uint32_t win = lt == "mixwin" ? 48u : lt == "ringmix" ? 96u : 0u;
             const uint32_t ld = (uint32_t)std::strtoul(argv[i + 2], nullptr, 10),
-                           ln = mix ? 1480u : (uint32_t)std::strtoul(argv[i + 3], nullptr, 10);
+                           ln = mix == 1 ? 1480u : mix == 2 ? 1500u : (uint32_t)std::strtoul(argv[i + 3], nullptr, 10);
             if (st == 0 || st > 2048u || ld + ln > st) {
                 std::fprintf(stderr, "layout %s: need stride <= 2048 and lead + len <= stride\n", argv[i]);
                 return 2;
             }
-            layouts.push_back({argv[i], st, ld, ln, mix});
+            layouts.push_back({argv[i], st, ld, ln, mix, win});
         }
     }
     const uint32_t n = 1u << 20;
@@ -182,17 +230,21 @@ int main(int argc, char** argv) {
     uint8_t* ring = nullptr;
     uint32_t *bits = nullptr, *sink = nullptr;
     uint16_t* dlens = nullptr;
-    std::vector<uint16_t> hmix(n);
+    std::vector<uint16_t> hmix(n), hring(n);
     {
         uint64_t x = 0x5EED0001ull;                                      // 20 / 556 / 1480 B at 7 : 4 : 1
         for (uint32_t i = 0; i < n; ++i) {
             x = x * 6364136223846793005ull + 1442695040888963407ull;
             const uint32_t r = (uint32_t)(x >> 33) % 12u;
             hmix[i] = r < 7u ? 20u : r < 11u ? 556u : 1480u;
+            hring[i] = (uint16_t)(hmix[i] + 20u);                        // the datagrams: 40 / 576 / 1500 B
         }
     }
+    uint16_t* dring = nullptr;
     CK(hipMalloc(&dlens, (size_t)n * 2u));
     CK(hipMemcpy(dlens, hmix.data(), (size_t)n * 2u, hipMemcpyHostToDevice));
+    CK(hipMalloc(&dring, (size_t)n * 2u));
+    CK(hipMemcpy(dring, hring.data(), (size_t)n * 2u, hipMemcpyHostToDevice));
     CK(hipMalloc(&ring, ring_bytes));
     CK(hipMalloc(&bits, ring_bytes / 64u / 8u + 1024u));
     CK(hipMemset(bits, 0, ring_bytes / 64u / 8u + 1024u));
@@ -204,12 +256,13 @@ int main(int argc, char** argv) {
     for (const Layout& L : layouts) {
         const uint64_t bytes = (uint64_t)n * L.stride + 4096u;
         const uint64_t nsect = bytes / 64u;
+        const uint16_t* lensp = L.mix == 1 ? dlens : L.mix == 2 ? dring : nullptr;
         hipLaunchKernelGGL(sectors_kernel, dim3((unsigned)((nsect / 32u + 256u) / 256u)), dim3(256), 0, 0, bits, nsect,
-                           L.stride, L.lead, L.len, L.mix ? dlens : nullptr, n);
+                           L.stride, L.lead, L.len, lensp, n, L.win);
         uint64_t dbytes = (uint64_t)n * L.len;
         if (L.mix) {
             dbytes = 0;
-            for (uint16_t m : hmix) dbytes += m;
+            for (uint16_t m : (L.mix == 1 ? hmix : hring)) dbytes += m;
         }
         CK(hipDeviceSynchronize());
         std::vector<uint32_t> hb(nsect / 32u);
@@ -222,21 +275,25 @@ int main(int argc, char** argv) {
             const char* tag;
             int live, d, touch;
         } vs[] = {{"whole", 0, 4, 0}, {"live", 1, 4, 0}, {"live.touch", 1, 4, 1}, {"live.d8", 1, 8, 0},
-                  {"live.d8.touch", 1, 8, 1}, {"whole.touch", 0, 4, 1}};
+                  {"live.d8.touch", 1, 8, 1}, {"whole.touch", 0, 4, 1}, {"compact", 2, 4, 0}, {"compact.touch", 2, 4, 1},
+                  {"compact.d8.touch", 2, 8, 1}, {"live.win", 1, 4, 2}, {"compact.win", 2, 4, 2}};
         for (int pass = 0; pass < 2; ++pass) {
             for (const V& v : vs) {
-                for (uint32_t R : {8u, 16u, 32u}) {
+                if ((v.touch == 2) != (L.mix == 2)) continue;            // the 96-B window: the ring only
+                for (uint32_t R : {8u, 16u, 30u, 32u, 41u}) {
                     if ((uint64_t)R * L.stride + 2048u > (63u << 10)) continue;   // a run within the bitmap's reach
+                    if ((R == 30u || R == 41u) && (uint64_t)(R + 1u) * L.stride + 2048u <= (63u << 10)) continue;   // (the longest run only)
                     const uint64_t waves = (n + R - 1u) / R;
                     const dim3 g((unsigned)((waves + 3u) / 4u)), b(256);
                     auto launch = [&]() {
 #define LRP_L(LV, DD, TT) hipLaunchKernelGGL((probe_kernel<LV, DD, TT>), g, b, 0, 0, ring, bytes, n, L.stride, L.lead, L.len, R, bits, sink)
-                        if (v.live && v.d == 4 && !v.touch) LRP_L(true, 4, false);
-                        else if (v.live && v.d == 4) LRP_L(true, 4, true);
-                        else if (v.live && !v.touch) LRP_L(true, 8, false);
-                        else if (v.live) LRP_L(true, 8, true);
-                        else if (!v.touch) LRP_L(false, 4, false);
-                        else LRP_L(false, 4, true);
+#define LRP_T(LV, DD) if (v.touch == 0) LRP_L(LV, DD, 0); else if (v.touch == 1) LRP_L(LV, DD, 1); else LRP_L(LV, DD, 2);
+                        if (v.live == 0) { LRP_T(0, 4) }
+                        else if (v.live == 1 && v.d == 4) { LRP_T(1, 4) }
+                        else if (v.live == 1) { LRP_T(1, 8) }
+                        else if (v.d == 4) { LRP_T(2, 4) }
+                        else { LRP_T(2, 8) }
+#undef LRP_T
 #undef LRP_L
                     };
                     for (int i = 0; i < 200; ++i) launch();
@@ -266,5 +323,6 @@ int main(int argc, char** argv) {
     CK(hipFree(bits));
     CK(hipFree(sink));
     CK(hipFree(dlens));
+    CK(hipFree(dring));
     return 0;
 }

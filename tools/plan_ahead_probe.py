@@ -46,8 +46,11 @@ def main():
     torch.cuda.synchronize()
     pid = 1000
     res = {k: {"unplanned": [], "ahead": [], "planned": [], "desc": {}} for k in cases}
+    # each case's planned id (the pool cases share their descriptor arrays' addresses: under one id
+    # each would run in the other's plan)
+    home = {name: 1 + i for i, name in enumerate(cases)}
     for name, fn in cases.items():                     # warm: each case's kernels and its planned id
-        netcsum.plan_bind(1)
+        netcsum.plan_bind(home[name])
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -55,7 +58,7 @@ def main():
         for name, fn in cases.items():
             for mode in ("unplanned", "ahead", "planned"):
                 if mode == "planned":
-                    netcsum.plan_bind(1)
+                    netcsum.plan_bind(home[name])
                 else:
                     pid += 1
                     netcsum.plan_bind(pid)

@@ -33,7 +33,8 @@ from ring_probe import events_ms  # noqa: E402
 LAYOUTS = {"pool1520": (1520, 34, False), "pool1520mix": (1520, 34, True), "pool2k": (2048, 84, False),
            "pool2kmix": (2048, 84, True), "c4": (0, 0, False)}
 VARIANTS = [("default", {}), ("pipe16", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GROUP_LANES: 16, netcsum.TUNE_CHUNKS: 6}),
-            ("runs8", {netcsum.TUNE_VARLEN_RUN_BYTES: 0})]
+            ("runs8", {netcsum.TUNE_VARLEN_RUN_BYTES: 0}),
+            ("pieces", {netcsum.TUNE_LIVE_COMPACT: 0})]   # round 6: the live pieces, not the compacted sectors
 if os.environ.get("POOL_LIVE"):                       # live-sector stream: run length x pieces in flight
     for r, dd in ((8, 4), (8, 8), (16, 4), (16, 8), (24, 4), (32, 4), (32, 8), (40, 4)):
         VARIANTS.append((f"live.s{r}.d{dd}", {netcsum.TUNE_TILE: r, netcsum.TUNE_CHUNKS: dd}))
@@ -42,7 +43,7 @@ if os.environ.get("POOL_PIPES"):                      # lane-group pipe geometri
         VARIANTS.append((f"pipe{g}k{k}t{t}", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GROUP_LANES: g,
                                               netcsum.TUNE_CHUNKS: k, netcsum.TUNE_TILE: t}))
 RESET = {netcsum.TUNE_KERNEL: 0, netcsum.TUNE_GROUP_LANES: 0, netcsum.TUNE_CHUNKS: 0, netcsum.TUNE_VARLEN_RUN_BYTES: -1,
-         netcsum.TUNE_TILE: -1}
+         netcsum.TUNE_TILE: -1, netcsum.TUNE_LIVE_COMPACT: -1}
 
 
 def main():

@@ -180,6 +180,10 @@ hipError_t launch_varlen_runlen(const uint64_t* offs, const uint16_t* lens, uint
 // one extra block samples the descriptors for the next batch's plan.
 hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hipStream_t s);
 void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
+// NETCSUM_TUNE_LIVE_COMPACT: the live-sector streams read their live sectors compacted, 16 per
+// wave-instruction (-1 default / 1), or as the live 1-KiB pieces of their span (0)
+void set_live_compact(int v);
+bool live_compact();
 uint32_t varlen_run_bytes();
 constexpr uint32_t kVarlenSpwMin = 3u;
 void set_hdr_burst(int v);     // NETCSUM_TUNE_HDR_BURST: header stream results written per run (1) or per piece (0)

@@ -59,6 +59,19 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 47) + (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Inclusive prefix sum over the 64 lanes (every lane active): the row scans of wave_total, then the
+// totals of the rows below added from lanes 15 / 31 / 47.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    return v + (lane >= 16u ? r0 : 0u) + (lane >= 32u ? r1 : 0u) + (lane >= 48u ? r2 : 0u);
+}
+
 // Row touch. Before streaming its run, a wave loads the first dword of every 1-KiB piece of the run
 // (lane q: piece q, and q + 64; plain cache policy) and never uses the values. The stream's own
 // loads are non-temporal 1-KiB wave-instructions issued D at a time; the touches put a request into

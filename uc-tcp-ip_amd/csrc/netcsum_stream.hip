@@ -520,7 +520,7 @@ __device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16
 constexpr uint64_t kSentinelPiece = 1ull << 63;
 constexpr uint32_t kNoEnd = ~0u;
 
-template <int D, int PH, bool NT>
+template <int D, int PH, bool NT, bool CMP>
 __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, uint32_t spw) {
     __shared__ uint32_t sect_all[4][32];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -649,9 +649,46 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
     }
     __builtin_amdgcn_wave_barrier();
     const uint32_t pm0 = reinterpret_cast<const uint16_t*>(sect)[lane];
-    uint64_t lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
-    const uint32_t nlive = (uint32_t)__builtin_popcountll(lm0);
-    lm0 |= kSentinelPiece;
+    const bool streamed = mine && len != 0u && !inwin;
+    // CMP: the run's live sectors COMPACTED, in address order, 16 per wave-instruction (lane l: the
+    // 16 B at (l & 3) * 16 of live sector 16 q + l / 4): a mixed pool's run holds ≈ 13 KB in ≈ 250
+    // sectors spread over ≈ 60 pieces, so the piece stream below waits for ≈ 15 rounds of D partly
+    // live pieces, the compacted one for ≈ 4 rounds of whole ones. A segment's bytes then lie at
+    // compacted offsets [cs_l, ce_l): sector s moves to 64 x its rank among the live sectors, so byte
+    // parity and 16-B alignment are kept, segments stay in address order, and the event walk below is
+    // the same with those offsets (the sector bytes outside every segment are masked as gaps are).
+    uint32_t nunits = 0u;                                      // pieces (or compacted pieces) to stream
+    uint32_t cs_l = 0u, ce_l = 0u;                             // CMP: lane k's compacted start / end
+    uint32_t nsect = 0u;                                       // CMP: the run's live sectors
+    uint64_t lm0 = 0u;
+    uint16_t* lst = nullptr;
+    if constexpr (CMP) {
+        __shared__ uint16_t lst_all[4][1024];                  // live sector indices (run-relative)
+        lst = lst_all[w];
+        const uint32_t cnt = (uint32_t)__builtin_popcount(pm0);
+        const uint32_t incl = wave_incl_scan(cnt, lane);
+        const uint32_t excl = incl - cnt;
+        nsect = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        for (uint32_t m = pm0, pos = excl; m != 0u; m &= m - 1u) {
+            lst[pos++] = (uint16_t)((lane << 4) | (uint32_t)__builtin_ctz(m));
+        }
+        auto rank = [&](uint32_t sidx) -> uint32_t {          // live sectors below sector sidx
+            const int q = (int)(sidx >> 4);
+            const uint32_t ex = (uint32_t)__shfl((int)excl, q, 64);
+            const uint32_t pm = (uint32_t)__shfl((int)pm0, q, 64);
+            return ex + (uint32_t)__builtin_popcount(pm & ((1u << (sidx & 15u)) - 1u));
+        };
+        const uint32_t r0 = rank(streamed ? (uint32_t)rel >> 6 : 0u);
+        const uint32_t r1 = rank(streamed ? ((uint32_t)end - 1u) >> 6 : 0u);
+        cs_l = streamed ? (r0 << 6) | ((uint32_t)rel & 63u) : 0u;
+        ce_l = streamed ? (r1 << 6) + (((uint32_t)end - 1u) & 63u) + 1u : 0u;
+        nunits = (nsect + 15u) >> 4;
+        __builtin_amdgcn_wave_barrier();                       // (the list written before any lane reads it)
+    } else {
+        lm0 = __builtin_amdgcn_ballot_w64(pm0 != 0u);
+        nunits = (uint32_t)__builtin_popcountll(lm0);
+        lm0 |= kSentinelPiece;
+    }
     const uint32_t lbit = 1u << (lane >> 2);
     auto pop = [&]() -> uint32_t {
         const uint32_t q = (uint32_t)__builtin_ctzll(lm0);
@@ -659,14 +696,19 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         return q;
     };
     auto live_voff = [&](uint32_t q) -> uint32_t {
-        const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
-        return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+        if constexpr (CMP) {                                   // compacted piece q: sector 16 q + lane / 4
+            const uint32_t i = (q << 4) + (lane >> 2);
+            return i < nsect ? ((uint32_t)lst[min(i, 1023u)] << 6) + ((lane & 3u) << 4) : kOOB;
+        } else {
+            const uint32_t sm = (uint32_t)__builtin_amdgcn_readlane((int)pm0, (int)q);
+            return (sm & lbit) ? (q << 10) + lane16 : kOOB;
+        }
     };
     u32x4 dv[D];
     uint32_t qd[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        qd[j] = pop();
+        qd[j] = CMP ? (uint32_t)j : pop();
         dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
     }
     // the in-window segments' sums now, while the first pieces are in flight (the window loads were
@@ -682,12 +724,15 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
 
     // the streamed segments, in address order (lane mask), and the next one's start / end; an event
     // leaves the segment's total in its lane (tot), the epilogue below is one vector pass
-    uint64_t srest = __builtin_amdgcn_ballot_w64(mine && len != 0u && !inwin);
+    uint64_t srest = __builtin_amdgcn_ballot_w64(streamed);
     const bool any = srest != 0u;
     uint32_t cur = any ? (uint32_t)__builtin_ctzll(srest) : 63u;
     srest &= srest - 1u;
-    uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)cur);
-    uint32_t ce = any ? cs + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)cur) : kNoEnd;
+    // the next segment's start / end in the stream's frame (run-relative bytes, or compacted offsets)
+    const uint32_t xs_l = CMP ? cs_l : (uint32_t)rel;
+    const uint32_t xe_l = CMP ? ce_l : (uint32_t)rel + len;
+    uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)xs_l, (int)cur);
+    uint32_t ce = any ? (uint32_t)__builtin_amdgcn_readlane((int)xe_l, (int)cur) : kNoEnd;
     uint32_t acc = 0u;
     auto consume = [&](uint32_t q, u32x4 v) {
         const uint32_t qb = q << 10;
@@ -709,8 +754,8 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
                 u = more ? (uint32_t)__builtin_ctzll(rs) : 63u;
                 rs &= rs - 1u;
                 const uint32_t pe = e;
-                c = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rel, (int)u);
-                e = more ? c + (uint32_t)__builtin_amdgcn_readlane((int)len, (int)u) : kNoEnd;
+                c = (uint32_t)__builtin_amdgcn_readlane((int)xs_l, (int)u);
+                e = more ? (uint32_t)__builtin_amdgcn_readlane((int)xe_l, (int)u) : kNoEnd;
                 Ps = (c == pe) ? Pe : piece_prefix(v, full, lane16, c <= qb ? 0u : min(c - qb, 1024u));
             } while (e <= pend);
             a = full - Ps;
@@ -722,12 +767,12 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         acc = a;
         tot = t;
     };
-    const uint32_t rounds = (nlive + (uint32_t)D - 1u) / (uint32_t)D;
+    const uint32_t rounds = (nunits + (uint32_t)D - 1u) / (uint32_t)D;
     for (uint32_t r = 0; r < rounds; ++r) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             consume(qd[j], opaque_tuple(dv[j]));
-            qd[j] = pop();                                     // none left: the sentinel, no loads
+            qd[j] = CMP ? qd[j] + (uint32_t)D : pop();         // none left: past the list / the sentinel, no loads
             dv[j] = buf_load16<NT>(rd, live_voff(qd[j]));
             asm volatile("" ::: "memory");
         }
@@ -745,12 +790,12 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
     store_run_results(A, s_begin, nres, lane, res0, res1);
 }
 
-template <int D, int PH, bool NT>
+template <int D, int PH, bool NT, bool CMP>
 hipError_t launch_live_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.xcd = stream_xcd(true) ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
-    hipLaunchKernelGGL((seg_live_varlen_kernel<D, PH, NT>), dim3((unsigned)((waves + 3u) / 4u + (a.plan_out ? 1u : 0u))),
+    hipLaunchKernelGGL((seg_live_varlen_kernel<D, PH, NT, CMP>), dim3((unsigned)((waves + 3u) / 4u + (a.plan_out ? 1u : 0u))),
                        dim3(256), stream_lds_bytes(0), s, a, spw);
     return hipGetLastError();
 }
@@ -892,6 +937,7 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
     }
 }
 
+thread_local TuneKnob g_live_compact{-1};   // NETCSUM_TUNE_LIVE_COMPACT
 thread_local TuneKnob g_stream_waves{-1};
 thread_local TuneKnob g_stream_touch{-1};
 thread_local TuneKnob g_stream_xcd{-1};
@@ -902,6 +948,14 @@ hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long
     hipLaunchKernelGGL(read_run_kernel, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
                        static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
     return hipGetLastError();
+}
+
+void set_live_compact(int v) {
+    g_live_compact.store(v);
+}
+
+bool live_compact() {
+    return g_live_compact.load() != 0;
 }
 
 void set_stream_waves(int w) {
@@ -1029,8 +1083,10 @@ hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hi
     // limit, checked here too so that no caller can reach the kernel with a longer one)
     if (a.pseudo != nullptr && a.pseudo_len > 64u) return hipErrorInvalidValue;
     const int ph = stream_ph(a);
+    const bool cmp = live_compact();
 #define NETCSUM_LV(D_, PH_) \
-    if (depth == D_ && ph == PH_) return launch_live_varlen_t<D_, PH_, true>(a, spw, s);
+    if (depth == D_ && ph == PH_) return cmp ? launch_live_varlen_t<D_, PH_, true, true>(a, spw, s) \
+                                             : launch_live_varlen_t<D_, PH_, true, false>(a, spw, s);
     NETCSUM_LV(4, 0) NETCSUM_LV(4, 1) NETCSUM_LV(4, 2) NETCSUM_LV(8, 0) NETCSUM_LV(8, 1) NETCSUM_LV(8, 2)
 #undef NETCSUM_LV
     return hipErrorInvalidValue;
