@@ -708,7 +708,7 @@ typedef enum netcsum_tune_key {
                                          for its plan word, i.e. for the stream's earlier work too) and
                                          run this batch in its plan; 0 = run the first batch unplanned
                                          (its own sampler block leaves the plan for the next batch);
-                                         -1 (default) = 1 from 1 Mi frames (rings) / 256 Ki segments
+                                         -1 (default) = 1 from 4 Mi frames (rings) / 512 Ki segments
                                          (pools), else 0. Never under stream capture.                 */
     NETCSUM_TUNE_LIVE_COMPACT  = 27   /* live-sector streams (segments one per pool buffer): 1 / -1
                                          (default) the run's live 64-B sectors read compacted, 16 per

@@ -36,7 +36,7 @@ VARIANTS = [("default", {}), ("pipe16", {netcsum.TUNE_KERNEL: 2, netcsum.TUNE_GR
             ("runs8", {netcsum.TUNE_VARLEN_RUN_BYTES: 0}),
             ("pieces", {netcsum.TUNE_LIVE_COMPACT: 0})]   # round 6: the live pieces, not the compacted sectors
 if os.environ.get("POOL_LIVE"):                       # live-sector stream: run length x pieces in flight
-    for r, dd in ((8, 4), (8, 8), (16, 4), (16, 8), (24, 4), (32, 4), (32, 8), (40, 4)):
+    for r, dd in ((8, 4), (8, 8), (16, 4), (16, 8), (24, 4), (24, 8), (32, 4), (32, 8), (40, 4), (40, 8)):
         VARIANTS.append((f"live.s{r}.d{dd}", {netcsum.TUNE_TILE: r, netcsum.TUNE_CHUNKS: dd}))
 if os.environ.get("POOL_PIPES"):                      # lane-group pipe geometries (kernel 2)
     for g, k, t in ((16, 6, 2), (16, 6, 8), (16, 6, 16), (32, 4, 4), (8, 8, 4), (16, 8, 4)):

@@ -510,8 +510,8 @@ thread_local uint32_t tls_plan_id = 0;
 // one-block launch the host waits for, from kPlanAheadRing frames / kPlanAheadPool segments), 0 never
 // (the first batch runs unplanned and leaves the plan for the next), 1 always.
 thread_local netcsum::TuneKnob g_tune_plan_ahead{-1};
-constexpr uint32_t kPlanAheadRing = 1u << 20;
-constexpr uint32_t kPlanAheadPool = 1u << 18;
+constexpr uint32_t kPlanAheadRing = 1u << 22;
+constexpr uint32_t kPlanAheadPool = 1u << 19;
 
 // The plan the ring's previous batch left (0: none yet), its word (host and device addresses) and tag
 // for this batch's plan block; *d_word = nullptr when no pool could be had (the batch then runs

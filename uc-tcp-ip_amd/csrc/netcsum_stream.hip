@@ -51,8 +51,14 @@ constexpr uint64_t kMaxGap = 64u;      // varlen runs stream across gaps of up t
 // holds segment k's pseudo-header sum, folded, in its own stream frame, from the 16-B-aligned chunks
 // that cover it (all loads issued before any is used). PH 1: <= 2 chunks per header, 2: <= 5.
 template <int PH>
-__device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t s_begin, uint32_t nres, uint32_t lane,
-                                                uint32_t& ps0, uint32_t& ps1) {
+struct PseudoChunks {
+    static constexpr int kPch = PH == 1 ? 2 : 5;              // chunks one pseudo-header can touch
+    u32x4 v[2][kPch];
+};
+
+template <int PH>
+__device__ __forceinline__ void run_pseudo_issue(const SegBatchArgs& A, uint32_t s_begin, uint32_t nres, uint32_t lane,
+                                                 PseudoChunks<PH>& P) {
     const uint32_t plen = A.pseudo_len;
     const uint32_t pst = A.pseudo_stride;
     const uintptr_t pfirst = (uintptr_t)A.pseudo + (uint64_t)s_begin * pst;
@@ -61,8 +67,8 @@ __device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t 
     const uint32_t pspan = plead + (nres - 1u) * pst + plen;
     const __amdgpu_buffer_rsrc_t rp = run_rsrc(PB, (pspan + 15u) & ~15u);
     const uint32_t nchmax = (plen + 30u) >> 4;                 // chunks one pseudo-header can touch
-    constexpr int kPch = PH == 1 ? 2 : 5;
-    u32x4 pv[2][kPch];
+    constexpr int kPch = PseudoChunks<PH>::kPch;
+    auto& pv = P.v;
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
         const uint32_t k = lane + 64u * (uint32_t)sl;
@@ -70,7 +76,10 @@ __device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t 
         const uint32_t hi = (a & 15u) + plen;
 #pragma unroll
         for (int i = 0; i < kPch; ++i) {
-            if ((uint32_t)i < nchmax) {                        // wave-uniform
+            // PH 1 (<= 17 B: both chunks, a chunk past the header at kOOB): no branch, so that no load is
+            // pending on one path only — the waitcnt pass would drain vmcnt(0) at the join, i.e. wait
+            // for the run's first pieces here (run_pseudo_issue's loads are consumed after the stream)
+            if (PH == 1 || (uint32_t)i < nchmax) {             // wave-uniform
                 const uint32_t off = (k < nres && 16u * (uint32_t)i < hi) ? (a & ~15u) + 16u * (uint32_t)i : kOOB;
                 pv[sl][i] = buf_load16<false>(rp, off);
             } else {
@@ -78,6 +87,16 @@ __device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t 
             }
         }
     }
+}
+
+template <int PH>
+__device__ __forceinline__ void run_pseudo_finish(const SegBatchArgs& A, uint32_t s_begin, uint32_t lane,
+                                                  const PseudoChunks<PH>& P, uint32_t& ps0, uint32_t& ps1) {
+    const uint32_t plen = A.pseudo_len;
+    const uint32_t pst = A.pseudo_stride;
+    const uint32_t plead = (uint32_t)(((uintptr_t)A.pseudo + (uint64_t)s_begin * pst) & 15u);
+    constexpr int kPch = PseudoChunks<PH>::kPch;
+    const auto& pv = P.v;
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
         const uint32_t k = lane + 64u * (uint32_t)sl;
@@ -100,6 +119,14 @@ __device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t 
             ps1 = s;
         }
     }
+}
+
+template <int PH>
+__device__ __forceinline__ void run_pseudo_sums(const SegBatchArgs& A, uint32_t s_begin, uint32_t nres, uint32_t lane,
+                                                uint32_t& ps0, uint32_t& ps1) {
+    PseudoChunks<PH> P;
+    run_pseudo_issue<PH>(A, s_begin, nres, lane, P);
+    run_pseudo_finish<PH>(A, s_begin, lane, P, ps0, ps1);
 }
 
 // Scalar epilogue shared by the stream kernels: the folded result of run segment k from the wave
@@ -171,16 +198,31 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     }
     const RunTouch touch = touch_run(rd, npieces, lane, A.touch != 0u);    // row touch (netcsum_stream.h)
 
-    // ... while the run's pseudo-header sums are computed.
+    // ... and the run's pseudo-headers behind them. 12-B headers (PH 1, C2 / C5): only LOADED here and
+    // added in a vector epilogue after the stream, so no wave waits for them before its first piece
+    // (loads return in order: they have arrived by the time the first refill is consumed) and a segment
+    // end costs no pseudo-header readlanes; longer ones (PH 2, 40-B IPv6) are summed here.
+    constexpr bool kDeferPseudo = PH == 1;
     uint32_t ps0 = 0u, ps1 = 0u;
-    if constexpr (PH != 0) {
+    PseudoChunks<kDeferPseudo ? 1 : 2> pvd;
+    if constexpr (kDeferPseudo) {
+        run_pseudo_issue<1>(A, s_begin, nres, lane, pvd);
+    } else if constexpr (PH != 0) {
         run_pseudo_sums<PH>(A, s_begin, nres, lane, ps0, ps1);
         touch_retire(touch);                                   // issued before the pseudo loads: retired
     }
 
     uint32_t res0 = 0u, res1 = 0u;                             // result of run segment k: lane k % 64
     auto finish = [&](uint32_t cur, uint32_t T, bool odd) {
-        finish_segment<PH>(cur - s_begin, T, odd, A.verify != 0u, lane, ps0, ps1, res0, res1);
+        if constexpr (kDeferPseudo) {                          // the folded, rotated sum; the epilogue the rest
+            uint32_t t = fold16(T);
+            t = odd ? rot8(t) : t;
+            const uint32_t k = cur - s_begin;
+            res0 = (lane == k) ? t : res0;
+            res1 = (lane + 64u == k) ? t : res1;
+        } else {
+            finish_segment<PH>(cur - s_begin, T, odd, A.verify != 0u, lane, ps0, ps1, res0, res1);
+        }
     };
 
     uint32_t cur = s_begin;                                    // next segment to finish
@@ -249,8 +291,14 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // trailing dummy pieces
-    if constexpr (PH == 0) {
+    if constexpr (PH == 0 || kDeferPseudo) {
         touch_retire(touch);
+    }
+    if constexpr (kDeferPseudo) {                              // + the pseudo-header, complement / compare
+        run_pseudo_finish<1>(A, s_begin, lane, pvd, ps0, ps1);
+        const uint32_t t0 = fold16(res0 + ps0), t1 = fold16(res1 + ps1);
+        res0 = A.verify ? (t0 == 0xFFFFu ? 1u : 0u) : (~t0 & 0xFFFFu);
+        res1 = A.verify ? (t1 == 0xFFFFu ? 1u : 0u) : (~t1 & 0xFFFFu);
     }
 
     store_run_results(A, s_begin, nres, lane, res0, res1);
