@@ -390,13 +390,6 @@ def c5_point(torch, netcsum, args, dev, stream):
         b.record(stream)
     torch.cuda.synchronize()
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / k
-    # diagnostic: the same launches without the pseudo-header stream (a second address stream)
-    for a, b in evs:
-        a.record(stream)
-        netcsum.batch_strided(seg, L, L, None, 0, 0, n, out, netcsum.OP_DATA_CALC, stream=stream)
-        b.record(stream)
-    torch.cuda.synchronize()
-    nop_ms = sum(a.elapsed_time(b) for a, b in evs) / k
     parity = None
     try:
         import oracle
@@ -409,6 +402,13 @@ def c5_point(torch, netcsum, args, dev, stream):
     except Exception as e:                        # noqa: BLE001
         parity = f"unchecked: {e}"
     desc = "netcsum::" + netcsum.last_launch()
+    # diagnostic (after the parity check, which reads `out`): the same launches without the pseudo-header stream (a second address stream)
+    for a, b in evs:
+        a.record(stream)
+        netcsum.batch_strided(seg, L, L, None, 0, 0, n, out, netcsum.OP_DATA_CALC, stream=stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    nop_ms = sum(a.elapsed_time(b) for a, b in evs) / k
     # the read ceilings over the same 25 GB (a box whose C5 rate falls while these
     # hold loses it in the kernel, one whose probes fall with it loses it in the access pattern)
     n16 = (n * L) // 16 * 16

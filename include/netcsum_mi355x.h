@@ -710,10 +710,14 @@ typedef enum netcsum_tune_key {
                                          (its own sampler block leaves the plan for the next batch);
                                          -1 (default) = 1 from 4 Mi frames (rings) / 512 Ki segments
                                          (pools), else 0. Never under stream capture.                 */
-    NETCSUM_TUNE_LIVE_COMPACT  = 27   /* live-sector streams (segments one per pool buffer): 1 / -1
+    NETCSUM_TUNE_LIVE_COMPACT  = 27,  /* live-sector streams (segments one per pool buffer): 1 / -1
                                          (default) the run's live 64-B sectors read compacted, 16 per
                                          wave-instruction; 0 the live 1-KiB pieces of the run's span,
                                          each lane loading its 16 B where its sector is live          */
+    NETCSUM_TUNE_STORE_GATHER  = 28   /* dense strided segment batches (C2 / C5): 1 / -1 (default) the
+                                         results of a workgroup's 4 runs gathered in LDS and written as
+                                         whole lines by its last wave; 0 each wave writes its own run's
+                                         results (partial lines)                                      */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

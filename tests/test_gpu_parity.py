@@ -30,6 +30,7 @@ def _reset_tuning():
     netcsum.tune(netcsum.TUNE_STREAM_WAVES, -1)
     netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)
     netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
+    netcsum.tune(netcsum.TUNE_STORE_GATHER, -1)
 
 
 @pytest.fixture(autouse=True)
@@ -590,3 +591,27 @@ def test_varlen_adaptive_runs_vs_oracle(run_bytes):
                 assert np.array_equal(_np_out(out), want), (n, op, kern)
     finally:
         netcsum.tune(netcsum.TUNE_VARLEN_RUN_BYTES, -1)
+
+
+@pytest.mark.parametrize("gather", [0, 1])
+@pytest.mark.parametrize("op", [0, 1])
+@pytest.mark.parametrize("plen", [0, 12, 40])
+def test_stream_result_gather_both_ways(gather, op, plen):
+    """NETCSUM_TUNE_STORE_GATHER: the dense stream kernel's results per workgroup (4 runs) gathered in
+    LDS and written whole by the workgroup's last wave, or per wave — Calc and Verify, pseudo-headers
+    of 0 / 12 / 40 B (the 12-B ones added after the stream), batches that end inside a workgroup (one,
+    two or three of its waves with a run, a short last run), runs of 1..128, odd bases."""
+    netcsum.tune(netcsum.TUNE_STORE_GATHER, gather)
+    rng = np.random.default_rng(31 * plen + 7 * op + gather)
+    L = 1024
+    for n, run in ((1, -1), (17, -1), (63, -1), (64, -1), (65, -1), (4099, -1), (4096 + 33, -1), (1000, 1),
+                   (1000, 5), (3000, 128), (513, 128)):
+        netcsum.tune(netcsum.TUNE_TILE, run)
+        data = _host_bytes(rng, n * L + 64, "random")
+        ph = _host_bytes(rng, n * max(plen, 1) + 64, "random")
+        data_d, ph_d = torch.from_numpy(data).to(DEV), torch.from_numpy(ph).to(DEV)
+        for base_off in (0, 3):
+            got = _gpu_strided(data_d, base_off, L, L, ph_d, plen, plen, n, op)
+            assert netcsum.last_launch().startswith("seg_stream_kernel"), netcsum.last_launch()
+            want = oracle.batch_strided(data, L, L, ph if plen else None, plen, plen, n, op, seg_offset=base_off)
+            assert np.array_equal(got, want), (n, run, base_off)

@@ -8,6 +8,7 @@ and on a C2 batch allocated beside it (GPU box only; JSON lines):
   run_probe         read_run_kernel: the kernel's access pattern, nothing computed (TUNE_PROBE 2)
   lds_probe         the LDS-DMA grid-stride read probe (TUNE_PROBE 1)
   touch0 / xcd0     the kernel without the row touch / in the plain block order
+  gather0           the kernel with each wave storing its own results (round 5's partial-line stores)
 Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
 import json
 import os
@@ -42,10 +43,11 @@ def main():
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
-    def tune(probe=1, touch=-1, xcd=-1):
+    def tune(probe=1, touch=-1, xcd=-1, gather=-1):
         netcsum.tune(netcsum.TUNE_PROBE, probe)
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
         netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
+        netcsum.tune(netcsum.TUNE_STORE_GATHER, gather)
 
     variants = []
     for name, (n, seg, ph, out) in bufs.items():
@@ -71,7 +73,8 @@ def main():
             return lambda: netcsum.read_stream(seg, n16, sink, stream=st)
         variants += [(f"{name}_kernel", {}, k(), algo), (f"{name}_nopseudo", {}, nop(), n * (L + 2)),
                      (f"{name}_run_probe", {"probe": 2}, rd(), n16), (f"{name}_lds_probe", {"probe": 1}, rd(), n16),
-                     (f"{name}_touch0", {"touch": 0}, k(), algo), (f"{name}_xcd0", {"xcd": 0}, k(), algo)]
+                     (f"{name}_touch0", {"touch": 0}, k(), algo), (f"{name}_xcd0", {"xcd": 0}, k(), algo),
+                     (f"{name}_gather0", {"gather": 0}, k(), algo)]
         if n > (1 << 20):
             variants.append((f"{name}_chunk1M", {}, chunked(), algo))
     if only:

@@ -34,6 +34,8 @@ struct SegBatchArgs {
                                    // larger than the launch's), nullptr = the launch's
     uint32_t*       plan_out;      // varlen live kernel: the batch's plan for the next batch on the same
     uint32_t        plan_tag;      // descriptors (an extra sampler block), nullptr = none
+    uint32_t        gather;        // dense stream kernel: a block's results gathered in LDS and stored as
+                                   // one line by its last wave (set by the launcher)
 };
 
 struct LaunchCfg {
@@ -184,6 +186,10 @@ void set_varlen_run_bytes(int v);   // NETCSUM_TUNE_VARLEN_RUN_BYTES
 // wave-instruction (-1 default / 1), or as the live 1-KiB pieces of their span (0)
 void set_live_compact(int v);
 bool live_compact();
+// NETCSUM_TUNE_STORE_GATHER: the dense segment stream kernel's results, per block of 4 runs, gathered in
+// LDS and stored whole by the block's last wave (-1 default / 1), or per wave (0)
+void set_store_gather(int v);
+bool store_gather();
 uint32_t varlen_run_bytes();
 constexpr uint32_t kVarlenSpwMin = 3u;
 void set_hdr_burst(int v);     // NETCSUM_TUNE_HDR_BURST: header stream results written per run (1) or per piece (0)

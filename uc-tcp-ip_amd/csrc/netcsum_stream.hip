@@ -168,11 +168,51 @@ __device__ __forceinline__ void store_run_results(const SegBatchArgs& A, uint32_
 // mask, one DPP reduction and a scalar epilogue. Otherwise the general walk (any number of events
 // per piece, gaps between segments).
 // PH: 0 no pseudo-header, 1 pseudo-headers touching <= 2 aligned chunks (<= 17 B), 2 up to 64 B.
+// Results of a block's 4 consecutive runs (4 x 16 segments in C2 / C5: 128 B of u16 checksums, one
+// aligned line) gathered in LDS and stored by the wave that finishes last, instead of 32 B per wave:
+// on some boxes the C5 shard ran at 84 % of spec against 90 % on others while its read probe did not
+// move (profiles/r6e_*: the kernel's L2 tag stalls 3.7 x those of a fast box, its translations no
+// different), i.e. the partial-line result stores, whose lines leave the L2 before their neighbours'
+// stores arrive once the stream exceeds what the caches hold.
+constexpr uint32_t kGatherMax = 4u * kMaxRun;
+
+__device__ __forceinline__ void gather_store_results(const SegBatchArgs& A, uint32_t blk, uint32_t w, uint32_t spw,
+                                                     uint32_t nres, uint32_t lane, uint32_t r0, uint32_t r1,
+                                                     uint16_t* res, uint32_t* cnt) {
+    const uint32_t k0 = w * spw;                               // this wave's results within the block
+    if (lane < nres) res[k0 + lane] = (uint16_t)r0;
+    if (lane + 64u < nres) res[k0 + lane + 64u] = (uint16_t)r1;
+    const uint64_t b0 = (uint64_t)blk * 4u * spw;              // the block's first segment
+    const uint64_t left = (uint64_t)A.n_seg - b0;
+    const uint32_t nw = (uint32_t)min<uint64_t>(4u, (left + spw - 1u) / spw);   // waves of the block with a run
+    uint32_t old = 0u;
+    if (lane == 0u) {
+        old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+    if (old + 1u == nw) {                                      // the last: the block's results, whole lines
+        const uint32_t tot = (uint32_t)min<uint64_t>(4u * spw, left);
+        if (A.verify) {
+            uint8_t* o = static_cast<uint8_t*>(A.out) + b0;
+            for (uint32_t i = lane; i < tot; i += 64u) o[i] = (uint8_t)res[i];
+        } else {
+            uint16_t* o = static_cast<uint16_t*>(A.out) + b0;
+            for (uint32_t i = lane; i < tot; i += 64u) o[i] = res[i];
+        }
+    }
+}
+
 template <int D, int PH, bool NT, bool ONE>
 __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_t spw) {
+    __shared__ uint16_t g_res[kGatherMax];
+    __shared__ uint32_t g_cnt;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    if (A.gather) {                                            // (every wave, before any returns)
+        if (threadIdx.x == 0u) g_cnt = 0u;
+        __syncthreads();
+    }
     const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
@@ -301,7 +341,11 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
         res1 = A.verify ? (t1 == 0xFFFFu ? 1u : 0u) : (~t1 & 0xFFFFu);
     }
 
-    store_run_results(A, s_begin, nres, lane, res0, res1);
+    if (A.gather) {
+        gather_store_results(A, blk, w, spw, nres, lane, res0, res1, g_res, &g_cnt);
+    } else {
+        store_run_results(A, s_begin, nres, lane, res0, res1);
+    }
 }
 
 // Variable-length batches (offset/length descriptors, config C4). A wave takes a run of segments;
@@ -919,12 +963,16 @@ hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) 
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
     a.xcd = stream_xcd(true) ? 1u : 0u;
+    a.gather = store_gather() ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     // dense batches default to 5 waves per SIMD with the row touch: C2 0.2188 ms against 0.2346 ms
-    // without either (r2ct; 0.2268 touch only, 0.2300 cap only)
-    hipLaunchKernelGGL((seg_stream_kernel<D, PH, NT, ONE>), dim3(grid), dim3(256), stream_lds_bytes(ONE ? 5 : 0), s, a,
-                       spw);
+    // without either (r2ct; 0.2268 touch only, 0.2300 cap only); the residency cap's LDS reservation
+    // less the kernel's static LDS (the results' gather), so that the same number of blocks fit
+    const uint32_t lds = stream_lds_bytes(ONE ? 5 : 0);
+    const uint32_t kStatic = kGatherMax * 2u + 16u;
+    hipLaunchKernelGGL((seg_stream_kernel<D, PH, NT, ONE>), dim3(grid), dim3(256), lds > kStatic ? lds - kStatic : lds,
+                       s, a, spw);
     return hipGetLastError();
 }
 
@@ -986,6 +1034,7 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
 }
 
 thread_local TuneKnob g_live_compact{-1};   // NETCSUM_TUNE_LIVE_COMPACT
+thread_local TuneKnob g_store_gather{-1};   // NETCSUM_TUNE_STORE_GATHER
 thread_local TuneKnob g_stream_waves{-1};
 thread_local TuneKnob g_stream_touch{-1};
 thread_local TuneKnob g_stream_xcd{-1};
@@ -996,6 +1045,14 @@ hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long
     hipLaunchKernelGGL(read_run_kernel, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
                        static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
     return hipGetLastError();
+}
+
+void set_store_gather(int v) {
+    g_store_gather.store(v);
+}
+
+bool store_gather() {
+    return g_store_gather.load() != 0;
 }
 
 void set_live_compact(int v) {

@@ -75,6 +75,7 @@ TUNE_BURST_SERVER_LIFE_US = 24
 TUNE_FAULT_INJECT = 25          # test only: the next offset/length packet batch skips its deferred pass and fails
 TUNE_PLAN_AHEAD = 26            # first batch on a layout: sample it first and run in its plan (-1 auto, 0, 1)
 TUNE_LIVE_COMPACT = 27          # live-sector streams: live sectors compacted (-1 default / 1) or live pieces (0)
+TUNE_STORE_GATHER = 28          # dense segment stream: a block's results stored as whole lines (-1 / 1) or per wave (0)
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
