@@ -193,3 +193,17 @@ def test_chain_batch_matches_single_segment_batch():
                          _dev(cb.pseudo, np.uint8), cb.pseudo_stride, 12, cb.n, out)
     torch.cuda.synchronize()
     assert np.array_equal(got, out.cpu().numpy().view(np.uint16))
+
+
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_chain_pass1_tile_order(xcd):
+    """Pass 1's XCD-aware tile order (NETCSUM_TUNE_STREAM_XCD; one tile of 64 pieces per block, the
+    tiles of one XCD contiguous) is a launch option: the same records, the oracle's results, for piece
+    counts that fill the tiles unevenly over the 8 XCDs."""
+    try:
+        netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
+        for n_chains, seed in ((1, 1), (37, 2), (700, 3)):
+            cb = make_chain_batch(random.Random(seed), n_chains, 12)
+            assert np.array_equal(_gpu(cb, 0), _want(cb, 0))
+    finally:
+        netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)

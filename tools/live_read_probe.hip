@@ -277,10 +277,18 @@ int main(int argc, char** argv) {
         } vs[] = {{"whole", 0, 4, 0}, {"live", 1, 4, 0}, {"live.touch", 1, 4, 1}, {"live.d8", 1, 8, 0},
                   {"live.d8.touch", 1, 8, 1}, {"whole.touch", 0, 4, 1}, {"compact", 2, 4, 0}, {"compact.touch", 2, 4, 1},
                   {"compact.d8.touch", 2, 8, 1}, {"live.win", 1, 4, 2}, {"compact.win", 2, 4, 2}};
-        for (int pass = 0; pass < 2; ++pass) {
+        // (LRP_FORM / LRP_RUN: one form / run length only; LRP_WARM, LRP_PASSES: fewer launches — for
+        // a rocprofv3 --pmc pass over one variant)
+        const char* only_form = std::getenv("LRP_FORM");
+        const uint32_t only_run = std::getenv("LRP_RUN") ? (uint32_t)std::atoi(std::getenv("LRP_RUN")) : 0u;
+        const int warm = std::getenv("LRP_WARM") ? std::atoi(std::getenv("LRP_WARM")) : 200;
+        const int passes = std::getenv("LRP_PASSES") ? std::atoi(std::getenv("LRP_PASSES")) : 2;
+        for (int pass = 0; pass < passes; ++pass) {
             for (const V& v : vs) {
                 if ((v.touch == 2) != (L.mix == 2)) continue;            // the 96-B window: the ring only
+                if (only_form && std::string(only_form) != v.tag) continue;
                 for (uint32_t R : {8u, 16u, 30u, 32u, 41u}) {
+                    if (only_run && R != only_run) continue;
                     if ((uint64_t)R * L.stride + 2048u > (63u << 10)) continue;   // a run within the bitmap's reach
                     if ((R == 30u || R == 41u) && (uint64_t)(R + 1u) * L.stride + 2048u <= (63u << 10)) continue;   // (the longest run only)
                     const uint64_t waves = (n + R - 1u) / R;
@@ -296,7 +304,7 @@ int main(int argc, char** argv) {
 #undef LRP_T
 #undef LRP_L
                     };
-                    for (int i = 0; i < 200; ++i) launch();
+                    for (int i = 0; i < warm; ++i) launch();
                     std::vector<float> t(20);
                     for (float& x : t) {
                         CK(hipEventRecord(e0, 0));

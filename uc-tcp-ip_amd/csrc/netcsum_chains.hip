@@ -393,10 +393,14 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
     if (blockIdx.x >= ntiles) {
         return;
     }
-    // this block's tiles: blockIdx.x, + gridDim.x, ...; group g takes pieces tile*64 + g + 16 k
-    const uint32_t iters = ((ntiles - blockIdx.x + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
+    // this block's tiles: bid, + gridDim.x, ...; group g takes pieces tile*64 + g + 16 k. With one tile
+    // per block (the default grid), the XCD-aware order: the blocks the dispatcher places on one XCD
+    // take one contiguous 1/8 of the tiles (sv::xcd_block over the first ntiles blocks, which are the
+    // ones with a tile), as the segment stream kernels' runs do
+    const uint32_t bid = (A.xcd && ntiles <= gridDim.x) ? sv::xcd_block(blockIdx.x, ntiles) : blockIdx.x;
+    const uint32_t iters = ((ntiles - bid + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
     auto piece_at = [&](uint32_t i) -> uint32_t {                 // the group's i-th piece
-        return (blockIdx.x + (i / kPTile) * gridDim.x) * tile + g + gpb * (i % kPTile);
+        return (bid + (i / kPTile) * gridDim.x) * tile + g + gpb * (i % kPTile);
     };
     const uintptr_t base = (uintptr_t)A.base;
     auto desc = [&](uint32_t j, uint64_t& off, uint32_t& len) {
@@ -727,7 +731,9 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     // (at most 2^20 blocks = 2^28 threads, within the launch limit; the tiles go round-robin beyond)
     const uint64_t g1 = std::min<uint64_t>(std::min<uint64_t>(((uint64_t)cap + 63u) / 64u, 1ull << 20),
                                            std::max<uint64_t>(resident, 2ull * a.n));
-    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, a, eo, cap);
+    ChainBatchArgs ax = a;
+    ax.xcd = stream_xcd(true) ? 1u : 0u;
+    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax, eo, cap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;

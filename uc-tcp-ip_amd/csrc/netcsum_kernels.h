@@ -125,6 +125,7 @@ struct ChainBatchArgs {
     uint32_t        n;
     uint32_t        verify;
     void*           out;
+    uint32_t        xcd;           // pass 1: XCD-aware tile order (set by the launcher)
 };
 
 hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipStream_t s);
