@@ -615,7 +615,8 @@ typedef enum netcsum_tune_key {
                                          run-stream kernels: 1-KiB pieces in flight (4 / 8)        */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),
                                          2 run-stream form of the checksum kernels (24-KiB runs per
-                                         wave, 4 nt pieces in flight, row touch, 5 waves per SIMD)  */
+                                         wave, 4 nt pieces in flight, row touch, 5 waves per SIMD),
+                                         3 the same with a ~128-clock pause after each piece        */
     NETCSUM_TUNE_GRID_MULT     = 8,   /* auto grid = resident blocks x CUs x this (0 = 1)          */
     NETCSUM_TUNE_TILE          = 9,   /* J > 0: each block owns a contiguous tile of J segments per
                                          group (grid = tiles); 0: grid-stride; -1: auto (J = 4).

@@ -9,6 +9,10 @@ and on a C2 batch allocated beside it (GPU box only; JSON lines):
   lds_probe         the LDS-DMA grid-stride read probe (TUNE_PROBE 1)
   touch0 / xcd0     the kernel without the row touch / in the plain block order
   gather0           the kernel with each wave storing its own results (round 5's partial-line stores)
+  d6 / d8           6 / 8 pieces in flight per wave (NETCSUM_TUNE_CHUNKS)
+  w4 / w6 / w8      4 / 6 / 8 resident waves per SIMD (NETCSUM_TUNE_STREAM_WAVES; default 5)
+  s8 / s24 / s32    runs of 8 / 24 / 32 segments (NETCSUM_TUNE_TILE; default 16)
+  run_probe_sleep   read_run_kernel with a ~128-clock pause after each piece (TUNE_PROBE 3)
 Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
 import json
 import os
@@ -43,7 +47,10 @@ def main():
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
-    def tune(probe=1, touch=-1, xcd=-1, gather=-1):
+    def tune(probe=1, touch=-1, xcd=-1, gather=-1, d=0, waves=-1, tile=-1):
+        netcsum.tune(netcsum.TUNE_TILE, tile)
+        netcsum.tune(netcsum.TUNE_CHUNKS, d)
+        netcsum.tune(netcsum.TUNE_STREAM_WAVES, waves)
         netcsum.tune(netcsum.TUNE_PROBE, probe)
         netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
         netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
@@ -74,7 +81,12 @@ def main():
         variants += [(f"{name}_kernel", {}, k(), algo), (f"{name}_nopseudo", {}, nop(), n * (L + 2)),
                      (f"{name}_run_probe", {"probe": 2}, rd(), n16), (f"{name}_lds_probe", {"probe": 1}, rd(), n16),
                      (f"{name}_touch0", {"touch": 0}, k(), algo), (f"{name}_xcd0", {"xcd": 0}, k(), algo),
-                     (f"{name}_gather0", {"gather": 0}, k(), algo)]
+                     (f"{name}_gather0", {"gather": 0}, k(), algo), (f"{name}_d6", {"d": 6}, k(), algo),
+                     (f"{name}_d8", {"d": 8}, k(), algo), (f"{name}_w4", {"waves": 4}, k(), algo),
+                     (f"{name}_w6", {"waves": 6}, k(), algo), (f"{name}_w8", {"waves": 8}, k(), algo),
+                     (f"{name}_s8", {"tile": 8}, k(), algo),
+                     (f"{name}_s24", {"tile": 24}, k(), algo), (f"{name}_s32", {"tile": 32}, k(), algo),
+                     (f"{name}_run_probe_sleep", {"probe": 3}, rd(), n16)]
         if n > (1 << 20):
             variants.append((f"{name}_chunk1M", {}, chunked(), algo))
     if only:

@@ -2218,9 +2218,9 @@ NET_ERR NetUtil_MI355X_ReadStream(const void* d_buf, uint64_t n_bytes, uint64_t*
     if (((uintptr_t)d_buf & 15u) != 0u || (n_bytes & 15u) != 0u) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
     int dev = 0;
     NC_HIP(hipGetDevice(&dev));
-    if (g_tune_probe.load() == 2) {                     // run-stream form (netcsum_stream.hip)
+    if (g_tune_probe.load() >= 2) {                     // run-stream form (netcsum_stream.hip); 3: with a pause per piece
         NC_HIP(netcsum::launch_read_run(d_buf, n_bytes, reinterpret_cast<unsigned long long*>(d_sink),
-                                        static_cast<hipStream_t>(hip_stream)));
+                                        static_cast<hipStream_t>(hip_stream), g_tune_probe.load() == 3));
         return NET_UTIL_ERR_NONE;
     }
     int grid = g_tune_grid.load();
@@ -2269,7 +2269,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         g_tune_tile.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_PROBE:
-        if (value < 0 || value > 2) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < 0 || value > 3) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         g_tune_probe.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_TX_PASSES:

@@ -296,6 +296,6 @@ hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint6
                        hipStream_t s);
 hipError_t launch_read_stream(const void* d_p, uint64_t n16, unsigned long long* d_sink, int grid, bool nt,
                               hipStream_t s, int variant);
-hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s);
+hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s, bool sleep);
 
 }  // namespace netcsum

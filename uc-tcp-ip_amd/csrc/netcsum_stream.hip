@@ -995,6 +995,9 @@ namespace {
 // bytes up: the read rate the checksum kernel's access pattern can reach, with none of its arithmetic.
 constexpr uint32_t kProbeRun = 16u * 1500u;
 
+// SLEEP (NETCSUM_TUNE_PROBE 3): s_sleep 2 (~128 clocks) after each piece's sum — the same reads
+// spread over a longer time per run, as the checksum kernel's per-piece work spreads them.
+template <int SLEEP>
 __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint64_t n_bytes, unsigned long long* sink) {
     constexpr int D = 4;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1022,6 +1025,9 @@ __global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint
         for (int j = 0; j < D; ++j) {
             const uint32_t q = r * (uint32_t)D + (uint32_t)j;
             acc = sum4(opaque_tuple(dv[j]), acc);
+            if constexpr (SLEEP != 0) {
+                __builtin_amdgcn_s_sleep(SLEEP);
+            }
             dv[j] = buf_load16<true>(rd, ((q + (uint32_t)D) << 10) + lane16);
             asm volatile("" ::: "memory");
         }
@@ -1040,10 +1046,15 @@ thread_local TuneKnob g_stream_touch{-1};
 thread_local TuneKnob g_stream_xcd{-1};
 }
 
-hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s) {
+hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s, bool sleep) {
     const uint64_t waves = (n_bytes + kProbeRun - 1u) / kProbeRun;
-    hipLaunchKernelGGL(read_run_kernel, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
-                       static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
+    if (sleep) {
+        hipLaunchKernelGGL(read_run_kernel<2>, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
+                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
+    } else {
+        hipLaunchKernelGGL(read_run_kernel<0>, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
+                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
+    }
     return hipGetLastError();
 }
 
