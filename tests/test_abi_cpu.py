@@ -132,7 +132,8 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CRC_WIDE, 3) == 219              # 0, 1 or 2
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CRC_NT, -1) == 219               # 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_FLUSH, 5) == 219              # -1..4
-    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STREAM_XCD, 2) == 219          # -1, 0 or 1
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STREAM_XCD, 4097) == 219       # -1 .. 4096
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STREAM_XCD, -2) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STREAM_TOUCH, 2) == 219          # -1, 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STREAM_WAVES, 2) == 219          # 3..8 or 0
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_TX_PASSES, 3) == 219

@@ -456,9 +456,10 @@ def test_stream_kernel_full_c2_equals_pipe_kernel():
 
 @pytest.mark.parametrize("touch", [0, 1])
 @pytest.mark.parametrize("waves", [0, 3, 5, 8])
-@pytest.mark.parametrize("xcd", [0, 1])
+@pytest.mark.parametrize("xcd", [0, 1, 3, 16])
 def test_stream_touch_and_residency_do_not_change_results(touch, waves, xcd):
-    """The row-touch prologue, the residency cap and the XCD-aware block order
+    """The row-touch prologue, the residency cap and the XCD-aware block order — slices (1) or
+    chunks of 3 / 16 blocks per XCD in turn, grids with and without a partial last round —
     (NETCSUM_TUNE_STREAM_TOUCH / _WAVES / _XCD) are launch options only: dense, gapped and varlen stream batches — runs short and long enough that the touch
     covers only their first 128 pieces — give the oracle's results under every combination."""
     rng = np.random.default_rng(100 * waves + touch + 7 * xcd)

@@ -13,6 +13,11 @@ and on a C2 batch allocated beside it (GPU box only; JSON lines):
   w4 / w6 / w8      4 / 6 / 8 resident waves per SIMD (NETCSUM_TUNE_STREAM_WAVES; default 5)
   s8 / s24 / s32    runs of 8 / 24 / 32 segments (NETCSUM_TUNE_TILE; default 16)
   run_probe_sleep   read_run_kernel with a ~128-clock pause after each piece (TUNE_PROBE 3)
+  alloc2 / alloc2_run_probe   the kernel / its read probe on a SECOND 25-GB allocation of the same shard
+  onealloc          the kernel with the pseudo-headers and the results inside the segments' allocation
+  seg1_out2 / seg2_out1 / seg1_ph2_out2   the first allocations' buffers crossed with the second's
+  x4 / x16 / x64 / x256   the kernel with XCD chunks of C blocks in turn (NETCSUM_TUNE_STREAM_XCD C)
+  alloc2_xcd0 / alloc2_x16  the second allocation in the plain / chunked block order
 Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
 import json
 import os
@@ -45,6 +50,38 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device=dev)
         bufs[name] = (n, seg, ph, out)
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
+    extra = []
+    if not only or any(x.startswith("alloc2") or x == "onealloc" or x.startswith("seg") for x in only.split(",")):
+        n = sizes["c5"]
+        seg2 = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
+        netcsum.fill(seg2, n * L, SEED, 0)
+        ph2 = bufs["c5"][2].clone()
+        out2 = torch.empty(n, dtype=torch.int16, device=dev)
+        big = torch.empty(n * L + 256 + n * P + 256 + 2 * n, dtype=torch.uint8, device=dev)   # one allocation
+        segb = big[: n * L + 256]
+        netcsum.fill(segb, n * L, SEED, 0)
+        phb = big[n * L + 256: n * L + 256 + n * P]
+        phb.copy_(bufs["c5"][2])
+        o0 = n * L + 256 + n * P + 256
+        outb = big[o0: o0 + 2 * n].view(torch.int16)
+        n5 = n                                   # (bound now: the loop below rebinds n)
+        extra = [("c5_alloc2", {}, lambda: netcsum.batch_strided(seg2, L, L, ph2, P, P, n5, out2, netcsum.OP_DATA_CALC, stream=st),
+                  n5 * (L + P + 2)),
+                 ("c5_alloc2_run_probe", {"probe": 2}, lambda: netcsum.read_stream(seg2, n5 * L // 16 * 16, sink, stream=st),
+                  n5 * L // 16 * 16),
+                 ("c5_onealloc", {}, lambda: netcsum.batch_strided(segb, L, L, phb, P, P, n5, outb, netcsum.OP_DATA_CALC, stream=st),
+                  n5 * (L + P + 2)),
+                 # which buffer of the first allocations carries the loss: crossed pairs
+                 ("c5_seg1_out2", {}, lambda: netcsum.batch_strided(bufs["c5"][1], L, L, bufs["c5"][2], P, P, n5, out2,
+                                                                    netcsum.OP_DATA_CALC, stream=st), n5 * (L + P + 2)),
+                 ("c5_seg2_out1", {}, lambda: netcsum.batch_strided(seg2, L, L, ph2, P, P, n5, bufs["c5"][3],
+                                                                    netcsum.OP_DATA_CALC, stream=st), n5 * (L + P + 2)),
+                 ("c5_alloc2_xcd0", {"xcd": 0}, lambda: netcsum.batch_strided(seg2, L, L, ph2, P, P, n5, out2,
+                                                                    netcsum.OP_DATA_CALC, stream=st), n5 * (L + P + 2)),
+                 ("c5_alloc2_x16", {"xcd": 16}, lambda: netcsum.batch_strided(seg2, L, L, ph2, P, P, n5, out2,
+                                                                  netcsum.OP_DATA_CALC, stream=st), n5 * (L + P + 2)),
+                 ("c5_seg1_ph2_out2", {}, lambda: netcsum.batch_strided(bufs["c5"][1], L, L, ph2, P, P, n5, out2,
+                                                                        netcsum.OP_DATA_CALC, stream=st), n5 * (L + P + 2))]
     torch.cuda.synchronize()
 
     def tune(probe=1, touch=-1, xcd=-1, gather=-1, d=0, waves=-1, tile=-1):
@@ -86,9 +123,12 @@ def main():
                      (f"{name}_w6", {"waves": 6}, k(), algo), (f"{name}_w8", {"waves": 8}, k(), algo),
                      (f"{name}_s8", {"tile": 8}, k(), algo),
                      (f"{name}_s24", {"tile": 24}, k(), algo), (f"{name}_s32", {"tile": 32}, k(), algo),
-                     (f"{name}_run_probe_sleep", {"probe": 3}, rd(), n16)]
+                     (f"{name}_run_probe_sleep", {"probe": 3}, rd(), n16),
+                     (f"{name}_x4", {"xcd": 4}, k(), algo), (f"{name}_x16", {"xcd": 16}, k(), algo),
+                     (f"{name}_x64", {"xcd": 64}, k(), algo), (f"{name}_x256", {"xcd": 256}, k(), algo)]
         if n > (1 << 20):
             variants.append((f"{name}_chunk1M", {}, chunked(), algo))
+    variants += extra
     if only:
         keep = only.split(",")
         variants = [v for v in variants if any(v[0].endswith(x) for x in keep)]

@@ -18,7 +18,7 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
        tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
   suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
   .kN = NETCSUM_TUNE_KERNEL N (chains.k3: pass 1 in the live-sector stream), .dN = NETCSUM_TUNE_CHUNKS N,
-  .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N
+  .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -55,6 +55,8 @@ def main():
             netcsum.tune(netcsum.TUNE_PKT_BOUND, int(part[1:]))
         elif part[:1] == "s":
             netcsum.tune(netcsum.TUNE_TILE, int(part[1:]))
+        elif part[:1] == "w":
+            netcsum.tune(netcsum.TUNE_STREAM_WAVES, int(part[1:]))
         elif part[:1] == "x":
             netcsum.tune(netcsum.TUNE_STREAM_XCD, int(part[1:]))
         elif part[:1] == "g":

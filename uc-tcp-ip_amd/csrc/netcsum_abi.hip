@@ -2281,7 +2281,7 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         netcsum::set_stream_waves(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_STREAM_XCD:
-        if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        if (value < -1 || value > 4096) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_stream_xcd(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_TX_FLUSH:

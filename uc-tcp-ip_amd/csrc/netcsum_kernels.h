@@ -290,6 +290,9 @@ bool stream_touch(bool auto_on);
 // 3.614 -> 3.561 ms, C2 0.2186 -> 0.2181, C4 0.6777 -> 0.6747 (on); C3 0.0579-0.0584 -> 0.0589 (off).
 void set_stream_xcd(int on);
 bool stream_xcd(bool auto_on);
+// the block-order mode for xcd_block (netcsum_stream.h): 0 dispatch order, 1 one slice per XCD, C >= 2
+// chunks of C blocks per XCD in turn; auto_mode when the knob is at its default (-1)
+uint32_t stream_xcd_mode(uint32_t auto_mode);
 hipError_t launch_stream_exact(const void* d_p, uint32_t n16, unsigned long long* d_sum, int grid,
                                hipStream_t s, uint32_t tag = 0u);   // tag != 0 (grid 1): completion word
 hipError_t launch_fill(void* d_buf, uint64_t n_bytes, uint64_t first_byte, uint64_t seed, int pattern, int grid,

@@ -97,12 +97,24 @@ __device__ __forceinline__ void touch_retire(RunTouch t) {
     asm volatile("" ::"v"(t.a), "v"(t.b));
 }
 
-// XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): blocks the dispatcher
-// places on one XCD (equal blockIdx mod 8) take one contiguous 1/8 of the grid's runs, so each XCD's
-// L2 and address translation see one slice of the batch instead of all of it.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t nwg) {
-    const uint32_t q = nwg >> 3, r = nwg & 7u, xcd = orig & 7u;
-    return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (orig >> 3);
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form). mode 1: blocks the
+// dispatcher places on one XCD (equal blockIdx mod 8) take one contiguous 1/8 of the grid's runs, so
+// each XCD's L2 and address translation see one slice of the batch instead of all of it. mode C >= 2
+// (round 6): each XCD takes chunks of C consecutive blocks in turn — chunk x, x + 8, x + 16, … — so
+// that each XCD still reads contiguous runs while the 8 XCDs stay in one moving window of the batch
+// instead of 8 streams a slice apart (blocks past the last whole round of 8 chunks keep their order).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t nwg, uint32_t mode = 1u) {
+    const uint32_t xcd = orig & 7u;
+    if (mode <= 1u) {
+        const uint32_t q = nwg >> 3, r = nwg & 7u;
+        return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + (orig >> 3);
+    }
+    const uint32_t full = nwg - nwg % (8u * mode);
+    if (orig >= full) {
+        return orig;
+    }
+    const uint32_t slot = orig >> 3;
+    return ((slot / mode) * 8u + xcd) * mode + slot % mode;
 }
 
 }  // namespace sv

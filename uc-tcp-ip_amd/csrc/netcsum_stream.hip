@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256) seg_stream_kernel(SegBatchArgs A, uint32_
     __shared__ uint32_t g_cnt;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, gridDim.x, A.xcd) : blockIdx.x;
     if (A.gather) {                                            // (every wave, before any returns)
         if (threadIdx.x == 0u) g_cnt = 0u;
         __syncthreads();
@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(256) seg_stream_varlen_kernel(SegBatchArgs A, 
             return;
         }
     }
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg) : blockIdx.x;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg, A.xcd) : blockIdx.x;
     const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
             return;
         }
     }
-    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg) : blockIdx.x;
+    const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg, A.xcd) : blockIdx.x;
     const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
     if (sb64 >= A.n_seg) {
         return;
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
 template <int D, int PH, bool NT, bool CMP>
 hipError_t launch_live_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
-    a.xcd = stream_xcd(true) ? 1u : 0u;
+    a.xcd = stream_xcd_mode(1);
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     hipLaunchKernelGGL((seg_live_varlen_kernel<D, PH, NT, CMP>), dim3((unsigned)((waves + 3u) / 4u + (a.plan_out ? 1u : 0u))),
                        dim3(256), stream_lds_bytes(0), s, a, spw);
@@ -900,7 +900,7 @@ hipError_t launch_stream_varlen_t(const SegBatchArgs& a0, uint32_t spw, hipStrea
     // count (C4: 3 segments = 13.6 KB, 0.657 ms; 40-1500 B: 32 segments = 25 KB, 0.158 ms against
     // 0.273 for runs of 8), so adaptive runs (run_dev) at full residency are the default.
     a.touch = stream_touch(true) ? 1u : 0u;
-    a.xcd = stream_xcd(true) ? 1u : 0u;
+    a.xcd = stream_xcd_mode(1);
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
     hipLaunchKernelGGL((seg_stream_varlen_kernel<D, PH, NT>), dim3(grid), dim3(256),
@@ -962,7 +962,7 @@ template <int D, int PH, bool NT, bool ONE>
 hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
-    a.xcd = stream_xcd(true) ? 1u : 0u;
+    a.xcd = stream_xcd_mode(1);
     a.gather = store_gather() ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
@@ -1101,6 +1101,11 @@ void set_stream_xcd(int on) {
 bool stream_xcd(bool auto_on) {
     const int x = g_stream_xcd.load(std::memory_order_relaxed);
     return x < 0 ? auto_on : x != 0;
+}
+
+uint32_t stream_xcd_mode(uint32_t auto_mode) {
+    const int x = g_stream_xcd.load(std::memory_order_relaxed);
+    return x < 0 ? auto_mode : (uint32_t)x;
 }
 
 bool stream_touch(bool auto_on) {
