@@ -717,10 +717,13 @@ typedef enum netcsum_tune_key {
                                          (default) the run's live 64-B sectors read compacted, 16 per
                                          wave-instruction; 0 the live 1-KiB pieces of the run's span,
                                          each lane loading its 16 B where its sector is live          */
-    NETCSUM_TUNE_STORE_GATHER  = 28   /* dense strided segment batches (C2 / C5): 1 / -1 (default) the
+    NETCSUM_TUNE_STORE_GATHER  = 28,  /* dense strided segment batches (C2 / C5): 1 / -1 (default) the
                                          results of a workgroup's 4 runs gathered in LDS and written as
                                          whole lines by its last wave; 0 each wave writes its own run's
                                          results (partial lines)                                      */
+    NETCSUM_TUNE_CHAIN_GRID    = 29   /* NET_BUF chain batches, pass 1: 0 / -1 (default) one tile of 64
+                                         consecutive pieces per block; k = 1..16 a grid of k x the
+                                         resident blocks, each owning an equal contiguous share      */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -18,7 +18,8 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
        tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
   suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
   .kN = NETCSUM_TUNE_KERNEL N (chains.k3: pass 1 in the live-sector stream), .dN = NETCSUM_TUNE_CHUNKS N,
-  .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N
+  .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N,
+  .cgN = NETCSUM_TUNE_CHAIN_GRID N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -59,6 +60,8 @@ def main():
             netcsum.tune(netcsum.TUNE_STREAM_WAVES, int(part[1:]))
         elif part[:1] == "x":
             netcsum.tune(netcsum.TUNE_STREAM_XCD, int(part[1:]))
+        elif part[:2] == "cg":
+            netcsum.tune(netcsum.TUNE_CHAIN_GRID, int(part[2:]))
         elif part[:1] == "g":
             netcsum.tune(netcsum.TUNE_STORE_GATHER, int(part[1:]))
     name = name.split(".")[0]

@@ -2334,6 +2334,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_store_gather(value);
         return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CHAIN_GRID:
+        if (value < -1 || value > 16) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        netcsum::set_chain_grid(value);
+        return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_LIVE_COMPACT:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_live_compact(value);

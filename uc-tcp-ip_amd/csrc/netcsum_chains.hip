@@ -380,6 +380,11 @@ __device__ __forceinline__ void piece_store(uint64_t* eo, uint32_t j, uint32_t b
     }
 }
 
+// BAL (NETCSUM_TUNE_CHAIN_GRID >= 1, round 6): a grid of whole multiples of the resident blocks, block b
+// owning the contiguous pieces [np b / grid, np (b + 1) / grid) — every group the same piece count
+// within one, no block starting late, the descriptors prefetched across what were tile boundaries —
+// group g taking pieces lo + g + 16 i. Otherwise one tile of 64 consecutive pieces per block.
+template <bool BAL>
 __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint64_t* eo, uint32_t cap) {
     const int lane = (int)(threadIdx.x & (kPG - 1));
     constexpr uint32_t gpb = 256u / kPG;                          // groups per block
@@ -390,23 +395,39 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
     if (np > cap) {                                               // no room for the records: the
         return;                                                   // combine pass does the batch
     }
-    if (blockIdx.x >= ntiles) {
-        return;
+    uint32_t bid, iters, lo = 0u, lim = np;
+    if constexpr (BAL) {
+        bid = A.xcd ? sv::xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+        lo = (uint32_t)(((uint64_t)np * bid) / gridDim.x);
+        lim = (uint32_t)(((uint64_t)np * (bid + 1u)) / gridDim.x);
+        iters = (lim - lo + gpb - 1u) / gpb;                      // block-uniform
+        iters += iters & 1u;                                      // (the loop takes two at a time)
+        if (iters == 0u) {
+            return;
+        }
+    } else {
+        if (blockIdx.x >= ntiles) {
+            return;
+        }
+        // this block's tiles: bid, + gridDim.x, ...; group g takes pieces tile*64 + g + 16 k. With one
+        // tile per block (the default grid), the XCD-aware order: the blocks the dispatcher places on one
+        // XCD take one contiguous 1/8 of the tiles (sv::xcd_block over the first ntiles blocks, which
+        // are the ones with a tile), as the segment stream kernels' runs do
+        bid = (A.xcd && ntiles <= gridDim.x) ? sv::xcd_block(blockIdx.x, ntiles) : blockIdx.x;
+        iters = ((ntiles - bid + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
     }
-    // this block's tiles: bid, + gridDim.x, ...; group g takes pieces tile*64 + g + 16 k. With one tile
-    // per block (the default grid), the XCD-aware order: the blocks the dispatcher places on one XCD
-    // take one contiguous 1/8 of the tiles (sv::xcd_block over the first ntiles blocks, which are the
-    // ones with a tile), as the segment stream kernels' runs do
-    const uint32_t bid = (A.xcd && ntiles <= gridDim.x) ? sv::xcd_block(blockIdx.x, ntiles) : blockIdx.x;
-    const uint32_t iters = ((ntiles - bid + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
     auto piece_at = [&](uint32_t i) -> uint32_t {                 // the group's i-th piece
-        return (bid + (i / kPTile) * gridDim.x) * tile + g + gpb * (i % kPTile);
+        if constexpr (BAL) {
+            return lo + g + gpb * i;
+        } else {
+            return (bid + (i / kPTile) * gridDim.x) * tile + g + gpb * (i % kPTile);
+        }
     };
     const uintptr_t base = (uintptr_t)A.base;
     auto desc = [&](uint32_t j, uint64_t& off, uint32_t& len) {
-        const uint32_t jc = j < np ? j : 0u;                       // clamped, branch-free prefetch
+        const uint32_t jc = j < lim ? j : 0u;                      // clamped, branch-free prefetch
         off = A.off[jc];
-        len = j < np ? (uint32_t)A.len[jc] : 0u;
+        len = j < lim ? (uint32_t)A.len[jc] : 0u;
     };
     uint64_t dn_o, dnn_o;
     uint32_t dn_l, dnn_l;
@@ -425,14 +446,14 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
         dn_o = dnn_o;
         dn_l = dnn_l;
         piece_consume(SA, lane, b, h);
-        piece_store(eo, jA, b, h, lane, jA < np);
+        piece_store(eo, jA, b, h, lane, jA < lim);
         jA = piece_at(i + 2u);
         desc(piece_at(i + 3u), dnn_o, dnn_l);
         piece_issue(SA, base + dn_o, dn_l, lane);
         dn_o = dnn_o;
         dn_l = dnn_l;
         piece_consume(SB, lane, b, h);
-        piece_store(eo, jB, b, h, lane, jB < np);
+        piece_store(eo, jB, b, h, lane, jB < lim);
     }
 }
 
@@ -699,6 +720,17 @@ __global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, co
 
 }  // namespace
 
+namespace {
+thread_local TuneKnob g_chain_grid{-1};                          // NETCSUM_TUNE_CHAIN_GRID
+}
+void set_chain_grid(int v) {
+    g_chain_grid.store(v);
+}
+int chain_grid() {
+    const int v = g_chain_grid.load();
+    return v < 0 ? 0 : v;
+}
+
 hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s, uint32_t live_spw,
                                  int live_depth) {
     if (live_spw != 0u) {                                          // pass 1 in the live-sector stream:
@@ -724,7 +756,7 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     // (profiles/r3w_chain_grid_ab.log, tools/r3w_cmd.sh). Pass 2: a 16-lane group per chain.
     static const int per_cu = [] {                                // thread-safe one-time query
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel<false>, 256, 0) != hipSuccess || nb <= 0) nb = 4;
         return nb;
     }();
     const uint64_t resident = (uint64_t)std::max(cus, 1) * (uint64_t)per_cu;
@@ -733,7 +765,13 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
                                            std::max<uint64_t>(resident, 2ull * a.n));
     ChainBatchArgs ax = a;
     ax.xcd = stream_xcd(true) ? 1u : 0u;
-    hipLaunchKernelGGL(chain_piece_kernel, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax, eo, cap);
+    const int cg = chain_grid();
+    if (cg >= 1) {                                                 // balanced: cg x the resident blocks
+        ax.xcd = stream_xcd(false) ? 1u : 0u;
+        hipLaunchKernelGGL(chain_piece_kernel<true>, dim3((unsigned)(resident * (uint64_t)cg)), dim3(256), 0, s, ax, eo, cap);
+    } else {
+        hipLaunchKernelGGL(chain_piece_kernel<false>, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax, eo, cap);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;

@@ -133,6 +133,10 @@ hipError_t launch_chain_batch(const ChainBatchArgs& a, int group, int grid, hipS
 // chain; batches of more than `cap` pieces fall back to the wave-per-chain form inside pass 2.
 // live_spw != 0: pass 1 in the live-sector stream, runs of live_spw (<= 64) consecutive pieces,
 // live_depth (4 / 8) pieces in flight.
+// NETCSUM_TUNE_CHAIN_GRID: 0 / -1 pass 1 in tiles of 64 pieces, one per block; k >= 1 a grid of k x the
+// resident blocks, each owning an equal contiguous share of the pieces
+void set_chain_grid(int v);
+int chain_grid();
 hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s,
                                  uint32_t live_spw = 0u, int live_depth = 8);
 

@@ -76,6 +76,7 @@ TUNE_FAULT_INJECT = 25          # test only: the next offset/length packet batch
 TUNE_PLAN_AHEAD = 26            # first batch on a layout: sample it first and run in its plan (-1 auto, 0, 1)
 TUNE_LIVE_COMPACT = 27          # live-sector streams: live sectors compacted (-1 default / 1) or live pieces (0)
 TUNE_STORE_GATHER = 28          # dense segment stream: a block's results stored as whole lines (-1 / 1) or per wave (0)
+TUNE_CHAIN_GRID = 29            # chain pass 1: tiles of 64 pieces per block (-1 / 0) or k x resident blocks, equal shares
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
