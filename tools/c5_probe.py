@@ -16,6 +16,7 @@ and on a C2 batch allocated beside it (GPU box only; JSON lines):
   alloc2 / alloc2_run_probe   the kernel / its read probe on a SECOND 25-GB allocation of the same shard
   onealloc          the kernel with the pseudo-headers and the results inside the segments' allocation
   seg1_out2 / seg2_out1 / seg1_ph2_out2   the first allocations' buffers crossed with the second's
+  run_probe_x1      the read probe in the kernel's XCD-slice block order (the probe's default: dispatch order)
   x4 / x16 / x64 / x256   the kernel with XCD chunks of C blocks in turn (NETCSUM_TUNE_STREAM_XCD C)
   alloc2_xcd0 / alloc2_x16  the second allocation in the plain / chunked block order
 Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
@@ -69,6 +70,8 @@ def main():
                   n5 * (L + P + 2)),
                  ("c5_alloc2_run_probe", {"probe": 2}, lambda: netcsum.read_stream(seg2, n5 * L // 16 * 16, sink, stream=st),
                   n5 * L // 16 * 16),
+                 ("c5_alloc2_run_probe_x1", {"probe": 2, "xcd": 1},
+                  lambda: netcsum.read_stream(seg2, n5 * L // 16 * 16, sink, stream=st), n5 * L // 16 * 16),
                  ("c5_onealloc", {}, lambda: netcsum.batch_strided(segb, L, L, phb, P, P, n5, outb, netcsum.OP_DATA_CALC, stream=st),
                   n5 * (L + P + 2)),
                  # which buffer of the first allocations carries the loss: crossed pairs
@@ -125,7 +128,8 @@ def main():
                      (f"{name}_s24", {"tile": 24}, k(), algo), (f"{name}_s32", {"tile": 32}, k(), algo),
                      (f"{name}_run_probe_sleep", {"probe": 3}, rd(), n16),
                      (f"{name}_x4", {"xcd": 4}, k(), algo), (f"{name}_x16", {"xcd": 16}, k(), algo),
-                     (f"{name}_x64", {"xcd": 64}, k(), algo), (f"{name}_x256", {"xcd": 256}, k(), algo)]
+                     (f"{name}_x64", {"xcd": 64}, k(), algo), (f"{name}_x256", {"xcd": 256}, k(), algo),
+                     (f"{name}_run_probe_x1", {"probe": 2, "xcd": 1}, rd(), n16)]
         if n > (1 << 20):
             variants.append((f"{name}_chunk1M", {}, chunked(), algo))
     variants += extra

@@ -998,11 +998,14 @@ constexpr uint32_t kProbeRun = 16u * 1500u;
 // SLEEP (NETCSUM_TUNE_PROBE 3): s_sleep 2 (~128 clocks) after each piece's sum — the same reads
 // spread over a longer time per run, as the checksum kernel's per-piece work spreads them.
 template <int SLEEP>
-__global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint64_t n_bytes, unsigned long long* sink) {
+// xcd: the block order (xcd_block's mode; NETCSUM_TUNE_STREAM_XCD, default 0 here: the dispatch order).
+__global__ void __launch_bounds__(256) read_run_kernel(const uint8_t* base, uint64_t n_bytes, unsigned long long* sink,
+                                                       uint32_t xcd) {
     constexpr int D = 4;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t start = ((uint64_t)blockIdx.x * 4u + w) * kProbeRun;
+    const uint32_t blk = xcd ? sv::xcd_block(blockIdx.x, gridDim.x, xcd) : blockIdx.x;
+    const uint64_t start = ((uint64_t)blk * 4u + w) * kProbeRun;
     if (start >= n_bytes) {
         return;
     }
@@ -1048,12 +1051,13 @@ thread_local TuneKnob g_stream_xcd{-1};
 
 hipError_t launch_read_run(const void* d_p, uint64_t n_bytes, unsigned long long* d_sink, hipStream_t s, bool sleep) {
     const uint64_t waves = (n_bytes + kProbeRun - 1u) / kProbeRun;
+    const uint32_t xcd = stream_xcd_mode(0);
     if (sleep) {
         hipLaunchKernelGGL(read_run_kernel<2>, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
-                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
+                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink, xcd);
     } else {
         hipLaunchKernelGGL(read_run_kernel<0>, dim3((unsigned)((waves + 3u) / 4u)), dim3(256), stream_lds_bytes(5), s,
-                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink);
+                           static_cast<const uint8_t*>(d_p), n_bytes, d_sink, xcd);
     }
     return hipGetLastError();
 }
