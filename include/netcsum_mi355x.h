@@ -642,11 +642,12 @@ typedef enum netcsum_tune_key {
                                          batches off)                                               */
     NETCSUM_TUNE_STREAM_XCD    = 13,  /* segment / varlen / header / packet stream kernels: 1 = XCD-
                                          aware block order (each XCD's blocks take one contiguous 1/8
-                                         of the runs), 0 = the dispatch order, -1 = each kernel's
-                                         default (segment and varlen batches on, header and packet
-                                         batches off); 2..4096 = (segment and varlen batches) each
-                                         XCD takes chunks of that many blocks in turn; the other
-                                         kernels read any value >= 1 as 1                            */
+                                         of the runs), 0 = the dispatch order, 2..4096 = (segment
+                                         and varlen batches, chain pass 1) each XCD takes chunks of
+                                         that many blocks in turn, the other kernels reading any
+                                         value >= 1 as 1; -1 = each kernel's default (strided segment
+                                         batches chunks of 256, varlen batches and chain pass 1 one
+                                         slice per XCD, header and packet batches off)               */
     NETCSUM_TUNE_TX_FLUSH      = 14,  /* run-stream Tx finalize, write-back of the dirty checksum-field
                                          lines: -1 / 0 none (they are evicted during later launches),
                                          1 scatter stores written through at system scope, 2 an L2

@@ -17,7 +17,8 @@ and on a C2 batch allocated beside it (GPU box only; JSON lines):
   onealloc          the kernel with the pseudo-headers and the results inside the segments' allocation
   seg1_out2 / seg2_out1 / seg1_ph2_out2   the first allocations' buffers crossed with the second's
   run_probe_x1      the read probe in the kernel's XCD-slice block order (the probe's default: dispatch order)
-  x4 / x16 / x64 / x256   the kernel with XCD chunks of C blocks in turn (NETCSUM_TUNE_STREAM_XCD C)
+  x4 / x16 / x64 / x128 / x256 / x1024 / x4096   the kernel with XCD chunks of C blocks in turn
+                    (NETCSUM_TUNE_STREAM_XCD C); xcd1 the one-slice-per-XCD order; run_probe_x256 the probe
   alloc2_xcd0 / alloc2_x16  the second allocation in the plain / chunked block order
 Median / min of C5P_REPS HIP-event-timed launches per variant, C5P_ROUNDS interleaved rounds."""
 import json
@@ -129,6 +130,9 @@ def main():
                      (f"{name}_run_probe_sleep", {"probe": 3}, rd(), n16),
                      (f"{name}_x4", {"xcd": 4}, k(), algo), (f"{name}_x16", {"xcd": 16}, k(), algo),
                      (f"{name}_x64", {"xcd": 64}, k(), algo), (f"{name}_x256", {"xcd": 256}, k(), algo),
+                     (f"{name}_x128", {"xcd": 128}, k(), algo), (f"{name}_x1024", {"xcd": 1024}, k(), algo),
+                     (f"{name}_x4096", {"xcd": 4096}, k(), algo), (f"{name}_xcd1", {"xcd": 1}, k(), algo),
+                     (f"{name}_run_probe_x256", {"probe": 2, "xcd": 256}, rd(), n16),
                      (f"{name}_run_probe_x1", {"probe": 2, "xcd": 1}, rd(), n16)]
         if n > (1 << 20):
             variants.append((f"{name}_chunk1M", {}, chunked(), algo))

@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
         // tile per block (the default grid), the XCD-aware order: the blocks the dispatcher places on one
         // XCD take one contiguous 1/8 of the tiles (sv::xcd_block over the first ntiles blocks, which
         // are the ones with a tile), as the segment stream kernels' runs do
-        bid = (A.xcd && ntiles <= gridDim.x) ? sv::xcd_block(blockIdx.x, ntiles) : blockIdx.x;
+        bid = (A.xcd && ntiles <= gridDim.x) ? sv::xcd_block(blockIdx.x, ntiles, A.xcd) : blockIdx.x;
         iters = ((ntiles - bid + gridDim.x - 1u) / gridDim.x) * kPTile;   // block-uniform
     }
     auto piece_at = [&](uint32_t i) -> uint32_t {                 // the group's i-th piece
@@ -764,7 +764,7 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     const uint64_t g1 = std::min<uint64_t>(std::min<uint64_t>(((uint64_t)cap + 63u) / 64u, 1ull << 20),
                                            std::max<uint64_t>(resident, 2ull * a.n));
     ChainBatchArgs ax = a;
-    ax.xcd = stream_xcd(true) ? 1u : 0u;
+    ax.xcd = stream_xcd_mode(1);
     const int cg = chain_grid();
     if (cg >= 1) {                                                 // balanced: cg x the resident blocks
         ax.xcd = stream_xcd(false) ? 1u : 0u;
