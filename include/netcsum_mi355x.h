@@ -646,8 +646,9 @@ typedef enum netcsum_tune_key {
                                          and varlen batches, chain pass 1) each XCD takes chunks of
                                          that many blocks in turn, the other kernels reading any
                                          value >= 1 as 1; -1 = each kernel's default (strided segment
-                                         batches chunks of 256, varlen batches and chain pass 1 one
-                                         slice per XCD, header and packet batches off)               */
+                                         batches chunks of 256 when an XCD's slice would span >= 1 GiB,
+                                         else one slice per XCD, as for varlen batches and chain pass
+                                         1; header and packet batches off)                           */
     NETCSUM_TUNE_TX_FLUSH      = 14,  /* run-stream Tx finalize, write-back of the dirty checksum-field
                                          lines: -1 / 0 none (they are evicted during later launches),
                                          1 scatter stores written through at system scope, 2 an L2

@@ -964,12 +964,15 @@ template <int D, int PH, bool NT, bool ONE>
 hipError_t launch_stream_t(const SegBatchArgs& a0, uint32_t spw, hipStream_t s) {
     SegBatchArgs a = a0;
     a.touch = stream_touch(true) ? 1u : 0u;
-    // strided batches: XCD chunks of 256 blocks in turn. One slice per XCD puts the 8 XCDs' streams
-    // n/8 strides apart — for C5 2^23 x 375 B, a multiple of 8 MiB — and on boxes where the shard's
-    // pages land that way the streams collide: C5 3.772 ms against 3.521 in chunks of 256 and a read
-    // probe of 3.458 in the dispatch order, the probe itself 3.659 in the slice order (profiles/
-    // r6o_c5_probe.jsonl, r6p_c5_probe.jsonl); elsewhere chunks cost 0.2 % (3.522 against 3.513, r6n)
-    a.xcd = stream_xcd_mode(kXcdChunk);
+    // block order: one slice of the runs per XCD, or — when a slice spans >= 1 GiB — XCD chunks of
+    // 256 blocks in turn. One slice per XCD puts the 8 XCDs' streams n/8 strides apart — for C5 2^23 x
+    // 375 B, a multiple of 8 MiB — and on boxes where the shard's pages land that way the streams
+    // collide: C5 3.772 ms against 3.521 in chunks of 256 and a read probe of 3.458 in the dispatch
+    // order, the probe itself 3.659 in the slice order (profiles/r6o_c5_probe.jsonl, r6p_c5_probe.jsonl).
+    // Elsewhere chunks cost 0.2-0.4 % (C5 3.517 / 3.522 against 3.507 / 3.513; C2 0.2189 against 0.2180,
+    // r6n, r6q_runs.log), and C2's 200-MB slices never collided (r6e-r6p), so they keep the slices.
+    const uint64_t span = (uint64_t)a.n_seg * (a.seg_stride ? a.seg_stride : a.seg_len);
+    a.xcd = stream_xcd_mode(span / 8u >= (1ull << 30) ? kXcdChunk : 1u);
     a.gather = store_gather() ? 1u : 0u;
     const uint64_t waves = ((uint64_t)a.n_seg + spw - 1u) / spw;
     const int grid = (int)((waves + 3u) / 4u);
