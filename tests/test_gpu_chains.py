@@ -195,19 +195,23 @@ def test_chain_batch_matches_single_segment_batch():
     assert np.array_equal(got, out.cpu().numpy().view(np.uint16))
 
 
-@pytest.mark.parametrize("xcd,cg", [(0, -1), (1, -1), (0, 1), (1, 1), (0, 3)])
-def test_chain_pass1_tile_order(xcd, cg):
+@pytest.mark.parametrize("xcd,cg,touch", [(0, -1, -1), (1, -1, -1), (0, 1, -1), (1, 1, -1), (0, 3, -1),
+                                           (1, -1, 1), (0, -1, 1), (16, -1, 0)])
+def test_chain_pass1_tile_order(xcd, cg, touch):
     """Pass 1's XCD-aware tile order (NETCSUM_TUNE_STREAM_XCD; one tile of 64 pieces per block, the
     tiles of one XCD contiguous) and its balanced grid (NETCSUM_TUNE_CHAIN_GRID k: k x the resident
     blocks, equal contiguous shares — most blocks empty or with a few pieces at these sizes) are launch
-    options: the same records, the oracle's results, for piece counts that fill the tiles unevenly over
-    the 8 XCDs."""
+    options, as are chunked tile orders and the row touch of a group's first pieces
+    (NETCSUM_TUNE_STREAM_TOUCH): the same records, the oracle's results, for piece counts that fill the
+    tiles unevenly over the 8 XCDs."""
     try:
         netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
         netcsum.tune(netcsum.TUNE_CHAIN_GRID, cg)
+        netcsum.tune(netcsum.TUNE_STREAM_TOUCH, touch)
         for n_chains, seed in ((1, 1), (37, 2), (700, 3), (3000, 4)):
             cb = make_chain_batch(random.Random(seed), n_chains, 12)
             assert np.array_equal(_gpu(cb, 0), _want(cb, 0))
     finally:
         netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
         netcsum.tune(netcsum.TUNE_CHAIN_GRID, -1)
+        netcsum.tune(netcsum.TUNE_STREAM_TOUCH, -1)

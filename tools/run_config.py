@@ -19,7 +19,7 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
   .kN = NETCSUM_TUNE_KERNEL N (chains.k3: pass 1 in the live-sector stream), .dN = NETCSUM_TUNE_CHUNKS N,
   .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N,
-  .cgN = NETCSUM_TUNE_CHAIN_GRID N
+  .cgN = NETCSUM_TUNE_CHAIN_GRID N, .tN = NETCSUM_TUNE_STREAM_TOUCH N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -48,7 +48,9 @@ def main():
         if part.startswith("nt"):
             netcsum.tune(netcsum.TUNE_NT_LOADS, int(part[2:]))
             continue
-        if part[:1] == "d":
+        if part[:1] == "t":
+            netcsum.tune(netcsum.TUNE_STREAM_TOUCH, int(part[1:]))
+        elif part[:1] == "d":
             netcsum.tune(netcsum.TUNE_CHUNKS, int(part[1:]))
         elif part[:1] == "k":
             netcsum.tune(netcsum.TUNE_KERNEL, int(part[1:]))

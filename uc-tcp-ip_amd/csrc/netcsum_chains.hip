@@ -384,7 +384,10 @@ __device__ __forceinline__ void piece_store(uint64_t* eo, uint32_t j, uint32_t b
 // owning the contiguous pieces [np b / grid, np (b + 1) / grid) — every group the same piece count
 // within one, no block starting late, the descriptors prefetched across what were tile boundaries —
 // group g taking pieces lo + g + 16 i. Otherwise one tile of 64 consecutive pieces per block.
-template <bool BAL>
+// TOUCH (NETCSUM_TUNE_STREAM_TOUCH 1): the row touch of the stream kernels (netcsum_stream.h) for a
+// group's first 4 pieces — lanes 0..7 load one dword, plain policy, at +0 / +1 KiB of piece l / 2 with
+// the first data loads, never used — so the pieces the group streams later have requests under way.
+template <bool BAL, bool TOUCH>
 __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint64_t* eo, uint32_t cap) {
     const int lane = (int)(threadIdx.x & (kPG - 1));
     constexpr uint32_t gpb = 256u / kPG;                          // groups per block
@@ -434,6 +437,15 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
     uint32_t jA = piece_at(0u);
     desc(jA, dn_o, dn_l);
     desc(piece_at(1u), dnn_o, dnn_l);                              // two ahead
+    uint32_t touch = 0u;
+    if constexpr (TOUCH) {
+        uint64_t to;
+        uint32_t tl;
+        const uint32_t ti = (uint32_t)lane >> 1, tb = ((uint32_t)lane & 1u) << 10;
+        desc(ti < 4u && ti < iters ? piece_at(ti) : ~0u, to, tl);
+        const uintptr_t ta = tb < tl ? base + to + tb : zero_addr();
+        touch = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(ta);
+    }
     PieceStage SA, SB;
     piece_issue(SA, base + dn_o, dn_l, lane);
     dn_o = dnn_o;
@@ -455,6 +467,7 @@ __global__ void __launch_bounds__(256) chain_piece_kernel(ChainBatchArgs A, uint
         piece_consume(SB, lane, b, h);
         piece_store(eo, jB, b, h, lane, jB < lim);
     }
+    asm volatile("" ::"v"(touch));                                 // (the touch is never used)
 }
 
 // Pass 1 in the live-sector stream (NETCSUM_TUNE_KERNEL 3; round 5): a wave takes a run of `spw` pieces
@@ -756,7 +769,7 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     // (profiles/r3w_chain_grid_ab.log, tools/r3w_cmd.sh). Pass 2: a 16-lane group per chain.
     static const int per_cu = [] {                                // thread-safe one-time query
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel<false>, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_piece_kernel<false, false>, 256, 0) != hipSuccess || nb <= 0) nb = 4;
         return nb;
     }();
     const uint64_t resident = (uint64_t)std::max(cus, 1) * (uint64_t)per_cu;
@@ -768,9 +781,14 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
     const int cg = chain_grid();
     if (cg >= 1) {                                                 // balanced: cg x the resident blocks
         ax.xcd = stream_xcd(false) ? 1u : 0u;
-        hipLaunchKernelGGL(chain_piece_kernel<true>, dim3((unsigned)(resident * (uint64_t)cg)), dim3(256), 0, s, ax, eo, cap);
+        hipLaunchKernelGGL((chain_piece_kernel<true, false>), dim3((unsigned)(resident * (uint64_t)cg)), dim3(256), 0, s, ax,
+                           eo, cap);
+    } else if (stream_touch(false)) {
+        hipLaunchKernelGGL((chain_piece_kernel<false, true>), dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax,
+                           eo, cap);
     } else {
-        hipLaunchKernelGGL(chain_piece_kernel<false>, dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax, eo, cap);
+        hipLaunchKernelGGL((chain_piece_kernel<false, false>), dim3((unsigned)std::max<uint64_t>(g1, 1u)), dim3(256), 0, s, ax,
+                           eo, cap);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
