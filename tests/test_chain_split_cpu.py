@@ -91,3 +91,88 @@ def test_split_past_the_u32_wrap():
     ph = np.arange(12, dtype=np.uint8)
     want = oracle.batch_chains(base, offs, lens, first, ph, 12, 12, 1, 0)
     assert model_chain(base, offs, lens, 0, per, ph, 0, 12) == int(want[0])
+
+
+# ---- the one-record form (round 6: seg_live_varlen_kernel<..., CH> + chain_combine_h_kernel) ----
+MOD_MAX = 131072                                                      # kChainModMax
+
+
+def half_word_sum(base: np.ndarray, a: int, n: int) -> int:
+    """Pass 1's record: the exact little-endian half-word sum h = e + 256 o of base[a:a+n] in the
+    absolute frame (the live stream's wave total of v_sad_u16 over its 128-B-aligned run)."""
+    if n == 0:
+        return 0
+    q0, q1 = a & ~1, (a + n + 1) & ~1
+    w = np.zeros(q1 - q0, np.uint8)
+    w[a - q0:a - q0 + n] = base[a:a + n]
+    h = int(w.view("<u2").astype(np.uint64).sum())
+    assert h < 2 ** 31                                                # pieces < 64 KiB
+    return h
+
+
+def fold64(s: int) -> int:
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+def model_chain_h(base, offs, lens, p0, p1, ph, pa, plen):
+    """chain_combine_h_kernel: S = sum(swap ? h : 256 h) + the pseudo-header's 256 E + O, folded —
+    T's one's-complement residue while the chain holds <= 131 072 stream bytes; longer chains take
+    the exact even / odd form (model_chain)."""
+    pl = (plen - 1 if (p0 == p1 and plen & 1) else plen) if plen else 0
+    if pl + sum(int(lens[j]) for j in range(p0, p1)) > MOD_MAX:
+        return model_chain(base, offs, lens, p0, p1, ph, pa, plen)
+    S = 0
+    if pl:
+        e, o = split(ph, pa, pl)
+        S += (o << 8) + e if pa & 1 else (e << 8) + o
+    par = plen & 1
+    for j in range(p0, p1):
+        h = half_word_sum(base, int(offs[j]), int(lens[j]))
+        S += h if (int(offs[j]) & 1) ^ par else h << 8
+        par ^= int(lens[j]) & 1
+    s = fold64(S)
+    host = ((s & 0xFF) << 8) | (s >> 8)
+    return (~host) & 0xFFFF
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_one_record_model_matches_oracle(seed):
+    rng = np.random.default_rng(100 + seed)
+    n_pieces = 600
+    lens = rng.integers(0, 2000, size=n_pieces).astype(np.uint16)
+    lens[rng.random(n_pieces) < 0.1] = 0
+    gaps = rng.integers(0, 5, size=n_pieces).astype(np.uint64)
+    offs = np.zeros(n_pieces, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    base = rng.integers(0, 256, size=int(offs[-1]) + 2100, dtype=np.uint8)
+    cuts = np.sort(rng.choice(np.arange(1, n_pieces), size=60, replace=False))
+    first = np.concatenate([[0], cuts, [n_pieces]]).astype(np.uint32)
+    first = np.insert(first, 5, first[5])                              # a NULL chain
+    n = len(first) - 1
+    plen = 13 if seed & 1 else 12
+    ph = rng.integers(0, 256, size=plen * n + 16, dtype=np.uint8)
+    want = oracle.batch_chains(base, offs, lens, first, ph[: plen * n], plen, plen, n, 0)
+    got = [model_chain_h(base, offs, lens, int(first[i]), int(first[i + 1]), ph, plen * i, plen) for i in range(n)]
+    assert np.array_equal(np.array(got, np.uint16), want)
+
+
+@pytest.mark.parametrize("total", [131070, 131072, 131074, 131076])
+def test_one_record_model_at_the_modulo_bound(total):
+    """All-0xFF chains around the 131 072-B bound (T = 2^32 - 1 at 131 074 B, the u32 wrap beyond),
+    odd pieces at odd addresses, and sums that are positive multiples of 65535 / zero."""
+    rng = np.random.default_rng(total)
+    k = 5
+    cuts = np.sort(rng.choice(np.arange(1, total - 12), size=k - 1, replace=False))
+    lens = np.diff(np.concatenate([[0], cuts, [total - 12]])).astype(np.uint16)
+    offs = np.cumsum(np.concatenate([[1], lens[:-1].astype(np.uint64) + 1])).astype(np.uint64)
+    base = np.full(int(offs[-1]) + int(lens[-1]) + 8, 0xFF, np.uint8)
+    first = np.array([0, k], np.uint32)
+    ph = np.full(12, 0xFF, np.uint8)
+    want = oracle.batch_chains(base, offs, lens, first, ph, 12, 12, 1, 0)
+    assert model_chain_h(base, offs, lens, 0, k, ph, 0, 12) == int(want[0])
+    z = np.zeros(64, np.uint8)
+    assert model_chain_h(z, np.array([1, 9], np.uint64), np.array([3, 5], np.uint16), 0, 2, z, 0, 12) == 0xFFFF
+    f = np.full(64, 0xFF, np.uint8)
+    assert model_chain_h(f, np.array([1, 9], np.uint64), np.array([3, 3], np.uint16), 0, 2, z, 0, 0) == 0

@@ -17,9 +17,9 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
        pkt_len 1506; rx_ringv / tx_ringv the same ring by offset/length descriptors; rx_nb2kv /
        tx_nb2kv 1500-B datagrams in 2-KiB slots at +64 by descriptors (tools/ring_layouts.py)
   suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
-  .kN = NETCSUM_TUNE_KERNEL N (chains.k3: pass 1 in the live-sector stream), .dN = NETCSUM_TUNE_CHUNKS N,
+  .kN = NETCSUM_TUNE_KERNEL N (chains.k3 / .k4: pass 1 in round 5's live form / tiled groups), .dN = NETCSUM_TUNE_CHUNKS N,
   .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N,
-  .cgN = NETCSUM_TUNE_CHAIN_GRID N, .tN = NETCSUM_TUNE_STREAM_TOUCH N
+  .cgN = NETCSUM_TUNE_CHAIN_GRID N, .tN = NETCSUM_TUNE_STREAM_TOUCH N, .lcN = NETCSUM_TUNE_LIVE_COMPACT N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -47,6 +47,9 @@ def main():
     for part in name.split(".")[1:]:
         if part.startswith("nt"):
             netcsum.tune(netcsum.TUNE_NT_LOADS, int(part[2:]))
+            continue
+        if part[:2] == "lc":
+            netcsum.tune(netcsum.TUNE_LIVE_COMPACT, int(part[2:]))
             continue
         if part[:1] == "t":
             netcsum.tune(netcsum.TUNE_STREAM_TOUCH, int(part[1:]))

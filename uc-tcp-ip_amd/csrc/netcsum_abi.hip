@@ -1395,16 +1395,32 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
     // be allocated (or is pinned by a stream capture) takes the wave-per-chain kernel instead.
     if (g == 0 && g_tune_kernel.load() != 1) {
         const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 20, 128ull * n_chains), 1ull << 24);
+        const int kern = g_tune_kernel.load();
+        // the default (0) and 5: one record per piece (4 B); 3 the round-5 live form, others the tiled
+        // 16-lane groups (both 8 B per piece)
+        const bool one_rec = kern == 0 || kern == 5;
         ScratchLease scratch;
-        if (scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * 8u) == hipSuccess) {
+        if (scratch.acquire(dev, static_cast<hipStream_t>(hip_stream), (size_t)cap * (one_rec ? 4u : 8u)) == hipSuccess) {
             // pass 1: tiled 16-lane groups, or with TUNE_KERNEL 3 the live-sector stream in runs of 16
             // pieces (TUNE_TILE 1..64 sets the run, TUNE_CHUNKS 4 the depth) — 0.1993-0.2046 ms on the
             // chain row against 0.1756-0.1803 for the groups (profiles/r5v_chains.log: two wave totals
             // per piece end, the byte and the half-word sums, cost more than the sectors save there)
+            // Default / TUNE_KERNEL 5 (round 6): the segment live-sector stream with ONE wave total per piece
+            // end, the piece's half-word sum, combined modulo 65535 (chain_combine_h_kernel)
             const int tk = g_tune_tile.load(), ch = g_tune_chunks.load();
-            const uint32_t live = g_tune_kernel.load() != 3 ? 0u : (tk >= 1 && tk <= 64) ? (uint32_t)tk : 16u;
+            const uint32_t live = (kern != 3 && !one_rec) ? 0u : (tk >= 1 && tk <= 64) ? (uint32_t)tk : 16u;
             const int depth = ch == 4 ? 4 : 8;
             char d[128];
+            if (one_rec) {
+                const bool cmp = netcsum::live_compact();
+                snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d,chain,nt%s> pieces_per_wave=%u +chain_combine_h_kernel",
+                         depth, cmp ? ",compact" : "", live);
+                netcsum::set_last_launch(d);
+                NC_HIP(netcsum::launch_chain_two_pass_h(a, static_cast<uint32_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
+                                                        static_cast<hipStream_t>(hip_stream), live, depth, cmp));
+                NC_HIP(scratch.end());
+                return NET_UTIL_ERR_NONE;
+            }
             if (live) {
                 snprintf(d, sizeof d, "chain_live_piece_kernel<D=%d,nt> pieces_per_wave=%u +chain_combine_kernel", depth, live);
             } else {

@@ -731,7 +731,125 @@ __global__ void __launch_bounds__(256) chain_combine_kernel(ChainBatchArgs A, co
     }
 }
 
+// ---- one record per piece (round 6) ------------------------------------------------------------
+// Pass 1 in the live-sector segment stream (launch_chain_live_records) leaves ONE number per piece: its
+// exact half-word sum h = e + 256 o in the absolute LE frame (e / o: its bytes at even / odd
+// addresses). A piece's share of the chain's big-endian word sum T is 256 e + o where its stream
+// parity equals its address parity and e + 256 o = h where it differs, and 256 e + o ≡ 256 h (mod
+// 65535). While T < 2^32 the reference's u32 accumulator never wraps (net_util.c:1554, :1685) and its
+// fold is T's one's-complement residue — the value in [1, 0xFFFF] congruent to T mod 65535, 0 only for
+// T = 0 — which is the fold of ANY non-negative S ≡ T (mod 65535) that is 0 exactly when T is: here
+// S = Σ (swap ? h : 256 h) + 256 E_p + O_p of the pseudo-header, each term 0 only when its bytes are.
+// T <= ceil(L / 2) x 0xFFFF < 2^32 for a chain of L <= 131 072 stream bytes (every IPv4 datagram,
+// every IPv6 one short of a jumbogram); a longer chain, whose accumulator may wrap, is re-read by its
+// group in the exact even / odd form (span_eo, as chain_batch_kernel) — correct, slower.
+constexpr uint64_t kChainModMax = 131072u;
+
+__device__ __forceinline__ uint32_t fold64(uint64_t s) {
+    while (s >> 16) {
+        s = (s & 0xFFFFu) + (s >> 16);
+    }
+    return (uint32_t)s;
+}
+
+__global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, const uint32_t* hr, uint32_t cap) {
+    const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
+    if (np > cap) {                                               // pass 1 had no room for the records:
+        const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // the wave-per-chain form
+        for (uint32_t ch = blockIdx.x * 4u + w; ch < A.n; ch += gridDim.x * 4u) {
+            wave_chain(A, ch);
+        }
+        return;
+    }
+    const int lane = (int)(threadIdx.x & (kCG - 1));
+    const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(kCG - 1);          // the group's ballot bits
+    const uint32_t below = (1u << lane) - 1u;
+    const uint32_t ngr = gridDim.x * (256u / kCG);
+    const uint32_t c0 = blockIdx.x * (256u / kCG) + (threadIdx.x & ~63u) / kCG;
+    const uint32_t rounds = c0 < A.n ? (A.n - c0 + ngr - 1u) / ngr : 0u;
+    const uintptr_t base = (uintptr_t)A.base;
+    for (uint32_t r = 0u; r < rounds; ++r) {
+        const uint32_t ch = c0 + r * ngr + (threadIdx.x & 63u) / kCG;
+        const bool live = ch < A.n;
+        const uint32_t p0 = live ? A.first[ch] : 0u;
+        const uint32_t p1 = live ? A.first[ch + 1u] : 0u;
+        uint64_t S = 0u, L = 0u;                                  // this lane's share of S, of the lengths
+        uint32_t plen = 0u, par = 0u;                             // par: stream parity at the next piece
+        uintptr_t pa = 0u;
+        if (live && A.pseudo && A.pseudo_len) {
+            plen = A.pseudo_len;
+            if (p0 == p1 && (plen & 1u)) {
+                plen -= 1u;                                       // NULL chain quirk
+            }
+            pa = (uintptr_t)A.pseudo + (uint64_t)ch * A.pseudo_stride;
+            const EO s = span_eo<kCG>(pa, plen, lane);
+            S += (pa & 1u) ? ((uint64_t)s.o << 8) + s.e : ((uint64_t)s.e << 8) + s.o;
+            par = A.pseudo_len & 1u;                              // pieces follow ALL pseudo bytes
+        }
+        const uint32_t par0 = par;
+        uint32_t steps = (p1 - p0 + kCG - 1u) / kCG;
+#pragma unroll
+        for (int m = 32; m >= kCG; m >>= 1) {                     // the wave's longest chain
+            steps = max(steps, (uint32_t)__shfl_xor((int)steps, m, 64));
+        }
+        for (uint32_t t = 0u; t < steps; ++t) {
+            const uint32_t j = p0 + t * kCG + (uint32_t)lane;
+            const bool v = j < p1;
+            const uint32_t len = v ? (uint32_t)A.len[j] : 0u;
+            const uint64_t off = v ? A.off[j] : 0u;
+            const uint64_t h = v ? hr[j] : 0u;
+            const uint32_t odd = (uint32_t)(__ballot((len & 1u) != 0u) >> sh) & 0xFFFFu;
+            const uint32_t spar = par ^ ((uint32_t)__popc(odd & below) & 1u);
+            const uint32_t swap = ((uint32_t)(base + off) & 1u) ^ spar;
+            S += swap ? h : h << 8;
+            L += len;
+            par ^= (uint32_t)__popc(odd) & 1u;
+        }
+        S = group_sum64<kCG>(S);
+        L = group_sum64<kCG>(L);
+        const bool big = live && L + plen > kChainModMax;         // group-uniform
+        if (big) {                                                // the exact form (u32 wrap included)
+            uint64_t E = 0u, O = 0u;
+            if (plen != 0u) {
+                const EO s = span_eo<kCG>(pa, plen, lane);
+                if (pa & 1u) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
+            }
+            uint32_t spos = par0;
+            for (uint32_t j = p0; j < p1; ++j) {
+                const uintptr_t a = base + A.off[j];
+                const uint32_t len = A.len[j];
+                const EO s = span_eo<kCG>(a, len, lane);
+                if (((uint32_t)(a & 1u)) != spos) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
+                spos ^= (len & 1u);
+            }
+            E = group_sum64<kCG>(E);
+            O = group_sum64<kCG>(O);
+            if (lane == 0) {
+                chain_out(A, ch, E, O);
+            }
+        } else if (live && lane == 0) {
+            const uint32_t sum = fold64(S);
+            const uint32_t host = ((sum & 0xFFu) << 8) | (sum >> 8);   // NET_UTIL_NET_TO_HOST_16
+            if (A.verify) {
+                static_cast<uint8_t*>(A.out)[ch] = (host == 0xFFFFu) ? 1u : 0u;
+            } else {
+                static_cast<uint16_t*>(A.out)[ch] = (uint16_t)(~host);
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_chain_two_pass_h(const ChainBatchArgs& a, uint32_t* rec, uint32_t cap, int cus, hipStream_t s,
+                                   uint32_t spw, int depth, bool cmp) {
+    hipError_t e = launch_chain_live_records(a, rec, cap, depth, spw, cmp, s);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;
+    const unsigned g2 = (unsigned)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 64u);
+    hipLaunchKernelGGL(chain_combine_h_kernel, dim3(g2), dim3(256), 0, s, a, (const uint32_t*)rec, cap);
+    return hipGetLastError();
+}
 
 namespace {
 thread_local TuneKnob g_chain_grid{-1};                          // NETCSUM_TUNE_CHAIN_GRID

@@ -36,6 +36,8 @@ struct SegBatchArgs {
     uint32_t        plan_tag;      // descriptors (an extra sampler block), nullptr = none
     uint32_t        gather;        // dense stream kernel: a block's results gathered in LDS and stored as
                                    // one line by its last wave (set by the launcher)
+    const uint32_t* n_dev;         // chain pass 1 (live kernel, CH): the segment count on the device
+                                   // (chain_first[n]); n_seg is then the records' capacity
 };
 
 struct LaunchCfg {
@@ -139,6 +141,14 @@ void set_chain_grid(int v);
 int chain_grid();
 hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t cap, int cus, hipStream_t s,
                                  uint32_t live_spw = 0u, int live_depth = 8);
+// Chain pass 1 in the live-sector segment stream (seg_live_varlen_kernel<…, CH>, netcsum_stream.hip):
+// runs of spw (<= 64) consecutive pieces, depth (4 / 8) pieces in flight, compacted sectors when cmp;
+// each piece's exact half-word sum (u32, absolute LE frame) into rec[j]. Then the combine pass over
+// those records (chain_combine_h_kernel, netcsum_chains.hip); the two together:
+hipError_t launch_chain_live_records(const ChainBatchArgs& c, uint32_t* rec, uint32_t cap, int depth, uint32_t spw, bool cmp,
+                                     hipStream_t s);
+hipError_t launch_chain_two_pass_h(const ChainBatchArgs& a, uint32_t* rec, uint32_t cap, int cus, hipStream_t s,
+                                   uint32_t spw, int depth, bool cmp);
 
 // CRC-32 batches (netcsum_crc.hip; net_util.c:485-636).
 struct CrcBatchArgs {

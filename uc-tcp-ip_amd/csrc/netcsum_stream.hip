@@ -612,13 +612,32 @@ __device__ __forceinline__ void varlen_sample(const uint64_t* offs, const uint16
 constexpr uint64_t kSentinelPiece = 1ull << 63;
 constexpr uint32_t kNoEnd = ~0u;
 
-template <int D, int PH, bool NT, bool CMP>
+// CH (round 6): pass 1 of a NET_BUF chain batch (netcsum_chains.hip). The segments are the chain
+// pieces, their count lives on the device (A.n_dev; A.n_seg is the records' capacity, a batch with
+// more pieces returns at once and the combine pass takes it whole), no pseudo-header (PH 0), and each
+// piece's record is its exact half-word sum T in the absolute LE frame (u32; < 2^31 for a piece of
+// < 64 KiB) — one wave total per piece end, as for a segment; the combine pass applies the chain's
+// stream parity.
+template <int D, int PH, bool NT, bool CMP, bool CH = false>
 __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, uint32_t spw) {
     __shared__ uint32_t sect_all[4][32];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t nwg = gridDim.x;
-    if (A.plan_out != nullptr) {                              // the last block: the next batch's plan
+    uint32_t nseg = A.n_seg;
+    if constexpr (CH) {
+        static_assert(PH == 0, "chain pieces carry no pseudo-header");
+        const uint32_t np = (uint32_t)__builtin_amdgcn_readfirstlane((int)*A.n_dev);
+        if (np > A.n_seg) {                                   // no room for the records
+            return;
+        }
+        const uint32_t need = (uint32_t)(((uint64_t)np + 4ull * spw - 1u) / (4ull * spw));
+        if (blockIdx.x >= need) {                             // (the grid is sized for the capacity)
+            return;
+        }
+        nseg = np;
+        nwg = need;                                           // the XCD order over the blocks with a run
+    } else if (A.plan_out != nullptr) {                       // the last block: the next batch's plan
         nwg -= 1u;
         if (blockIdx.x == nwg) {
             __shared__ uint32_t part[4][3];
@@ -635,11 +654,11 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
     }
     const uint32_t blk = A.xcd ? xcd_block(blockIdx.x, nwg, A.xcd) : blockIdx.x;
     const uint64_t sb64 = ((uint64_t)blk * 4u + w) * spw;
-    if (sb64 >= A.n_seg) {
+    if (sb64 >= nseg) {
         return;
     }
     const uint32_t s_begin = (uint32_t)sb64;
-    const uint32_t nres = min(A.n_seg - s_begin, spw);       // spw <= 64: segment k in lane k
+    const uint32_t nres = min(nseg - s_begin, spw);          // spw <= 64: segment k in lane k
     const uint32_t lane16 = 16u * lane;
     const bool ph_odd = PH != 0 && (A.pseudo_len & 1u) != 0u;
     const uintptr_t base = (uintptr_t)A.base;
@@ -716,13 +735,21 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
             for (uint32_t i = 0; i < 4u; ++i) {
                 if (k0 + i < nres) {
                     const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)(16u * i));
-                    const bool od = __builtin_amdgcn_readlane((int)odd, (int)(16u * i)) != 0;
-                    finish_segment<PH>(k0 + i, T, od, A.verify != 0u, lane, ps0, ps1, res0, res1);
+                    if constexpr (CH) {
+                        res0 = (lane == k0 + i) ? T : res0;
+                    } else {
+                        const bool od = __builtin_amdgcn_readlane((int)odd, (int)(16u * i)) != 0;
+                        finish_segment<PH>(k0 + i, T, od, A.verify != 0u, lane, ps0, ps1, res0, res1);
+                    }
                 }
             }
         }
         asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
-        store_run_results(A, s_begin, nres, lane, res0, res1);
+        if constexpr (CH) {
+            if (mine) static_cast<uint32_t*>(A.out)[s_begin + lane] = res0;
+        } else {
+            store_run_results(A, s_begin, nres, lane, res0, res1);
+        }
         return;
     }
 
@@ -870,6 +897,10 @@ __global__ void __launch_bounds__(256) seg_live_varlen_kernel(SegBatchArgs A, ui
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (CH) {                                        // lane k: piece k's exact sum
+        if (mine) static_cast<uint32_t*>(A.out)[s_begin + lane] = tot;
+        return;
+    }
     // vector epilogue, lane k = segment k (an empty one: its pseudo-header alone)
     uint32_t t = fold16(tot);
     if ((((uint32_t)rel & 1u) != 0u) != ph_odd) {
@@ -1224,6 +1255,29 @@ hipError_t launch_live_varlen(const SegBatchArgs& a, int depth, uint32_t spw, hi
                                              : launch_live_varlen_t<D_, PH_, true, false>(a, spw, s);
     NETCSUM_LV(4, 0) NETCSUM_LV(4, 1) NETCSUM_LV(4, 2) NETCSUM_LV(8, 0) NETCSUM_LV(8, 1) NETCSUM_LV(8, 2)
 #undef NETCSUM_LV
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_chain_live_records(const ChainBatchArgs& c, uint32_t* rec, uint32_t cap, int depth, uint32_t spw, bool cmp,
+                                     hipStream_t s) {
+    if (rec == nullptr || spw == 0u || spw > 64u || cap == 0u) return hipErrorInvalidValue;
+    SegBatchArgs a{};
+    a.base = c.base;
+    a.seg_off = c.off;
+    a.seg_len_v = c.len;
+    a.n_seg = cap;                                             // capacity; the count is chain_first[n]
+    a.n_dev = c.first + c.n;
+    a.out = rec;
+    a.xcd = stream_xcd_mode(1);
+    const dim3 grid((unsigned)((((uint64_t)cap + spw - 1u) / spw + 3u) / 4u));
+#define NETCSUM_LC(D_)                                                                                         \
+    if (depth == D_) {                                                                                         \
+        if (cmp) hipLaunchKernelGGL((seg_live_varlen_kernel<D_, 0, true, true, true>), grid, dim3(256), stream_lds_bytes(0), s, a, spw); \
+        else hipLaunchKernelGGL((seg_live_varlen_kernel<D_, 0, true, false, true>), grid, dim3(256), stream_lds_bytes(0), s, a, spw); \
+        return hipGetLastError();                                                                              \
+    }
+    NETCSUM_LC(4) NETCSUM_LC(8)
+#undef NETCSUM_LC
     return hipErrorInvalidValue;
 }
 
