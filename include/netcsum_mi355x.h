@@ -463,11 +463,14 @@ NET_ERR  NetUtil_MI355X_TxBurstHost        (void            *h_base,
  * reference's pdata_buf == NULL case (an odd pseudo-header loses its last octet,
  * net_util.c:1601-1611); describe a chain of empty buffers with one zero-length piece.
  * op: NETCSUM_OP_DATA_CALC (u16 out) or NETCSUM_OP_DATA_VERIFY (u8 DEF_OK/DEF_FAIL out).
- * Forms: by default two launches on the stream — per-piece sums in piece order into this thread's
- * device scratch for the stream (8 B per piece, room for max(2^20, 128 * n_chains) pieces; a batch
- * with more pieces is done in the wave-per-chain form instead, same results), then one combine per
- * chain; NETCSUM_TUNE_KERNEL 1 selects the wave-per-chain form, NETCSUM_TUNE_GROUP_LANES 16 / 32 / 64
- * a lane group per chain. Graph capture: as for the Tx scratch (one uncaptured call first).
+ * Forms: by default two launches on the stream — the pieces read as a segment stream (live 64-B
+ * sectors, runs of 12 pieces), each piece's exact half-word sum into this thread's device scratch
+ * for the stream (4 B per piece, room for max(2^20, 128 * n_chains) pieces; a batch with more pieces
+ * is done in the wave-per-chain form instead, same results), then one combine per chain, modulo
+ * 65535 up to 131 072 stream bytes and in the exact u32-wrapping form beyond;
+ * NETCSUM_TUNE_KERNEL 1 selects the wave-per-chain form, 4 the round-5 two-pass form (tiled 16-lane
+ * groups, 8-B even / odd records), NETCSUM_TUNE_GROUP_LANES 16 / 32 / 64 a lane group per chain.
+ * Graph capture: as for the Tx scratch (one uncaptured call first).
  * ============================================================================================ */
 NET_ERR  NetUtil_MI355X_ChkSumBatchChains  (const void      *d_base,
                                             const uint64_t  *d_piece_off,
@@ -608,9 +611,12 @@ typedef enum netcsum_tune_key {
                                          CHUNKS 4 / 8 = pieces in flight; TILE = headers per run,
                                          auto: the most that fit 4 KiB from any 128-B lead, 192 for
                                          20-B headers). Chain batches: 1 = the wave-per-chain form
-                                         (default: two passes, see (2c)), 3 = two passes with the
-                                         first in the live-sector stream (TILE = pieces per run,
-                                         CHUNKS 4 / 8 = pieces in flight)                          */
+                                         (default / 5: two passes, the first in the segment
+                                         live-sector stream with one record per piece, see (2c)), 3 =
+                                         two passes with round 5's live-sector pass 1 (two sums per
+                                         piece), 4 = two passes with tiled 16-lane groups in pass 1;
+                                         3 / 5: TILE = pieces per run, CHUNKS 4 / 8 = pieces in
+                                         flight                                                       */
     NETCSUM_TUNE_CHUNKS        = 6,   /* 16-B chunks per lane per pass: 0 auto, 1,2,3,4,6,8;
                                          run-stream kernels: 1-KiB pieces in flight (4 / 8)        */
     NETCSUM_TUNE_PROBE         = 7,   /* read-stream probe: 0 register loads, 1 LDS-DMA (default),
@@ -723,9 +729,13 @@ typedef enum netcsum_tune_key {
                                          results of a workgroup's 4 runs gathered in LDS and written as
                                          whole lines by its last wave; 0 each wave writes its own run's
                                          results (partial lines)                                      */
-    NETCSUM_TUNE_CHAIN_GRID    = 29   /* NET_BUF chain batches, pass 1: 0 / -1 (default) one tile of 64
-                                         consecutive pieces per block; k = 1..16 a grid of k x the
-                                         resident blocks, each owning an equal contiguous share      */
+    NETCSUM_TUNE_CHAIN_GRID    = 29,  /* NET_BUF chain batches, tiled pass 1 (TUNE_KERNEL 4): 0 / -1
+                                         (default) one tile of 64 consecutive pieces per block; k =
+                                         1..16 a grid of k x the resident blocks, each owning an equal
+                                         contiguous share                                             */
+    NETCSUM_TUNE_CHAIN_COMBINE = 30   /* NET_BUF chain batches, the one-record form's combine pass:
+                                         16 or 64 lanes per chain; -1 (default) = chosen by the
+                                         library                                                      */
 } NETCSUM_TUNE_KEY;
 
 NET_ERR  NetUtil_MI355X_Tune               (int key, int value);

@@ -110,9 +110,11 @@ def test_batch_argument_validation_before_device_work():
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_GROUP_LANES, 3) == 219
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_BLOCK_THREADS, 512) == 219
     assert L.NetUtil_MI355X_Tune(99, 1) == 219
-    assert L.NetUtil_MI355X_Tune(30, 0) == 219                                 # no such key
+    assert L.NetUtil_MI355X_Tune(31, 0) == 219                                 # no such key
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CHAIN_GRID, 17) == 219           # -1 .. 16
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CHAIN_GRID, -1) == 200
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CHAIN_COMBINE, 32) == 219        # -1, 16 or 64
+    assert L.NetUtil_MI355X_Tune(netcsum.TUNE_CHAIN_COMBINE, -1) == 200
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_STORE_GATHER, 2) == 219          # -1, 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_LIVE_COMPACT, 2) == 219          # -1, 0 or 1
     assert L.NetUtil_MI355X_Tune(netcsum.TUNE_PLAN_AHEAD, 2) == 219            # -1, 0 or 1

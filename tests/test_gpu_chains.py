@@ -25,7 +25,9 @@ def _defaults():
     netcsum.tune(netcsum.TUNE_GROUP_LANES, 0)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
     netcsum.tune(netcsum.TUNE_KERNEL, 0)
+    netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, -1)
     yield
+    netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, -1)
     netcsum.tune(netcsum.TUNE_GROUP_LANES, 0)
     netcsum.tune(netcsum.TUNE_GRID_BLOCKS, 0)
     netcsum.tune(netcsum.TUNE_KERNEL, 0)
@@ -56,17 +58,19 @@ def _want(cb, op):
 
 # pass 1 of each TUNE_KERNEL value (0: the default)
 PASS1 = {0: "seg_live_varlen_kernel", 1: "chain_wave_kernel", 3: "chain_live_piece_kernel", 4: "chain_piece_kernel",
-         5: "seg_live_varlen_kernel"}
+         5: "seg_live_varlen_kernel", 6: "seg_live_varlen_kernel"}
 
 
-@pytest.mark.parametrize("group", [0, 1, 3, 4, 5, 16, 32, 64])  # 1-5: TUNE_KERNEL, 16-64: TUNE_GROUP_LANES
+@pytest.mark.parametrize("group", [0, 1, 3, 4, 5, 6, 16, 32, 64])  # 1-5: TUNE_KERNEL, 6: 5 with 64-lane combine,
+#                                                                    16-64: TUNE_GROUP_LANES
 @pytest.mark.parametrize("pseudo_len", [0, 12, 13, 40])
 @pytest.mark.parametrize("op", [0, 1])
 def test_chain_batch_matches_oracle(group, pseudo_len, op):
     rng = random.Random(group * 131 + pseudo_len * 3 + op)
     cb = make_chain_batch(rng, 1500, pseudo_len=pseudo_len, self_verify=0.5 if op else 0.0)
-    if group <= 5:
-        netcsum.tune(netcsum.TUNE_KERNEL, group)
+    netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, 64 if group == 6 else -1)
+    if group <= 6:
+        netcsum.tune(netcsum.TUNE_KERNEL, 5 if group == 6 else group)
     else:
         netcsum.tune(netcsum.TUNE_GROUP_LANES, group)
     got, want = _gpu(cb, op), _want(cb, op)
@@ -202,14 +206,15 @@ def test_chain_batch_fragments_live_runs(order, spw, form):
         netcsum.tune(netcsum.TUNE_LIVE_COMPACT, -1)
 
 
-@pytest.mark.parametrize("kernel", [0, 4, 1])
+@pytest.mark.parametrize("kernel,cl", [(0, -1), (0, 64), (4, -1), (1, -1)])
 @pytest.mark.parametrize("pseudo_len", [0, 12, 13])
-def test_chain_batch_mod65535_boundaries(kernel, pseudo_len):
+def test_chain_batch_mod65535_boundaries(kernel, cl, pseudo_len):
     """The one-record form's arithmetic at its edges: all-0xFF chains of 131 050 - 131 100 stream
     bytes (the modulo-65535 form up to 131 072, the exact re-read past it, the reference's u32
     accumulator at 2^32 - 1 and wrapping beyond), all-zero chains (T = 0: Calc 0xFFFF), chains whose
     sum is a positive multiple of 65535 (Calc 0), odd pieces at odd addresses; against the oracle."""
     netcsum.tune(netcsum.TUNE_KERNEL, kernel)
+    netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, cl)
     rng = np.random.default_rng(pseudo_len + 3)
     chains = []                                                   # (bytes value, [piece lengths])
     for total in range(131050, 131101, 3):
@@ -257,6 +262,7 @@ def test_chain_batch_mod65535_boundaries(kernel, pseudo_len):
         assert bad.size == 0, (op, [(int(i), int(got[i]), int(want[i])) for i in bad[:5]])
         if op == 0 and pseudo_len == 0:
             assert int(got[-4]) == 0xFFFF - 0 and all(int(g) == 0 for g in got[-3:])   # T = 0 / multiples
+    netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, -1)
 
 
 def test_chain_batch_matches_single_segment_batch():
@@ -281,6 +287,7 @@ def test_chain_pass1_tile_order(xcd, cg, touch):
     options, as are chunked tile orders and the row touch of a group's first pieces
     (NETCSUM_TUNE_STREAM_TOUCH): the same records, the oracle's results, for piece counts that fill the
     tiles unevenly over the 8 XCDs."""
+    netcsum.tune(netcsum.TUNE_KERNEL, 4)                           # the tiled pass 1
     try:
         netcsum.tune(netcsum.TUNE_STREAM_XCD, xcd)
         netcsum.tune(netcsum.TUNE_CHAIN_GRID, cg)
@@ -288,6 +295,7 @@ def test_chain_pass1_tile_order(xcd, cg, touch):
         for n_chains, seed in ((1, 1), (37, 2), (700, 3), (3000, 4)):
             cb = make_chain_batch(random.Random(seed), n_chains, 12)
             assert np.array_equal(_gpu(cb, 0), _want(cb, 0))
+            assert netcsum.last_launch().startswith("chain_piece_kernel")
     finally:
         netcsum.tune(netcsum.TUNE_STREAM_XCD, -1)
         netcsum.tune(netcsum.TUNE_CHAIN_GRID, -1)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, session U: chain pass 1 as the segment live-sector stream with one record per piece
+# Round 6, sessions U / X: chain pass 1 as the segment live-sector stream with one record per piece
 # (default, TUNE_KERNEL 5) against the tiled groups (.k4): runs (.sN), depth (.dN), compacted or not (.lcN).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd "$R"
@@ -9,7 +9,7 @@ O=$R/gpurun_out; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_chains.py -x -q --timeout 120 --timeout-method thread \
   -p no:cacheprovider > $O/${T}_tests.log 2>&1 || { tail -30 $O/${T}_tests.log; exit 1; }
 tail -1 $O/${T}_tests.log
-for c in ${CONFIGS:-chains chains.k4 chains.lc0 chains.s8 chains.s8.d4 chains.s32 chains.lc0.s8.d4 chains chains.k4 chains.lc0 chains.s8 chains.s8.d4}; do
+for c in ${CONFIGS:-chains chains.cc64 chains.s16 chains chains.cc64 chains.s16 chains.k4}; do
   echo "== $c" >> $O/${T}_runs.log
   timeout -k 10 120 python tools/run_config.py $c 60 >> $O/${T}_runs.log 2>&1 || { tail $O/${T}_runs.log; exit 1; }
 done

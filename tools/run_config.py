@@ -19,7 +19,8 @@ box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   suffix .bN = NETCSUM_TUNE_PKT_BOUND N, .sN = packets per wave run, .ntN = NETCSUM_TUNE_NT_LOADS N,
   .kN = NETCSUM_TUNE_KERNEL N (chains.k3 / .k4: pass 1 in round 5's live form / tiled groups), .dN = NETCSUM_TUNE_CHUNKS N,
   .xN = NETCSUM_TUNE_STREAM_XCD N, .gN = NETCSUM_TUNE_STORE_GATHER N, .wN = NETCSUM_TUNE_STREAM_WAVES N,
-  .cgN = NETCSUM_TUNE_CHAIN_GRID N, .tN = NETCSUM_TUNE_STREAM_TOUCH N, .lcN = NETCSUM_TUNE_LIVE_COMPACT N
+  .cgN = NETCSUM_TUNE_CHAIN_GRID N, .tN = NETCSUM_TUNE_STREAM_TOUCH N, .lcN = NETCSUM_TUNE_LIVE_COMPACT N,
+  .ccN = NETCSUM_TUNE_CHAIN_COMBINE N
   (e.g. rx_ring.b0.s32, rx_nb2k.nt0)
   chains  16 Ki NET_BUF chains of 45 fragments (64 KiB UDP datagrams, each fragment in its own
        2 KiB buffer at +42), DataCalc
@@ -47,6 +48,9 @@ def main():
     for part in name.split(".")[1:]:
         if part.startswith("nt"):
             netcsum.tune(netcsum.TUNE_NT_LOADS, int(part[2:]))
+            continue
+        if part[:2] == "cc":
+            netcsum.tune(netcsum.TUNE_CHAIN_COMBINE, int(part[2:]))
             continue
         if part[:2] == "lc":
             netcsum.tune(netcsum.TUNE_LIVE_COMPACT, int(part[2:]))

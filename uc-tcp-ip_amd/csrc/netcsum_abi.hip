@@ -29,6 +29,7 @@ thread_local netcsum::TuneKnob g_tune_grid{0};
 thread_local netcsum::TuneKnob g_tune_group{0};
 thread_local netcsum::TuneKnob g_tune_nt{-1};                   // -1: auto (nt when groups share no chunks)
 thread_local netcsum::TuneKnob g_tune_block{256};
+thread_local netcsum::TuneKnob g_tune_chain_combine{-1};         // NETCSUM_TUNE_CHAIN_COMBINE
 thread_local netcsum::TuneKnob g_tune_kernel{0};                 // 0 = auto (5 when small_supported, else 2)
 thread_local netcsum::TuneKnob g_tune_chunks{0};
 thread_local netcsum::TuneKnob g_tune_probe{1};                 // LDS-DMA read probe by default
@@ -1408,16 +1409,19 @@ NET_ERR NetUtil_MI355X_ChkSumBatchChains(const void* d_base, const uint64_t* d_p
             // Default / TUNE_KERNEL 5 (round 6): the segment live-sector stream with ONE wave total per piece
             // end, the piece's half-word sum, combined modulo 65535 (chain_combine_h_kernel)
             const int tk = g_tune_tile.load(), ch = g_tune_chunks.load();
-            const uint32_t live = (kern != 3 && !one_rec) ? 0u : (tk >= 1 && tk <= 64) ? (uint32_t)tk : 16u;
+            // runs: TUNE_TILE, else 16 pieces (round 5's live form) / 12 (the one-record form: 0.1686-0.1691
+            // ms on the chain row against 0.1709-0.1715 for 16, profiles/r6v_*, r6w_*)
+            const uint32_t live = (kern != 3 && !one_rec) ? 0u : (tk >= 1 && tk <= 64) ? (uint32_t)tk : one_rec ? 12u : 16u;
             const int depth = ch == 4 ? 4 : 8;
             char d[128];
             if (one_rec) {
                 const bool cmp = netcsum::live_compact();
-                snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d,chain,nt%s> pieces_per_wave=%u +chain_combine_h_kernel",
-                         depth, cmp ? ",compact" : "", live);
+                const int cl = g_tune_chain_combine.load() == 64 ? 64 : 16;
+                snprintf(d, sizeof d, "seg_live_varlen_kernel<D=%d,chain,nt%s> pieces_per_wave=%u +chain_combine_h_kernel<%d>",
+                         depth, cmp ? ",compact" : "", live, cl);
                 netcsum::set_last_launch(d);
                 NC_HIP(netcsum::launch_chain_two_pass_h(a, static_cast<uint32_t*>(scratch.ptr()), (uint32_t)cap, cu_count(dev),
-                                                        static_cast<hipStream_t>(hip_stream), live, depth, cmp));
+                                                        static_cast<hipStream_t>(hip_stream), live, depth, cmp, cl));
                 NC_HIP(scratch.end());
                 return NET_UTIL_ERR_NONE;
             }
@@ -2353,6 +2357,10 @@ NET_ERR NetUtil_MI355X_Tune(int key, int value) {
     case NETCSUM_TUNE_CHAIN_GRID:
         if (value < -1 || value > 16) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
         netcsum::set_chain_grid(value);
+        return NET_UTIL_ERR_NONE;
+    case NETCSUM_TUNE_CHAIN_COMBINE:
+        if (value != -1 && value != 16 && value != 64) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;
+        g_tune_chain_combine.store(value);
         return NET_UTIL_ERR_NONE;
     case NETCSUM_TUNE_LIVE_COMPACT:
         if (value < -1 || value > 1) return (NET_ERR)NET_UTIL_ERR_MI355X_INVALID_ARG;

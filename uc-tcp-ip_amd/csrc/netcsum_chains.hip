@@ -752,6 +752,10 @@ __device__ __forceinline__ uint32_t fold64(uint64_t s) {
     return (uint32_t)s;
 }
 
+// A CG-lane group per chain (CG 16: 4 chains per wave, 16 pieces per step; CG 64: a wave per chain,
+// 64 pieces per step — a 45-fragment datagram in one step, one dependent memory round trip after the
+// chain's bounds).
+template <int CG>
 __global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, const uint32_t* hr, uint32_t cap) {
     const uint32_t np = *reinterpret_cast<c_u32*>(reinterpret_cast<uintptr_t>(A.first + A.n));
     if (np > cap) {                                               // pass 1 had no room for the records:
@@ -761,15 +765,16 @@ __global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, 
         }
         return;
     }
-    const int lane = (int)(threadIdx.x & (kCG - 1));
-    const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(kCG - 1);          // the group's ballot bits
-    const uint32_t below = (1u << lane) - 1u;
-    const uint32_t ngr = gridDim.x * (256u / kCG);
-    const uint32_t c0 = blockIdx.x * (256u / kCG) + (threadIdx.x & ~63u) / kCG;
+    const int lane = (int)(threadIdx.x & (CG - 1));
+    const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(CG - 1);          // the group's ballot bits
+    const uint64_t gmask = CG == 64 ? ~0ull : ((1ull << CG) - 1u);
+    const uint64_t below = (1ull << lane) - 1u;
+    const uint32_t ngr = gridDim.x * (256u / CG);
+    const uint32_t c0 = blockIdx.x * (256u / CG) + (threadIdx.x & ~63u) / CG;
     const uint32_t rounds = c0 < A.n ? (A.n - c0 + ngr - 1u) / ngr : 0u;
     const uintptr_t base = (uintptr_t)A.base;
     for (uint32_t r = 0u; r < rounds; ++r) {
-        const uint32_t ch = c0 + r * ngr + (threadIdx.x & 63u) / kCG;
+        const uint32_t ch = c0 + r * ngr + (threadIdx.x & 63u) / CG;
         const bool live = ch < A.n;
         const uint32_t p0 = live ? A.first[ch] : 0u;
         const uint32_t p1 = live ? A.first[ch + 1u] : 0u;
@@ -782,48 +787,48 @@ __global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, 
                 plen -= 1u;                                       // NULL chain quirk
             }
             pa = (uintptr_t)A.pseudo + (uint64_t)ch * A.pseudo_stride;
-            const EO s = span_eo<kCG>(pa, plen, lane);
+            const EO s = span_eo<CG>(pa, plen, lane);
             S += (pa & 1u) ? ((uint64_t)s.o << 8) + s.e : ((uint64_t)s.e << 8) + s.o;
             par = A.pseudo_len & 1u;                              // pieces follow ALL pseudo bytes
         }
         const uint32_t par0 = par;
-        uint32_t steps = (p1 - p0 + kCG - 1u) / kCG;
+        uint32_t steps = (p1 - p0 + CG - 1u) / CG;
 #pragma unroll
-        for (int m = 32; m >= kCG; m >>= 1) {                     // the wave's longest chain
+        for (int m = 32; m >= CG; m >>= 1) {                      // the wave's longest chain
             steps = max(steps, (uint32_t)__shfl_xor((int)steps, m, 64));
         }
         for (uint32_t t = 0u; t < steps; ++t) {
-            const uint32_t j = p0 + t * kCG + (uint32_t)lane;
+            const uint32_t j = p0 + t * CG + (uint32_t)lane;
             const bool v = j < p1;
             const uint32_t len = v ? (uint32_t)A.len[j] : 0u;
             const uint64_t off = v ? A.off[j] : 0u;
             const uint64_t h = v ? hr[j] : 0u;
-            const uint32_t odd = (uint32_t)(__ballot((len & 1u) != 0u) >> sh) & 0xFFFFu;
-            const uint32_t spar = par ^ ((uint32_t)__popc(odd & below) & 1u);
+            const uint64_t odd = (__ballot((len & 1u) != 0u) >> sh) & gmask;
+            const uint32_t spar = par ^ ((uint32_t)__popcll(odd & below) & 1u);
             const uint32_t swap = ((uint32_t)(base + off) & 1u) ^ spar;
             S += swap ? h : h << 8;
             L += len;
-            par ^= (uint32_t)__popc(odd) & 1u;
+            par ^= (uint32_t)__popcll(odd) & 1u;
         }
-        S = group_sum64<kCG>(S);
-        L = group_sum64<kCG>(L);
+        S = group_sum64<CG>(S);
+        L = group_sum64<CG>(L);
         const bool big = live && L + plen > kChainModMax;         // group-uniform
         if (big) {                                                // the exact form (u32 wrap included)
             uint64_t E = 0u, O = 0u;
             if (plen != 0u) {
-                const EO s = span_eo<kCG>(pa, plen, lane);
+                const EO s = span_eo<CG>(pa, plen, lane);
                 if (pa & 1u) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
             }
             uint32_t spos = par0;
             for (uint32_t j = p0; j < p1; ++j) {
                 const uintptr_t a = base + A.off[j];
                 const uint32_t len = A.len[j];
-                const EO s = span_eo<kCG>(a, len, lane);
+                const EO s = span_eo<CG>(a, len, lane);
                 if (((uint32_t)(a & 1u)) != spos) { E += s.o; O += s.e; } else { E += s.e; O += s.o; }
                 spos ^= (len & 1u);
             }
-            E = group_sum64<kCG>(E);
-            O = group_sum64<kCG>(O);
+            E = group_sum64<CG>(E);
+            O = group_sum64<CG>(O);
             if (lane == 0) {
                 chain_out(A, ch, E, O);
             }
@@ -842,12 +847,17 @@ __global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, 
 }  // namespace
 
 hipError_t launch_chain_two_pass_h(const ChainBatchArgs& a, uint32_t* rec, uint32_t cap, int cus, hipStream_t s,
-                                   uint32_t spw, int depth, bool cmp) {
+                                   uint32_t spw, int depth, bool cmp, int combine_lanes) {
     hipError_t e = launch_chain_live_records(a, rec, cap, depth, spw, cmp, s);
     if (e != hipSuccess) return e;
-    const uint64_t blocks = ((uint64_t)a.n + 15u) / 16u;
+    const uint32_t cg = combine_lanes == 64 ? 64u : 16u;
+    const uint64_t blocks = ((uint64_t)a.n + 256u / cg - 1u) / (256u / cg);
     const unsigned g2 = (unsigned)std::min<uint64_t>(blocks, (uint64_t)std::max(cus, 1) * 64u);
-    hipLaunchKernelGGL(chain_combine_h_kernel, dim3(g2), dim3(256), 0, s, a, (const uint32_t*)rec, cap);
+    if (cg == 64u) {
+        hipLaunchKernelGGL(chain_combine_h_kernel<64>, dim3(g2), dim3(256), 0, s, a, (const uint32_t*)rec, cap);
+    } else {
+        hipLaunchKernelGGL(chain_combine_h_kernel<16>, dim3(g2), dim3(256), 0, s, a, (const uint32_t*)rec, cap);
+    }
     return hipGetLastError();
 }
 

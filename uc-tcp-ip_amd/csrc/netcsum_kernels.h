@@ -147,8 +147,9 @@ hipError_t launch_chain_two_pass(const ChainBatchArgs& a, uint64_t* eo, uint32_t
 // those records (chain_combine_h_kernel, netcsum_chains.hip); the two together:
 hipError_t launch_chain_live_records(const ChainBatchArgs& c, uint32_t* rec, uint32_t cap, int depth, uint32_t spw, bool cmp,
                                      hipStream_t s);
+// combine_lanes: 16 or 64 lanes per chain in the combine pass
 hipError_t launch_chain_two_pass_h(const ChainBatchArgs& a, uint32_t* rec, uint32_t cap, int cus, hipStream_t s,
-                                   uint32_t spw, int depth, bool cmp);
+                                   uint32_t spw, int depth, bool cmp, int combine_lanes);
 
 // CRC-32 batches (netcsum_crc.hip; net_util.c:485-636).
 struct CrcBatchArgs {

@@ -77,6 +77,7 @@ TUNE_PLAN_AHEAD = 26            # first batch on a layout: sample it first and r
 TUNE_LIVE_COMPACT = 27          # live-sector streams: live sectors compacted (-1 default / 1) or live pieces (0)
 TUNE_STORE_GATHER = 28          # dense segment stream: a block's results stored as whole lines (-1 / 1) or per wave (0)
 TUNE_CHAIN_GRID = 29            # chain pass 1: tiles of 64 pieces per block (-1 / 0) or k x resident blocks, equal shares
+TUNE_CHAIN_COMBINE = 30         # chain combine pass of the one-record form: 16 or 64 lanes per chain (-1 default)
 
 
 # --------------------------------------------------------------------------- NET_BUF mirror
