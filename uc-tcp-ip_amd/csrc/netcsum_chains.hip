@@ -797,18 +797,29 @@ __global__ void __launch_bounds__(256) chain_combine_h_kernel(ChainBatchArgs A, 
         for (int m = 32; m >= CG; m >>= 1) {                      // the wave's longest chain
             steps = max(steps, (uint32_t)__shfl_xor((int)steps, m, 64));
         }
-        for (uint32_t t = 0u; t < steps; ++t) {
-            const uint32_t j = p0 + t * CG + (uint32_t)lane;
-            const bool v = j < p1;
-            const uint32_t len = v ? (uint32_t)A.len[j] : 0u;
-            const uint64_t off = v ? A.off[j] : 0u;
-            const uint64_t h = v ? hr[j] : 0u;
-            const uint64_t odd = (__ballot((len & 1u) != 0u) >> sh) & gmask;
-            const uint32_t spar = par ^ ((uint32_t)__popcll(odd & below) & 1u);
-            const uint32_t swap = ((uint32_t)(base + off) & 1u) ^ spar;
-            S += swap ? h : h << 8;
-            L += len;
-            par ^= (uint32_t)__popcll(odd) & 1u;
+        // U steps' descriptors and records loaded before any is used: one memory round trip for a
+        // chain of up to U x CG pieces after its bounds (a 45-fragment datagram: one)
+        constexpr uint32_t U = 4u;
+        for (uint32_t t0 = 0u; t0 < steps; t0 += U) {
+            uint32_t len[U];
+            uint64_t off[U], h[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = p0 + (t0 + u) * CG + (uint32_t)lane;
+                const bool v = t0 + u < steps && j < p1;
+                len[u] = v ? (uint32_t)A.len[j] : 0u;
+                off[u] = v ? A.off[j] : 0u;
+                h[u] = v ? hr[j] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint64_t odd = (__ballot((len[u] & 1u) != 0u) >> sh) & gmask;
+                const uint32_t spar = par ^ ((uint32_t)__popcll(odd & below) & 1u);
+                const uint32_t swap = ((uint32_t)(base + off[u]) & 1u) ^ spar;
+                S += swap ? h[u] : h[u] << 8;
+                L += len[u];
+                par ^= (uint32_t)__popcll(odd) & 1u;
+            }
         }
         S = group_sum64<CG>(S);
         L = group_sum64<CG>(L);
