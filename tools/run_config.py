@@ -2,6 +2,7 @@
 """Run ONE BASELINE config's default launch N times (for rocprofv3 kernel-trace / --pmc passes; GPU
 box only). Usage: python tools/run_config.py <c2|c3|c4|c5|rx|tx|tx2> [reps]
   c2  1 M x 1500 B + 12-B pseudo, DataCalc       c3  16 M x 20-B IPv4 headers, HdrCalc
+  c2np  C2 without pseudo-headers (diagnostic)
   c4  1 M packed UDP 40-9000 B + pseudo          c5  16 M x 1500 B + pseudo (one GPU's shard)
   rx / tx  fused Rx / Tx finalize, 1 M x 1500-B IPv4/TCP, strided; tx2 = two-pass Tx
   rx6 / rxmix  fused Rx of the same datagrams as IPv6/TCP / alternating IPv4 and IPv6 (bench_configs)
@@ -93,14 +94,16 @@ def main():
         else:
             fn = lambda: netcsum.rx_validate_ipv4(base, n, flags, stream=st, **kw)  # noqa: E731
             algo = r["datagram_bytes"] + n
-    elif name in ("c2", "c5"):
-        n, L = (1 << 20) if name == "c2" else (1 << 24), 1500
+    elif name in ("c2", "c5", "c2np"):
+        # c2np: C2 without its pseudo-header stream (a diagnostic, not a BASELINE config)
+        n, L = (1 << 24) if name == "c5" else (1 << 20), 1500
         seg = torch.empty(n * L + 256, dtype=torch.uint8, device=dev)
         netcsum.fill(seg, n * L, SEED, 0)
-        ph = torch.from_numpy(c2_pseudo_headers(0, n, L, 12)).to(dev)
+        ph = torch.from_numpy(c2_pseudo_headers(0, n, L, 12)).to(dev) if name != "c2np" else None
+        pl = 0 if ph is None else 12
         out = torch.empty(n, dtype=torch.int16, device=dev)
-        fn = lambda: netcsum.batch_strided(seg, L, L, ph, 12, 12, n, out, 0, stream=st)  # noqa: E731
-        algo = n * (L + 12 + 2)
+        fn = lambda: netcsum.batch_strided(seg, L, L, ph, pl, pl, n, out, 0, stream=st)  # noqa: E731
+        algo = n * (L + pl + 2)
     elif name == "c3":
         n, L = 1 << 24, 20
         hdr = torch.empty(n * L, dtype=torch.uint8, device=dev)
