@@ -454,6 +454,26 @@ def test_stream_kernel_full_c2_equals_pipe_kernel():
     assert bool(ok.all())
 
 
+@pytest.mark.parametrize("L,run", [(1024, 20), (2048, 10), (4096, 5), (8192, 3), (9000, 2), (1500, 16),
+                                   (1460, 16), (16384, 1)])
+def test_dense_run_length_by_bytes(L, run):
+    """Dense strided batches take runs of 16 segments unless that run's bytes are a multiple of 16 KiB
+    or past 48 KiB; then runs of about 20 KiB that are not (profiles/r6zq_seglen.jsonl). Batches big
+    enough that the small-batch halving leaves the run alone, every result against the oracle, odd and
+    even bases."""
+    rng = np.random.default_rng(L)
+    n = max(2048 * run, 4096)
+    data = _host_bytes(rng, n * L + 64, "random")
+    ph = _host_bytes(rng, n * 12 + 64, "random")
+    data_d, ph_d = torch.from_numpy(data).to(DEV), torch.from_numpy(ph).to(DEV)
+    for base_off in (0, 1):
+        got = _gpu_strided(data_d, base_off, L, L, ph_d, 12, 12, n, 0)
+        ll = netcsum.last_launch()
+        assert ll.startswith("seg_stream_kernel") and ll.endswith(f"segs_per_wave={run}"), ll
+        want = oracle.batch_strided(data, L, L, ph, 12, 12, n, 0, seg_offset=base_off)
+        assert np.array_equal(got, want), (L, base_off)
+
+
 @pytest.mark.parametrize("touch", [0, 1])
 @pytest.mark.parametrize("waves", [0, 3, 5, 8])
 @pytest.mark.parametrize("xcd", [0, 1, 3, 16])

@@ -221,6 +221,18 @@ netcsum::LaunchCfg choose_cfg(int dev, const netcsum::SegBatchArgs& a, uint32_t 
                 // runs of 8 (r2ct) with VARLEN_RUN_BYTES 0
                 c.run_bytes = varlen ? netcsum::varlen_run_bytes() : 0u;
                 uint64_t run = !varlen ? 16u : c.run_bytes ? netcsum::kVarlenSpwMin : 8u;
+                if (!varlen) {
+                    // a run whose bytes are a multiple of 16 KiB (16 x 1 / 2 / 4 / 8 KiB segments) or
+                    // past 48 KiB (9000-B jumbo frames) runs at 79-87 % of spec against 90-91 % for
+                    // runs of about 20 KiB that are not (profiles/r6zq_seglen.jsonl: 1024 B x 16
+                    // 0.2397 ms, x 20 0.2091; 4096 x 16 0.2183, x 5 0.2069; 9000 x 16 0.2359, x 2
+                    // 0.2071); C2's 16 x 1500 B stays
+                    const uint64_t st = a.seg_stride ? a.seg_stride : a.seg_len;
+                    if ((16u * st) % 16384u == 0u || 16u * st > 49152u) {
+                        run = std::max<uint64_t>(1u, (20480u + st / 2u) / st);
+                        if ((run * st) % 16384u == 0u && st % 16384u != 0u) run += 1u;
+                    }
+                }
                 if (!varlen) {                         // small batches: latency-bound runs halve until
                     while (run > 1u && (uint64_t)a.n_seg < 2048u * run) run >>= 1;   // >= 2048 waves
                 }                                      // (as the packet batches, pkt_batch)
