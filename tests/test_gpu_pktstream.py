@@ -327,11 +327,14 @@ def test_pkt_stream_v6_c2_shape_round_trip_1M():
 
 
 @pytest.mark.parametrize("stride,pkt_len,run", [(1500, 1500, 8), (1000, 1000, 16), (577, 577, 32), (256, 200, 64),
-                                                (128, 128, 64), (9000, 9000, 8), (1520, 1506, 16), (2048, 1984, 8)])
+                                                (128, 128, 64), (9000, 9000, 1), (2048, 2048, 5), (4096, 4096, 2),
+                                                (8192, 8192, 1), (3000, 3000, 8), (1520, 1506, 16), (2048, 1984, 8)])
 @pytest.mark.parametrize("copies", [1, 1000])
 def test_pkt_stream_default_run_length_by_bytes(stride, pkt_len, run, copies):
     """Default run: about 20 KB of datagrams per wave for packed batches (the whole-span form 0, r2zq sweep) and
-    24 KB of slots for the live-piece form 2 of other layouts (r4m ring probe), in multiples of 8, 8..64, halved while
+    24 KB of slots for the live-piece form 2 of other layouts (r4m ring probe), in multiples of 8, 8..64 — except
+    packed runs whose bytes would be a multiple of 16 KiB or past 48 KiB, which take about 10 KiB (round 6,
+    profiles/r6zu_pktlen.jsonl: 2 / 4 / 8 KiB and 9000-B datagrams in runs of 5 / 2 / 1 / 1) —, halved while
     the batch has fewer than 2048 runs (small bursts are latency-bound); results equal the lane-group kernel's.
     copies: the 300-datagram batch repeated (300 000 datagrams keep the full run). Layouts that are not
     packed run with TUNE_PKT_BOUND 2 here: by default their batches of >= 16 Ki datagrams take ring plans
